@@ -1,0 +1,203 @@
+/*
+ * kme.h -- C ABI of the MI355X-native matching core (drop-in for the KProcessor matching path).
+ *
+ * The reference runs one `MatchingEngine implements Processor<String, Order>` per stream task
+ * (/root/reference/src/main/java/KProcessor.java:52, 63-445; "KP" below) that handles ONE record
+ * per process() call against five RocksDB stores.  This ABI is what that processor's JNI / Panama
+ * FFM binding calls instead: the Java side buffers records into an epoch and hands
+ * the epoch over as structure-of-arrays; the engine returns, per input, exactly what the reference
+ * would have forwarded ("IN" echo, maker/taker fills, "OUT" echo: KP:97, 124, 272-273).
+ *
+ * Plain C: integers, pointers and sizes only.  All functions return a kme_status (0 = OK).
+ * One submitting thread per handle (the reference's process() is never concurrent either).
+ */
+#ifndef KME_H
+#define KME_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KME_ABI_VERSION 1
+
+/* Order.action codes (KP:65-75). */
+enum kme_action {
+    KME_ADD_SYMBOL = 0, KME_REMOVE_SYMBOL = 1, KME_BUY = 2, KME_SELL = 3, KME_CANCEL = 4,
+    KME_BOUGHT = 5, KME_SOLD = 6, KME_REJECT = 7,
+    KME_CREATE_BALANCE = 100, KME_TRANSFER = 101, KME_PAYOUT = 200
+};
+
+typedef enum kme_status {
+    KME_OK = 0,
+    KME_E_INVALID = 1,      /* bad argument / handle */
+    KME_E_CAPACITY = 2,     /* epoch, order pool, oid table, trade buffer or symbol capacity exceeded */
+    KME_E_DOMAIN = 3,       /* input where the reference throws (NPE) or never terminates, or that
+                               falls outside the documented parity domain (detail: kme_domain) */
+    KME_E_UNFUNDED = 4,     /* FUNDED mode: acceptance of some order is not provably
+                               independent of the ledger (see kme_mode) */
+    KME_E_UNSUPPORTED = 5,  /* operation not available in this mode (PAYOUT of an absent symbol in
+                               FUNDED mode needs the positions ledger) */
+    KME_E_HIP = 6,          /* HIP runtime error */
+    KME_E_FAILED = 7        /* engine already failed; like the reference's dead stream thread,
+                               it accepts nothing further */
+} kme_status;
+
+/* Detail for KME_E_DOMAIN / KME_E_CAPACITY (kme_epoch_status.detail). */
+enum kme_domain {
+    KME_D_NONE = 0,
+    KME_D_NPE_POSITION = 1,  /* position null with adj != 0 (KP:179-180, 332): negative sizes */
+    KME_D_NPE_BUCKET = 2,    /* log10 bit scan points at an empty level (KP:234-235, 252-253; H5) */
+    KME_D_NPE_ORDER = 3,     /* missing order node (KP:236-237, 257) */
+    KME_D_NPE_BALANCE = 4,   /* balance null (KP:157, 286, 331) */
+    KME_D_HANG = 5,          /* removeAllOrders on a non-empty book never returns (KP:341-353) */
+    KME_D_NPE_BOOK = 6,      /* book missing for a resting order (KP:294) */
+    KME_D_PRICE = 7,         /* a resting price outside 0..126 aliases buckets across symbols (KP:379-416) */
+    KME_D_DUP_OID = 8,       /* BUY/SELL reuses the oid of a live order (KP:221 would corrupt lists) */
+    KME_D_FUNDED_RANGE = 9,  /* FUNDED mode: BUY/SELL price outside 0..100 or size < 0 */
+    KME_D_SENTINEL_OID = 10, /* oid equal to the reserved table sentinels (Long.MIN_VALUE, MIN_VALUE+1) */
+    KME_D_CAP_POOL = 11, KME_D_CAP_OIDTAB = 12, KME_D_CAP_TRADES = 13, KME_D_CAP_SYMBOL = 14,
+    KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17
+};
+
+/* Engine modes.
+ * EXACT : every store of the reference (Books, Buckets, Orders, Balances, Positions, KP:30-49) is
+ *         kept bit-exactly on the device, including the value-keyed position writes (KP:434-436).
+ *         One wavefront applies the epoch in arrival order (the ledger couples all symbols).
+ * FUNDED: symbol groups are matched in parallel, one wavefront per group.  Legal only while every
+ *         BUY/SELL provably passes checkBalance (KP:167-182) -- the engine verifies this per epoch
+ *         with a conservative per-account reservation bound and fails with KME_E_UNFUNDED
+ *         otherwise.  Tape and book state are bit-exact; the ledger keeps account existence and
+ *         the reservation bound only (exact balances/positions: EXACT mode). */
+enum kme_mode { KME_MODE_EXACT = 0, KME_MODE_FUNDED = 1 };
+
+typedef struct kme_config {
+    uint32_t abi_version;      /* KME_ABI_VERSION */
+    uint32_t mode;             /* kme_mode */
+    uint32_t max_symbols;      /* symbol groups: |sid| < max_symbols (books +sid and -sid, KP:184-191) */
+    uint32_t max_accounts;     /* FUNDED: account ids 0 <= aid < max_accounts */
+    uint32_t max_epoch;        /* max records per submitted epoch */
+    uint32_t max_trades;       /* max trades per epoch (each trade = 2 fill records) */
+    uint64_t max_resting;      /* order-node pool capacity (resting orders, the Orders store) */
+    uint64_t ledger_capacity;  /* EXACT: hash capacity of Balances and of Positions */
+    int32_t device;            /* HIP device ordinal */
+    uint32_t flags;            /* reserved, 0 */
+} kme_config;
+
+/* One epoch of input records, structure-of-arrays (Order fields KP:451-456).  The reference's
+ * optional next/prev input fields must be null and are not carried. */
+typedef struct kme_orders {
+    const int32_t* action;
+    const int64_t* oid;
+    const int64_t* aid;
+    const int64_t* sid;
+    const int32_t* price;
+    const int32_t* size;
+} kme_orders;
+
+/* One trade = the reference's two fill records (executeTrade, KP:265-274):
+ *   maker fill  {taker BUY ? SOLD : BOUGHT, maker_oid, maker_aid, maker_sid, price 0, size}
+ *   taker fill  {taker BUY ? BOUGHT : SOLD, taker oid, aid, sid, taker.price - maker_price, size} */
+typedef struct kme_trade {
+    int64_t maker_oid, maker_aid, maker_sid;
+    int32_t maker_price, size;
+} kme_trade; /* 32 bytes */
+
+/* Per-epoch results.  For input i the reference forwards, in order:
+ *   IN  = input i unchanged;
+ *   for t in [trade_off[i], trade_off[i+1]): maker fill, taker fill of trades[t];
+ *   OUT = input i with action = out_action[i], size = out_size[i],
+ *         prev = (out_flags[i] & KME_OUT_HAS_PREV) ? out_prev[i] : null, next = null. */
+#define KME_OUT_HAS_PREV 1u
+typedef struct kme_epoch_result {
+    int32_t* out_action;   /* [n] */
+    int32_t* out_size;     /* [n] */
+    int64_t* out_prev;     /* [n] */
+    uint8_t* out_flags;    /* [n] */
+    uint32_t* trade_off;   /* [n + 1] exclusive prefix sum of per-input trade counts */
+    kme_trade* trades;     /* [trades_cap] */
+    uint32_t trades_cap;
+} kme_epoch_result;
+
+typedef struct kme_epoch_status {
+    int32_t status;        /* kme_status of the epoch */
+    int32_t detail;        /* kme_domain */
+    int64_t error_index;   /* input index of the first fault, or -1 */
+    uint32_t n_inputs;
+    uint32_t n_trades;
+    uint64_t n_orders;     /* BUY/SELL/CANCEL records (headline metric unit) */
+    uint64_t n_rests, n_maker_visits, n_cancel_ok;
+} kme_epoch_status;
+
+typedef struct kme_engine kme_engine;
+
+/* Creates the stores (KP:30-49) in HBM and binds them (MatchingEngine.init, KP:86-93). */
+kme_status kme_create(const kme_config* cfg, kme_engine** out);
+/* MatchingEngine.close (KP:129): frees device memory. */
+kme_status kme_destroy(kme_engine* e);
+
+/* Use this HIP stream (hipStream_t) for all device work; NULL = the engine's own stream. */
+kme_status kme_set_stream(kme_engine* e, void* hip_stream);
+
+/* MatchingEngine.process (KP:96-126) for n records, HOST buffers, synchronous.  In FUNDED mode the
+ * epoch is split at account records (CREATE_BALANCE / TRANSFER) so that the reservation bound is
+ * checked per run; the result arrays are filled as one epoch. */
+kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n,
+                            kme_epoch_result* out, kme_epoch_status* st);
+
+/* Same for DEVICE-resident inputs and outputs (pointers into HBM), asynchronous on the engine
+ * stream; completes at kme_wait.  `out` may be NULL to keep results in engine-owned buffers
+ * (see kme_device_results).  No splitting: a FUNDED epoch must not mix account records with
+ * orders of a just-created account (kme_submit_epoch does that split for host callers). */
+kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in_dev, uint32_t n,
+                                   const kme_epoch_result* out_dev);
+kme_status kme_wait(kme_engine* e, kme_epoch_status* st);
+/* Engine-owned device result buffers of the last device epoch. */
+kme_status kme_device_results(kme_engine* e, kme_epoch_result* out_dev);
+
+/* Canonical text snapshots (sorted), identical in format to the reference stores' contents:
+ *   books : "B <key> <msb> <lsb>" (Books), "K <bucketPtr> <firstOid> <lastOid>" (Buckets),
+ *           "O <oid> <action> <aid> <sid> <price> <size> <next|null> <prev|null>" (Orders)
+ *   ledger: "A <aid> <balance>" (Balances), "P <keyMsb> <keyLsb> <amount> <available>" (Positions);
+ *           EXACT mode only (FUNDED: KME_E_UNSUPPORTED).
+ * *text is malloc'd; free with kme_free. */
+kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len);
+kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len);
+void kme_free(void* p);
+
+/* Top-of-book market data per symbol group g (device buffer of max_symbols entries, async):
+ * {best bid price, best ask price, bid qty, ask qty} as int32 (-1 / 0 when a side is empty).
+ * Bid = highest price in book +g, ask = lowest price in book -g (book 0 is shared). */
+typedef struct kme_tob { int32_t bid_px, ask_px, bid_qty, ask_qty; } kme_tob;
+kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out);
+
+/* Wall-clock (HIP event) duration in ms of each kernel phase of the last epoch; index by name
+ * (kme_phase_names).  Used by bench.py for the roofline of the dominant kernel. */
+#define KME_MAX_PHASES 16
+kme_status kme_phase_times(kme_engine* e, float* ms, int* n_phases);
+const char* kme_phase_name(int i);
+kme_status kme_enable_timing(kme_engine* e, int enable);
+
+/* Serialises a processed epoch exactly as consumer.js prints MatchOut (consumer.js:19):
+ * "IN <json>\nOUT <json>\n..." with Jackson's Order layout (KP:488-494).  Host buffers.
+ * Writes at most cap bytes; *len receives the full length (call again with a bigger buffer
+ * if *len > cap). */
+kme_status kme_tape_json(const kme_orders* in, uint32_t n, const kme_epoch_result* res,
+                         char* buf, size_t cap, size_t* len);
+
+/* Jackson JsonDeserializer<Order> (KP:513-520) for one record: numbers or numeric strings,
+ * unknown properties rejected, next/prev must be absent or null. */
+kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, int64_t* oid,
+                               int64_t* aid, int64_t* sid, int32_t* price, int32_t* size);
+
+/* Kafka's default keyed partitioner over decimal(|sid|) (murmur2, toPositive, % n). */
+uint32_t kme_shard_of(int64_t sid, uint32_t n_shards);
+
+const char* kme_strerror(int status);
+const char* kme_domain_str(int detail);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

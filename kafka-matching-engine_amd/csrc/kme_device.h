@@ -1,0 +1,138 @@
+// kme_device.h -- device-side data layout of the matching core (HBM-resident stores).
+//
+// The reference keeps five RocksDB stores (KProcessor.java:30-49).  Here the book stores become
+// structure-of-arrays in HBM, sized for the 288 GB of an MI355X:
+//
+//   GroupState[G]        one per symbol group |sid| (books +sid and -sid, KP:184-191; sid 0 is one
+//                        shared book, H4): existence, two 128-bit level bitmaps (the Books values,
+//                        KP:38-41), the group's node free list and bump chunk.
+//   Level[G][2][128]     one per (book side, price level) = the Buckets store (KP:42-45): FIFO
+//                        head/tail node slots, resting count and quantity, tail oid.
+//   Node[P]              order-node pool = the Orders store (KP:46-49), one 64-byte line per order.
+//   oid table            open-addressing oid -> node slot (lazy deletion: entries are validated
+//                        against the node, stale ones are dropped at rebuild).
+//   ledger               FUNDED: per-account existence + reservation bound; EXACT: Balances and
+//                        Positions as device hash tables (KP:30-37).
+#pragma once
+#include <stdint.h>
+
+namespace kme {
+
+constexpr int NLEV = 128;          // price levels 0..126 (+1 pad)
+constexpr int NACT = 11;
+
+enum Action : int32_t {
+    ADD_SYMBOL = 0, REMOVE_SYMBOL = 1, BUY = 2, SELL = 3, CANCEL = 4, BOUGHT = 5, SOLD = 6,
+    REJECT = 7, CREATE_BALANCE = 100, TRANSFER = 101, PAYOUT = 200
+};
+
+struct alignas(32) Level {         // one bucket (KP:379-389)
+    int32_t head, tail;            // node slots, -1 = none
+    int32_t count, _pad;
+    int64_t qty;                   // sum of resting sizes (sweep scan, top of book)
+    int64_t tail_oid;              // oid of the tail node (OUT.prev on append, KP:217)
+};
+static_assert(sizeof(Level) == 32, "Level");
+
+struct alignas(64) Node {          // one resting Order (KP:449-458)
+    int64_t oid, aid, sid;
+    int64_t prev_oid;              // oid of the previous node in the level (valid when prev >= 0)
+    int32_t size, next, prev, group;
+    int32_t price, action, live, _pad;
+};
+static_assert(sizeof(Node) == 64, "Node");
+
+struct alignas(64) GroupState {
+    uint64_t bm0_lsb, bm0_msb;     // book +g  (KP:391-404 layout: lsb = prices 0..62, msb = 63..126)
+    uint64_t bm1_lsb, bm1_msb;     // book -g
+    int32_t exists, free_head, chunk_next, chunk_end;
+    int32_t _pad[4];
+};
+static_assert(sizeof(GroupState) == 64, "GroupState");
+
+struct TradeRec {                  // == kme_trade
+    int64_t moid, maid, msid;
+    int32_t mprice, size;
+};
+static_assert(sizeof(TradeRec) == 32, "TradeRec");
+
+struct TradeTmp {                  // unordered trade scratch written by the group wavefronts
+    TradeRec t;
+    int32_t seq, ord;
+};
+static_assert(sizeof(TradeTmp) == 40, "TradeTmp");
+
+struct PosEntry { int64_t k0, k1, v0, v1; };   // Positions: UUID(aid,sid) -> UUID(amount,available)
+
+// Counters block (u64 words).
+enum Ctr : int {
+    C_ERR = 0,         // (index << 16) | (detail << 8) | status; UINT64_MAX = none
+    C_TRADES, C_RESTS, C_VISITS, C_CANCEL_OK, C_ORDERS,
+    C_TTMP,            // trade scratch records reserved
+    C_POOL_BUMP,       // pool slots handed out in chunks
+    C_OTAB_USED,       // non-empty oid-table slots
+    C_ACCT_OPS,        // FUNDED: account records in the epoch
+    C_BAL_USED, C_POS_USED,
+    C_NCTR = 16
+};
+
+constexpr uint64_t OID_SALT = 0x8000000000000000ull;   // stored key = oid ^ SALT, 0 = empty
+
+struct DevState {
+    int32_t G, mode, A, passes;
+    uint32_t pool_cap, otab_mask, _pad0, ttmp_cap;
+    uint32_t bal_mask, pos_mask, trades_cap, _pad;
+    GroupState* grp;
+    Level* lev;
+    Node* pool;
+    uint64_t* otab_key;
+    int32_t* otab_val;
+    // FUNDED ledger
+    int64_t* acct_since;
+    int64_t* acct_lb;
+    int64_t* acct_need;
+    int64_t* acct_negx;
+    int64_t* acct_xfer;
+    // EXACT ledger
+    uint32_t* bal_state;
+    int64_t* bal_key;
+    int64_t* bal_val;
+    uint32_t* pos_state;
+    PosEntry* pos;
+    // per-epoch scratch
+    uint64_t* emap_key;
+    int32_t* emap_val;
+    int32_t* route_grp;
+    int64_t* cancel_tgt;
+    int32_t* rest_slot;
+    uint8_t* acct_ok;
+    uint32_t* rkeys[2];
+    uint32_t* rvals[2];
+    uint32_t* ghist;
+    uint32_t* seg;
+    TradeTmp* ttmp;
+    unsigned long long* ctr;
+};
+
+struct EpochIO {
+    const int32_t* action;
+    const int64_t* oid;
+    const int64_t* aid;
+    const int64_t* sid;
+    const int32_t* price;
+    const int32_t* size;
+    int32_t* out_action;
+    int32_t* out_size;
+    int64_t* out_prev;
+    uint8_t* out_flags;
+    uint32_t* n_trades;
+    uint32_t* trade_off;
+    TradeRec* trades;
+    uint32_t n;
+    uint32_t trades_cap;
+    int64_t seq_base;
+    uint32_t emap_mask;
+    uint32_t _pad;
+};
+
+}  // namespace kme

@@ -1,0 +1,242 @@
+// kme_host.cpp -- host-side wire format of the matching path (no device code).
+//
+//   kme_tape_json        JsonSerializer<Order> (KP:477-495) applied to every forwarded record, in
+//                        the order the processor forwards them (KP:97, 272-273, 124), printed as
+//                        consumer.js prints MatchOut (consumer.js:19): "<key> <value>\n".
+//   kme_order_from_json  JsonDeserializer<Order> (KP:497-521) with Jackson 2.9 defaults: creator
+//                        properties action/oid/aid/sid/price/size (KP:462-474), numeric strings and
+//                        floats coerced, unknown properties rejected.
+//   kme_shard_of         Kafka's default keyed partitioner (murmur2) over decimal(|sid|).
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+
+#include "kme.h"
+
+namespace {
+
+inline char* put_i64(char* p, int64_t v) {
+    char tmp[24];
+    int n = 0;
+    uint64_t u = v < 0 ? (0ull - (uint64_t)v) : (uint64_t)v;
+    do { tmp[n++] = (char)('0' + (u % 10)); u /= 10; } while (u);
+    if (v < 0) *p++ = '-';
+    while (n) *p++ = tmp[--n];
+    return p;
+}
+inline char* put_lit(char* p, const char* s) {
+    while (*s) *p++ = *s++;
+    return p;
+}
+// {"action":A,"oid":O,"aid":A,"sid":S,"price":P,"size":Z,"next":N,"prev":V}
+inline char* put_order(char* p, int32_t action, int64_t oid, int64_t aid, int64_t sid, int32_t price, int32_t size,
+                       bool has_prev, int64_t prev) {
+    p = put_lit(p, "{\"action\":"); p = put_i64(p, action);
+    p = put_lit(p, ",\"oid\":"); p = put_i64(p, oid);
+    p = put_lit(p, ",\"aid\":"); p = put_i64(p, aid);
+    p = put_lit(p, ",\"sid\":"); p = put_i64(p, sid);
+    p = put_lit(p, ",\"price\":"); p = put_i64(p, price);
+    p = put_lit(p, ",\"size\":"); p = put_i64(p, size);
+    p = put_lit(p, ",\"next\":null,\"prev\":");
+    if (has_prev) p = put_i64(p, prev); else p = put_lit(p, "null");
+    *p++ = '}';
+    return p;
+}
+
+struct Out {
+    char* buf;
+    size_t cap, len;
+    char tmp[320];
+    void line(const char* key, char* end_of_tmp_value) {
+        (void)key;
+        const size_t n = (size_t)(end_of_tmp_value - tmp);
+        if (len + n <= cap) std::memcpy(buf + len, tmp, n);
+        len += n;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+kme_status kme_tape_json(const kme_orders* in, uint32_t n, const kme_epoch_result* r, char* buf, size_t cap, size_t* len) {
+    if (!in || !r || !len) return KME_E_INVALID;
+    Out o{buf, buf ? cap : 0, 0, {}};
+    for (uint32_t i = 0; i < n; ++i) {
+        const int32_t a = in->action[i];
+        // IN: the record as received (next/prev null)
+        char* p = put_lit(o.tmp, "IN ");
+        p = put_order(p, a, in->oid[i], in->aid[i], in->sid[i], in->price[i], in->size[i], false, 0);
+        *p++ = '\n';
+        o.line("IN", p);
+        const bool taker_buy = a == KME_BUY;
+        for (uint32_t t = r->trade_off[i]; t < r->trade_off[i + 1]; ++t) {
+            const kme_trade& tr = r->trades[t];
+            p = put_lit(o.tmp, "OUT ");
+            p = put_order(p, taker_buy ? KME_SOLD : KME_BOUGHT, tr.maker_oid, tr.maker_aid, tr.maker_sid, 0, tr.size, false, 0);
+            *p++ = '\n';
+            o.line("OUT", p);
+            p = put_lit(o.tmp, "OUT ");
+            const int32_t dp = (int32_t)((uint32_t)in->price[i] - (uint32_t)tr.maker_price);
+            p = put_order(p, taker_buy ? KME_BOUGHT : KME_SOLD, in->oid[i], in->aid[i], in->sid[i], dp, tr.size, false, 0);
+            *p++ = '\n';
+            o.line("OUT", p);
+        }
+        p = put_lit(o.tmp, "OUT ");
+        p = put_order(p, r->out_action[i], in->oid[i], in->aid[i], in->sid[i], in->price[i], r->out_size[i],
+                      (r->out_flags[i] & KME_OUT_HAS_PREV) != 0, r->out_prev[i]);
+        *p++ = '\n';
+        o.line("OUT", p);
+    }
+    *len = o.len;
+    return KME_OK;
+}
+
+// ------------------------------------------------------------------ JSON -> Order
+namespace {
+struct Parser {
+    const char* p;
+    const char* e;
+    void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p; }
+    bool lit(char c) { ws(); if (p < e && *p == c) { ++p; return true; } return false; }
+    bool word(const char* w) {
+        size_t n = std::strlen(w);
+        if ((size_t)(e - p) >= n && std::memcmp(p, w, n) == 0) { p += n; return true; }
+        return false;
+    }
+    // string without escapes beyond \" \\ (enough for keys and numeric strings)
+    bool str(char* out, size_t cap) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        ++p;
+        size_t n = 0;
+        while (p < e && *p != '"') {
+            char c = *p++;
+            if (c == '\\') { if (p >= e) return false; c = *p++; }
+            if (n + 1 >= cap) return false;
+            out[n++] = c;
+        }
+        if (p >= e) return false;
+        ++p;
+        out[n] = 0;
+        return true;
+    }
+};
+
+// Jackson's coercion of a scalar token to a Java long / int (Jackson 2.9 defaults).
+// kind: 0 = number token, 1 = string token.  Returns false on a value Jackson would reject.
+bool to_integral(const char* s, size_t n, bool is_int, int64_t* out) {
+    if (n == 0) return false;
+    bool fp = false;
+    for (size_t i = 0; i < n; ++i)
+        if (s[i] == '.' || s[i] == 'e' || s[i] == 'E') fp = true;
+    char buf[64];
+    if (n >= sizeof buf) return false;
+    std::memcpy(buf, s, n);
+    buf[n] = 0;
+    if (fp) {  // ACCEPT_FLOAT_AS_INT: truncation toward zero
+        char* end = nullptr;
+        double d = std::strtod(buf, &end);
+        if (end != buf + n || !std::isfinite(d)) return false;
+        d = std::trunc(d);
+        if (is_int ? (d < -2147483648.0 || d > 2147483647.0) : (d < -9223372036854775808.0 || d >= 9223372036854775808.0))
+            return false;
+        *out = (int64_t)d;
+        return true;
+    }
+    size_t i = 0;
+    bool neg = false;
+    if (buf[0] == '-' || buf[0] == '+') { neg = buf[0] == '-'; i = 1; }
+    if (i >= n) return false;
+    uint64_t acc = 0;
+    for (; i < n; ++i) {
+        if (buf[i] < '0' || buf[i] > '9') return false;
+        const uint64_t d = (uint64_t)(buf[i] - '0');
+        if (acc > (UINT64_MAX - d) / 10) return false;
+        acc = acc * 10 + d;
+    }
+    const uint64_t lim = is_int ? (neg ? 2147483648ull : 2147483647ull) : (neg ? 9223372036854775808ull : 9223372036854775807ull);
+    if (acc > lim) return false;
+    *out = neg ? (int64_t)(0ull - acc) : (int64_t)acc;
+    return true;
+}
+}  // namespace
+
+kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, int64_t* oid, int64_t* aid,
+                               int64_t* sid, int32_t* price, int32_t* size) {
+    if (!json || !action || !oid || !aid || !sid || !price || !size) return KME_E_INVALID;
+    Parser P{json, json + len};
+    int64_t v[6] = {0, 0, 0, 0, 0, 0};   // absent creator properties default to 0
+    static const char* names[8] = {"action", "oid", "aid", "sid", "price", "size", "next", "prev"};
+    static const bool is_int[6] = {true, false, false, false, true, true};
+    if (!P.lit('{')) return KME_E_INVALID;
+    if (!P.lit('}')) {
+        for (;;) {
+            char key[32];
+            if (!P.str(key, sizeof key)) return KME_E_INVALID;
+            if (!P.lit(':')) return KME_E_INVALID;
+            int k = -1;
+            for (int j = 0; j < 8; ++j) if (std::strcmp(key, names[j]) == 0) k = j;
+            if (k < 0) return KME_E_INVALID;              // FAIL_ON_UNKNOWN_PROPERTIES
+            P.ws();
+            if (P.p >= P.e) return KME_E_INVALID;
+            if (P.word("null")) {
+                if (k < 6) v[k] = 0;                       // null -> primitive default
+            } else if (*P.p == '"') {
+                char s[64];
+                if (!P.str(s, sizeof s)) return KME_E_INVALID;
+                if (k >= 6) return KME_E_DOMAIN;          // linked input orders are not carried
+                int64_t x;
+                if (!to_integral(s, std::strlen(s), is_int[k], &x)) return KME_E_INVALID;
+                v[k] = x;
+            } else {
+                const char* b = P.p;
+                while (P.p < P.e && (std::strchr("+-0123456789.eE", *P.p) != nullptr)) ++P.p;
+                if (P.p == b) return KME_E_INVALID;       // true/false/objects/arrays
+                if (k >= 6) return KME_E_DOMAIN;
+                int64_t x;
+                if (!to_integral(b, (size_t)(P.p - b), is_int[k], &x)) return KME_E_INVALID;
+                v[k] = x;
+            }
+            if (P.lit(',')) continue;
+            if (P.lit('}')) break;
+            return KME_E_INVALID;
+        }
+    }
+    P.ws();
+    if (P.p != P.e) return KME_E_INVALID;
+    *action = (int32_t)v[0]; *oid = v[1]; *aid = v[2]; *sid = v[3]; *price = (int32_t)v[4]; *size = (int32_t)v[5];
+    return KME_OK;
+}
+
+// org.apache.kafka.common.utils.Utils.murmur2 + toPositive, over the UTF-8 decimal of |sid|.
+uint32_t kme_shard_of(int64_t sid, uint32_t n_shards) {
+    if (n_shards == 0) return 0;
+    char d[24];
+    uint64_t u = sid < 0 ? (0ull - (uint64_t)sid) : (uint64_t)sid;
+    int n = 0;
+    char tmp[24];
+    do { tmp[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    for (int i = 0; i < n; ++i) d[i] = tmp[n - 1 - i];
+    const uint32_t m = 0x5bd1e995u;
+    const int r = 24;
+    uint32_t h = 0x9747b28cu ^ (uint32_t)n;
+    const int n4 = n / 4;
+    for (int i = 0; i < n4; ++i) {
+        const int i4 = i * 4;
+        uint32_t k = (uint32_t)(uint8_t)d[i4] | ((uint32_t)(uint8_t)d[i4 + 1] << 8) |
+                     ((uint32_t)(uint8_t)d[i4 + 2] << 16) | ((uint32_t)(uint8_t)d[i4 + 3] << 24);
+        k *= m; k ^= k >> r; k *= m;
+        h *= m; h ^= k;
+    }
+    switch (n % 4) {
+    case 3: h ^= (uint32_t)(uint8_t)d[(n & ~3) + 2] << 16; [[fallthrough]];
+    case 2: h ^= (uint32_t)(uint8_t)d[(n & ~3) + 1] << 8; [[fallthrough]];
+    case 1: h ^= (uint32_t)(uint8_t)d[n & ~3]; h *= m;
+    }
+    h ^= h >> 13; h *= m; h ^= h >> 15;
+    return (h & 0x7fffffffu) % n_shards;
+}
+
+}  // extern "C"

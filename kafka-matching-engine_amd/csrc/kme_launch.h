@@ -1,0 +1,29 @@
+// kme_launch.h -- host-side launchers of the epoch kernels (kme_kernels.hip), used by the runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "kme_device.h"
+
+namespace kme {
+
+constexpr int RADIX_TILE = 4096;     // inputs per partition tile (256 threads x 16)
+constexpr int TRADE_CHUNK = 64;      // trade-scratch records reserved per wavefront at a time
+constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
+
+// FUNDED pipeline
+void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);
+void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
+void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);
+void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st);
+// returns the buffer index (0/1) holding the sorted input permutation
+int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st);
+void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st);
+void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st);
+void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
+// EXACT pipeline (emap + route shared)
+void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
+// maintenance
+void launch_otab_rebuild(const DevState& S, hipStream_t st);
+void launch_tob(const DevState& S, void* out, hipStream_t st);
+void launch_init_state(const DevState& S, hipStream_t st);
+
+}  // namespace kme

@@ -1,0 +1,620 @@
+// kme_runtime.cpp -- host runtime behind include/kme.h: HBM allocation of the stores, the epoch
+// launch sequence, result retrieval and canonical snapshots.
+//
+// Reference correspondence (KProcessor.java, "KP"):
+//   kme_create            KP:30-49 (store builders) + MatchingEngine.init KP:86-93
+//   kme_submit_epoch[_device]  MatchingEngine.process KP:96-126, for a whole epoch of records
+//   kme_destroy           MatchingEngine.close KP:129
+//   kme_snapshot_*        the contents of Books/Buckets/Orders and Balances/Positions
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kme.h"
+#include "kme_device.h"
+#include "kme_launch.h"
+
+using namespace kme;
+
+namespace {
+
+const char* kPhaseNames[] = {"emap", "ledger", "route", "partition", "match", "compact", "table", "serial"};
+enum Phase { PH_EMAP, PH_LEDGER, PH_ROUTE, PH_PART, PH_MATCH, PH_COMPACT, PH_TABLE, PH_SERIAL, PH_N };
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct kme_engine {
+    kme_config cfg{};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    DevState S{};
+    DevState* d_S = nullptr;
+    EpochIO* d_io = nullptr;
+    // engine-owned epoch buffers
+    int32_t *d_action = nullptr, *d_price = nullptr, *d_size = nullptr;
+    int64_t *d_oid = nullptr, *d_aid = nullptr, *d_sid = nullptr;
+    int32_t *d_out_action = nullptr, *d_out_size = nullptr;
+    int64_t* d_out_prev = nullptr;
+    uint8_t* d_out_flags = nullptr;
+    uint32_t *d_ntrades = nullptr, *d_trade_off = nullptr;
+    TradeRec* d_trades = nullptr;
+    unsigned long long* h_ctr = nullptr;  // pinned copy of the counters block
+    std::vector<void*> allocs;
+    int64_t seq_base = 0;
+    uint32_t last_n = 0;
+    bool pending = false;
+    int failed = 0;
+    int fail_status = 0, fail_detail = 0;
+    bool timing = false;
+    hipEvent_t ev[PH_N * 2] = {};
+    bool ev_used[PH_N] = {};
+    float phase_ms[KME_MAX_PHASES] = {};
+    uint64_t otab_cap = 0;
+};
+
+#define HIP_TRY(x)                                                                          \
+    do {                                                                                    \
+        hipError_t _e = (x);                                                                \
+        if (_e != hipSuccess) {                                                             \
+            std::fprintf(stderr, "kme: HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+            return KME_E_HIP;                                                               \
+        }                                                                                   \
+    } while (0)
+
+template <class T>
+static kme_status dalloc(kme_engine* e, T** p, size_t count) {
+    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    void* q = nullptr;
+    HIP_TRY(hipMalloc(&q, bytes));
+    e->allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return KME_OK;
+}
+
+#define ALLOC(ptr, n)                                  \
+    do {                                               \
+        kme_status _s = dalloc(e, &(ptr), (size_t)(n)); \
+        if (_s != KME_OK) { kme_destroy(e); return _s; } \
+    } while (0)
+
+static void phase_begin(kme_engine* e, int ph) {
+    if (!e->timing) return;
+    (void)hipEventRecord(e->ev[2 * ph], e->stream);
+    e->ev_used[ph] = true;
+}
+static void phase_end(kme_engine* e, int ph) {
+    if (!e->timing) return;
+    (void)hipEventRecord(e->ev[2 * ph + 1], e->stream);
+}
+
+extern "C" {
+
+const char* kme_strerror(int s) {
+    switch (s) {
+    case KME_OK: return "ok";
+    case KME_E_INVALID: return "invalid argument";
+    case KME_E_CAPACITY: return "capacity exceeded";
+    case KME_E_DOMAIN: return "input outside the parity domain (reference would throw or hang)";
+    case KME_E_UNFUNDED: return "FUNDED mode: order acceptance not provably ledger-independent";
+    case KME_E_UNSUPPORTED: return "operation not supported in this mode";
+    case KME_E_HIP: return "HIP runtime error";
+    case KME_E_FAILED: return "engine failed earlier";
+    default: return "unknown";
+    }
+}
+const char* kme_domain_str(int d) {
+    static const char* names[] = {"none", "NPE position (KP:179-180/332)", "NPE bucket (KP:234-235/252-253)",
+                                  "NPE order (KP:236-237/257)", "NPE balance (KP:157/286/331)",
+                                  "removeAllOrders never returns (KP:341-353)", "NPE book (KP:294)",
+                                  "resting price outside 0..126", "duplicate live oid", "FUNDED price/size range",
+                                  "sentinel oid", "order pool full", "oid table full", "trade buffer full",
+                                  "symbol id >= max_symbols", "account id >= max_accounts", "ledger table full",
+                                  "epoch larger than max_epoch"};
+    if (d < 0 || d >= (int)(sizeof(names) / sizeof(names[0]))) return "unknown";
+    return names[d];
+}
+void kme_free(void* p) { std::free(p); }
+
+kme_status kme_create(const kme_config* cfg, kme_engine** out) {
+    if (!cfg || !out) return KME_E_INVALID;
+    if (cfg->abi_version != KME_ABI_VERSION) return KME_E_INVALID;
+    if (cfg->mode != KME_MODE_EXACT && cfg->mode != KME_MODE_FUNDED) return KME_E_INVALID;
+    if (cfg->max_symbols == 0 || cfg->max_symbols > (1u << 24) || cfg->max_epoch == 0 ||
+        cfg->max_epoch > (1u << 30) || cfg->max_resting == 0 || cfg->max_resting >= (1ull << 31) ||
+        cfg->max_trades == 0)
+        return KME_E_INVALID;
+    if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28)))
+        return KME_E_INVALID;
+    kme_engine* e = new kme_engine();
+    e->cfg = *cfg;
+    e->device = cfg->device;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+    e->stream = e->own_stream;
+    for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
+
+    const bool funded = cfg->mode == KME_MODE_FUNDED;
+    const uint32_t G = cfg->max_symbols;
+    const uint32_t E = cfg->max_epoch;
+    const uint64_t P = cfg->max_resting;
+    DevState& S = e->S;
+    S.G = (int32_t)G;
+    S.mode = (int32_t)cfg->mode;
+    S.A = funded ? (int32_t)cfg->max_accounts : 0;
+    {
+        int bits = 0;
+        while ((1ull << bits) <= (uint64_t)G) ++bits;   // keys 0..G
+        S.passes = (bits + 7) / 8;
+    }
+    S.pool_cap = (uint32_t)P;
+    e->otab_cap = pow2_at_least(std::max<uint64_t>(2 * P, 1024));
+    S.otab_mask = (uint32_t)(e->otab_cap - 1);
+    S.trades_cap = cfg->max_trades;
+    const uint64_t ttmp_cap = funded ? (uint64_t)cfg->max_trades + (uint64_t)(G + 64) * TRADE_CHUNK : 1;
+    if (ttmp_cap >= (1ull << 32)) { kme_destroy(e); return KME_E_INVALID; }
+    S.ttmp_cap = (uint32_t)ttmp_cap;
+
+    ALLOC(S.grp, G);
+    ALLOC(S.lev, (size_t)G * 2 * NLEV);
+    ALLOC(S.pool, P);
+    ALLOC(S.otab_key, e->otab_cap);
+    ALLOC(S.otab_val, e->otab_cap);
+    if (funded) {
+        ALLOC(S.acct_since, cfg->max_accounts);
+        ALLOC(S.acct_lb, cfg->max_accounts);
+        ALLOC(S.acct_need, cfg->max_accounts);
+        ALLOC(S.acct_negx, cfg->max_accounts);
+        ALLOC(S.acct_xfer, cfg->max_accounts);
+    } else {
+        const uint64_t lc = pow2_at_least(std::max<uint64_t>(2 * std::max<uint64_t>(cfg->ledger_capacity, 1024), 2048));
+        if (lc > (1ull << 31)) { kme_destroy(e); return KME_E_INVALID; }
+        S.bal_mask = (uint32_t)(lc - 1);
+        S.pos_mask = (uint32_t)(lc - 1);
+        ALLOC(S.bal_state, lc);
+        ALLOC(S.bal_key, lc);
+        ALLOC(S.bal_val, lc);
+        ALLOC(S.pos_state, lc);
+        ALLOC(S.pos, lc);
+    }
+    const uint64_t emap_cap = pow2_at_least(std::max<uint64_t>(2ull * E, 1024));
+    ALLOC(S.emap_key, emap_cap);
+    ALLOC(S.emap_val, emap_cap);
+    ALLOC(S.route_grp, E);
+    ALLOC(S.cancel_tgt, E);
+    ALLOC(S.rest_slot, E);
+    ALLOC(S.acct_ok, E);
+    if (funded) {
+        ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
+        ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);
+        ALLOC(S.ttmp, ttmp_cap);
+    }
+    const uint64_t ntiles = (E + RADIX_TILE - 1) / RADIX_TILE;
+    ALLOC(S.ghist, 256 * ntiles + 2 * (E / 2048 + 16) + 4096);
+    ALLOC(S.seg, (size_t)G + 2);
+    ALLOC(S.ctr, C_NCTR);
+    // epoch buffers
+    ALLOC(e->d_action, E); ALLOC(e->d_price, E); ALLOC(e->d_size, E);
+    ALLOC(e->d_oid, E); ALLOC(e->d_aid, E); ALLOC(e->d_sid, E);
+    ALLOC(e->d_out_action, E); ALLOC(e->d_out_size, E); ALLOC(e->d_out_prev, E);
+    ALLOC(e->d_out_flags, E); ALLOC(e->d_ntrades, E); ALLOC(e->d_trade_off, (size_t)E + 1);
+    ALLOC(e->d_trades, cfg->max_trades);
+    ALLOC(e->d_S, 1);
+    ALLOC(e->d_io, 1);
+    HIP_TRY(hipHostMalloc((void**)&e->h_ctr, C_NCTR * sizeof(unsigned long long), hipHostMallocDefault));
+
+    // initial store contents: every group absent, empty tables
+    hipStream_t st = e->stream;
+    HIP_TRY(hipMemsetAsync(S.otab_key, 0, e->otab_cap * sizeof(uint64_t), st));
+    HIP_TRY(hipMemsetAsync(S.otab_val, 0xFF, e->otab_cap * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(S.pool, 0, P * sizeof(Node), st));
+    HIP_TRY(hipMemsetAsync(S.ctr, 0, C_NCTR * sizeof(unsigned long long), st));
+    if (funded) {
+        HIP_TRY(hipMemsetAsync(S.acct_lb, 0, cfg->max_accounts * sizeof(int64_t), st));
+        HIP_TRY(hipMemsetAsync(S.acct_need, 0, cfg->max_accounts * sizeof(int64_t), st));
+        HIP_TRY(hipMemsetAsync(S.acct_negx, 0, cfg->max_accounts * sizeof(int64_t), st));
+        HIP_TRY(hipMemsetAsync(S.acct_xfer, 0, cfg->max_accounts * sizeof(int64_t), st));
+    } else {
+        const size_t lc = (size_t)S.bal_mask + 1;
+        HIP_TRY(hipMemsetAsync(S.bal_state, 0, lc * sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(S.pos_state, 0, lc * sizeof(uint32_t), st));
+    }
+    launch_init_state(S, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(e->d_S, &e->S, sizeof(DevState), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *out = e;
+    return KME_OK;
+}
+
+kme_status kme_destroy(kme_engine* e) {
+    if (!e) return KME_E_INVALID;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (void* p : e->allocs) (void)hipFree(p);
+    if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+    for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    delete e;
+    return KME_OK;
+}
+
+kme_status kme_set_stream(kme_engine* e, void* s) {
+    if (!e) return KME_E_INVALID;
+    e->stream = s ? reinterpret_cast<hipStream_t>(s) : e->own_stream;
+    return KME_OK;
+}
+
+kme_status kme_enable_timing(kme_engine* e, int enable) {
+    if (!e) return KME_E_INVALID;
+    e->timing = enable != 0;
+    return KME_OK;
+}
+
+static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
+    if (e->failed) return KME_E_FAILED;
+    if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
+    const bool funded = e->cfg.mode == KME_MODE_FUNDED;
+    DevState& S = e->S;
+    hipStream_t st = e->stream;
+    EpochIO io{};
+    io.action = in->action; io.oid = in->oid; io.aid = in->aid; io.sid = in->sid;
+    io.price = in->price; io.size = in->size;
+    if (out) {
+        io.out_action = out->out_action; io.out_size = out->out_size; io.out_prev = out->out_prev;
+        io.out_flags = out->out_flags; io.trade_off = out->trade_off; io.trades = reinterpret_cast<TradeRec*>(out->trades);
+        io.trades_cap = out->trades_cap;
+    } else {
+        io.out_action = e->d_out_action; io.out_size = e->d_out_size; io.out_prev = e->d_out_prev;
+        io.out_flags = e->d_out_flags; io.trade_off = e->d_trade_off; io.trades = e->d_trades;
+        io.trades_cap = e->cfg.max_trades;
+    }
+    io.n_trades = e->d_ntrades;
+    io.n = n;
+    io.seq_base = e->seq_base;
+    const uint64_t emap_cap = pow2_at_least(std::max<uint64_t>(2ull * n, 1024));
+    io.emap_mask = (uint32_t)(emap_cap - 1);
+    for (bool& u : e->ev_used) u = false;
+
+    // per-epoch counters: error = none, stats = 0 (pool bump / table usage persist)
+    HIP_TRY(hipMemsetAsync(&S.ctr[C_ERR], 0xFF, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[C_TRADES], 0, (C_TTMP - C_TRADES + 1) * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[C_ACCT_OPS], 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(S.emap_key, 0, emap_cap * sizeof(uint64_t), st));
+
+    phase_begin(e, PH_EMAP);
+    launch_emap(S, io, funded, e->d_io, st);
+    phase_end(e, PH_EMAP);
+    if (funded) {
+        phase_begin(e, PH_LEDGER);
+        launch_ledger_funded(S, io, st);
+        launch_check_funded(S, io, st);
+        phase_end(e, PH_LEDGER);
+    }
+    phase_begin(e, PH_ROUTE);
+    launch_route(S, io, funded, st);
+    phase_end(e, PH_ROUTE);
+    if (funded) {
+        phase_begin(e, PH_PART);
+        const int buf = launch_partition(S, io, st);
+        phase_end(e, PH_PART);
+        phase_begin(e, PH_MATCH);
+        launch_match(S, e->d_S, e->d_io, buf, st);
+        phase_end(e, PH_MATCH);
+        phase_begin(e, PH_COMPACT);
+        launch_compact(S, io, st);
+        phase_end(e, PH_COMPACT);
+    } else {
+        phase_begin(e, PH_SERIAL);
+        launch_serial(e->d_S, e->d_io, st);
+        phase_end(e, PH_SERIAL);
+    }
+    phase_begin(e, PH_TABLE);
+    launch_table(S, io, st);
+    phase_end(e, PH_TABLE);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(e->h_ctr, S.ctr, C_NCTR * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    e->seq_base += n;
+    e->last_n = n;
+    e->pending = true;
+    return KME_OK;
+}
+
+kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
+    if (!e || !in) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    return submit(e, in, n, out);
+}
+
+kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
+    if (!e) return KME_E_INVALID;
+    kme_epoch_status s{};
+    s.error_index = -1;
+    if (!e->pending) {
+        s.status = e->failed ? e->fail_status : KME_OK;
+        if (st) *st = s;
+        return (kme_status)s.status;
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->pending = false;
+    const unsigned long long* c = e->h_ctr;
+    s.n_inputs = e->last_n;
+    s.n_trades = (uint32_t)c[C_TRADES];
+    s.n_orders = c[C_ORDERS];
+    s.n_rests = c[C_RESTS];
+    s.n_maker_visits = c[C_VISITS];
+    s.n_cancel_ok = c[C_CANCEL_OK];
+    if (c[C_ERR] != ~0ull) {
+        s.status = (int32_t)(c[C_ERR] & 0xFF);
+        s.detail = (int32_t)((c[C_ERR] >> 8) & 0xFF);
+        const uint64_t ix = c[C_ERR] >> 16;
+        s.error_index = ix == 0xFFFFFFFFFFFFull ? -1 : (int64_t)ix;
+        e->failed = 1;
+        e->fail_status = s.status;
+        e->fail_detail = s.detail;
+    }
+    if (e->timing) {
+        for (int p = 0; p < PH_N; ++p) {
+            e->phase_ms[p] = 0.f;
+            if (e->ev_used[p]) (void)hipEventElapsedTime(&e->phase_ms[p], e->ev[2 * p], e->ev[2 * p + 1]);
+        }
+    }
+    // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild
+    if (!e->failed && c[C_OTAB_USED] * 2 > e->otab_cap) {
+        launch_otab_rebuild(e->S, e->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, C_NCTR * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (e->h_ctr[C_ERR] != ~0ull || e->h_ctr[C_OTAB_USED] * 4 > e->otab_cap * 3) {
+            e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_OIDTAB;
+        }
+    }
+    if (st) *st = s;
+    return (kme_status)s.status;
+}
+
+kme_status kme_device_results(kme_engine* e, kme_epoch_result* r) {
+    if (!e || !r) return KME_E_INVALID;
+    r->out_action = e->d_out_action; r->out_size = e->d_out_size; r->out_prev = e->d_out_prev;
+    r->out_flags = e->d_out_flags; r->trade_off = e->d_trade_off;
+    r->trades = reinterpret_cast<kme_trade*>(e->d_trades);
+    r->trades_cap = e->cfg.max_trades;
+    return KME_OK;
+}
+
+kme_status kme_phase_times(kme_engine* e, float* ms, int* n) {
+    if (!e || !ms || !n) return KME_E_INVALID;
+    for (int p = 0; p < PH_N; ++p) ms[p] = e->phase_ms[p];
+    *n = PH_N;
+    return KME_OK;
+}
+const char* kme_phase_name(int i) { return (i >= 0 && i < PH_N) ? kPhaseNames[i] : ""; }
+
+// Host-buffer epoch: copies in, runs, copies out.  FUNDED epochs are split into runs at account
+// records so that the reservation proof never has to reason across a CREATE/TRANSFER boundary.
+kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme_epoch_result* out,
+                            kme_epoch_status* st) {
+    if (!e || !in || !out) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    kme_epoch_status total{};
+    total.error_index = -1;
+    total.n_inputs = n;
+    uint32_t a = 0;
+    uint32_t tbase = 0;
+    out->trade_off[0] = 0;
+    const bool funded = e->cfg.mode == KME_MODE_FUNDED;
+    auto is_acct = [&](uint32_t i) { return in->action[i] == KME_CREATE_BALANCE || in->action[i] == KME_TRANSFER; };
+    while (a < n || (n == 0 && a == 0)) {
+        uint32_t b = a;
+        if (n > 0) {
+            if (funded) {
+                const bool kind = is_acct(a);
+                while (b < n && is_acct(b) == kind && b - a < e->cfg.max_epoch) ++b;
+            } else {
+                b = std::min<uint64_t>(n, (uint64_t)a + e->cfg.max_epoch);
+            }
+        }
+        const uint32_t m = b - a;
+        hipStream_t s = e->stream;
+        if (m > 0) {
+            HIP_TRY(hipMemcpyAsync(e->d_action, in->action + a, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->d_oid, in->oid + a, m * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->d_aid, in->aid + a, m * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->d_sid, in->sid + a, m * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->d_price, in->price + a, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->d_size, in->size + a, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        }
+        kme_orders din{e->d_action, e->d_oid, e->d_aid, e->d_sid, e->d_price, e->d_size};
+        kme_status rc = submit(e, &din, m, nullptr);
+        if (rc != KME_OK) return rc;
+        kme_epoch_status es{};
+        rc = kme_wait(e, &es);
+        total.n_trades += es.n_trades;
+        total.n_orders += es.n_orders;
+        total.n_rests += es.n_rests;
+        total.n_maker_visits += es.n_maker_visits;
+        total.n_cancel_ok += es.n_cancel_ok;
+        if (rc != KME_OK) {
+            total.status = es.status;
+            total.detail = es.detail;
+            total.error_index = es.error_index >= 0 ? es.error_index + a : -1;
+            if (st) *st = total;
+            return rc;
+        }
+        if (tbase + es.n_trades > out->trades_cap) {
+            total.status = KME_E_CAPACITY;
+            total.detail = KME_D_CAP_TRADES;
+            if (st) *st = total;
+            e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_TRADES;
+            return KME_E_CAPACITY;
+        }
+        if (m > 0) {
+            HIP_TRY(hipMemcpyAsync(out->out_action + a, e->d_out_action, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(out->out_size + a, e->d_out_size, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(out->out_prev + a, e->d_out_prev, m * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(out->out_flags + a, e->d_out_flags, m * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(out->trade_off + a + 1, e->d_trade_off + 1, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            if (es.n_trades)
+                HIP_TRY(hipMemcpyAsync(out->trades + tbase, e->d_trades, (size_t)es.n_trades * sizeof(kme_trade), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            for (uint32_t k = a + 1; k <= b; ++k) out->trade_off[k] += tbase;
+        }
+        tbase += es.n_trades;
+        a = b;
+        if (n == 0) break;
+    }
+    total.n_trades = tbase;
+    if (st) *st = total;
+    return KME_OK;
+}
+
+kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out) {
+    if (!e || !dev_out) return KME_E_INVALID;
+    launch_tob(e->S, dev_out, e->stream);
+    HIP_TRY(hipGetLastError());
+    return KME_OK;
+}
+
+// ------------------------------------------------------------------ snapshots
+static char* dup_string(const std::string& s, size_t* len) {
+    char* p = (char*)std::malloc(s.size() + 1);
+    std::memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    if (len) *len = s.size();
+    return p;
+}
+
+kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
+    if (!e || !text) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const uint32_t G = e->cfg.max_symbols;
+    std::vector<GroupState> grp(G);
+    std::vector<Level> lev((size_t)G * 2 * NLEV);
+    unsigned long long ctr[C_NCTR];
+    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    const uint64_t nslots = std::min<uint64_t>(ctr[C_POOL_BUMP], e->cfg.max_resting);
+    std::vector<Node> pool(nslots);
+    HIP_TRY(hipMemcpy(grp.data(), e->S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lev.data(), e->S.lev, lev.size() * sizeof(Level), hipMemcpyDeviceToHost));
+    if (nslots) HIP_TRY(hipMemcpy(pool.data(), e->S.pool, nslots * sizeof(Node), hipMemcpyDeviceToHost));
+
+    struct BookLine { int64_t key, msb, lsb; };
+    struct BucketLine { int64_t ptr, first, last; };
+    std::vector<BookLine> books;
+    std::vector<BucketLine> buckets;
+    std::vector<std::string> problems;
+    uint64_t listed = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        const GroupState& gs = grp[g];
+        if (!gs.exists) continue;
+        for (int side = 0; side < (g == 0 ? 1 : 2); ++side) {
+            const int64_t key = side ? -(int64_t)g : (int64_t)g;
+            const uint64_t l = side ? gs.bm1_lsb : gs.bm0_lsb, m = side ? gs.bm1_msb : gs.bm0_msb;
+            books.push_back({key, (int64_t)m, (int64_t)l});
+            for (int p = 0; p <= 126; ++p) {
+                const bool set = p < 63 ? ((l >> p) & 1) : ((m >> (p - 63)) & 1);
+                if (!set) continue;
+                const Level& L = lev[((size_t)g * 2 + side) * NLEV + p];
+                if (L.head < 0 || (uint64_t)L.head >= nslots || L.tail < 0 || (uint64_t)L.tail >= nslots) {
+                    problems.push_back("X level head/tail out of range");
+                    continue;
+                }
+                buckets.push_back({(int64_t)((uint64_t)key << 8) | p, pool[L.head].oid, pool[L.tail].oid});
+                // invariant walk: list links, count, quantity, tail oid
+                int32_t s = L.head, prev = -1, cnt = 0;
+                int64_t qty = 0;
+                while (s >= 0 && (uint64_t)s < nslots && cnt <= (int32_t)nslots) {
+                    const Node& nd = pool[s];
+                    if (!nd.live || nd.prev != prev || nd.price != p || nd.group != (int32_t)g) {
+                        problems.push_back("X broken list at key " + std::to_string(key) + " price " + std::to_string(p));
+                        break;
+                    }
+                    if (prev >= 0 && nd.prev_oid != pool[prev].oid) problems.push_back("X prev_oid mismatch");
+                    qty += nd.size;
+                    ++cnt;
+                    prev = s;
+                    s = nd.next;
+                }
+                listed += cnt;
+                if (prev != L.tail || cnt != L.count || qty != L.qty || L.tail_oid != pool[L.tail].oid)
+                    problems.push_back("X level bookkeeping mismatch at key " + std::to_string(key) + " price " + std::to_string(p));
+            }
+        }
+    }
+    std::sort(books.begin(), books.end(), [](const BookLine& a, const BookLine& b) { return a.key < b.key; });
+    std::sort(buckets.begin(), buckets.end(), [](const BucketLine& a, const BucketLine& b) { return a.ptr < b.ptr; });
+    std::vector<const Node*> live;
+    for (uint64_t s = 0; s < nslots; ++s) if (pool[s].live) live.push_back(&pool[s]);
+    if (live.size() != listed) problems.push_back("X live nodes not reachable from a level: " + std::to_string(live.size()) + " vs " + std::to_string(listed));
+    std::sort(live.begin(), live.end(), [](const Node* a, const Node* b) { return a->oid < b->oid; });
+    std::string out;
+    out.reserve(64 * (books.size() + buckets.size() + live.size()) + 64);
+    char line[256];
+    for (auto& b : books) {
+        int k = std::snprintf(line, sizeof line, "B %lld %lld %lld\n", (long long)b.key, (long long)b.msb, (long long)b.lsb);
+        out.append(line, k);
+    }
+    for (auto& b : buckets) {
+        int k = std::snprintf(line, sizeof line, "K %lld %lld %lld\n", (long long)b.ptr, (long long)b.first, (long long)b.last);
+        out.append(line, k);
+    }
+    for (const Node* nd : live) {
+        char nx[32], pv[32];
+        if (nd->next >= 0) std::snprintf(nx, sizeof nx, "%lld", (long long)pool[nd->next].oid); else std::strcpy(nx, "null");
+        if (nd->prev >= 0) std::snprintf(pv, sizeof pv, "%lld", (long long)nd->prev_oid); else std::strcpy(pv, "null");
+        int k = std::snprintf(line, sizeof line, "O %lld %d %lld %lld %d %d %s %s\n", (long long)nd->oid, nd->action,
+                              (long long)nd->aid, (long long)nd->sid, nd->price, nd->size, nx, pv);
+        out.append(line, k);
+    }
+    for (auto& p : problems) { out += p; out += '\n'; }
+    *text = dup_string(out, len);
+    return KME_OK;
+}
+
+kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
+    if (!e || !text) return KME_E_INVALID;
+    if (e->cfg.mode != KME_MODE_EXACT) return KME_E_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const size_t lc = (size_t)e->S.bal_mask + 1;
+    std::vector<uint32_t> bst(lc), pst(lc);
+    std::vector<int64_t> bk(lc), bv(lc);
+    std::vector<PosEntry> pos(lc);
+    HIP_TRY(hipMemcpy(bst.data(), e->S.bal_state, lc * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(bk.data(), e->S.bal_key, lc * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(bv.data(), e->S.bal_val, lc * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(pst.data(), e->S.pos_state, lc * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(pos.data(), e->S.pos, lc * sizeof(PosEntry), hipMemcpyDeviceToHost));
+    std::vector<std::pair<int64_t, int64_t>> bal;
+    for (size_t h = 0; h < lc; ++h) if (bst[h] == 1) bal.push_back({bk[h], bv[h]});
+    std::sort(bal.begin(), bal.end());
+    std::vector<PosEntry> ps;
+    for (size_t h = 0; h < lc; ++h) if (pst[h] == 1) ps.push_back(pos[h]);
+    std::sort(ps.begin(), ps.end(), [](const PosEntry& a, const PosEntry& b) { return a.k0 != b.k0 ? a.k0 < b.k0 : a.k1 < b.k1; });
+    std::string out;
+    char line[256];
+    for (auto& b : bal) {
+        int k = std::snprintf(line, sizeof line, "A %lld %lld\n", (long long)b.first, (long long)b.second);
+        out.append(line, k);
+    }
+    for (auto& p : ps) {
+        int k = std::snprintf(line, sizeof line, "P %lld %lld %lld %lld\n", (long long)p.k0, (long long)p.k1, (long long)p.v0, (long long)p.v1);
+        out.append(line, k);
+    }
+    *text = dup_string(out, len);
+    return KME_OK;
+}
+
+}  // extern "C"

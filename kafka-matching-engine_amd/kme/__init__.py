@@ -1,0 +1,353 @@
+"""Python host layer of the MI355X matching core: ctypes bindings of include/kme.h and
+include/kme_processor.h (libkme.so, built in-tree by __graft_entry__.build()).
+
+The product path is the HIP engine in libkme.so; there is no CPU fallback.  Loading fails loudly
+when the shared object is missing, and creating an engine fails when no HIP device is present.
+
+Reference correspondence (KProcessor.java, "KP"):
+    Engine            the five stores + MatchingEngine (KP:30-49, 63-445) for one stream task
+    Engine.process    MatchingEngine.process (KP:96-126) over an epoch of records
+    Processor         MatchingEngine as a Processor<String, Order> fed JSON records (KP:52, 96)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .workloads import Orders  # noqa: F401  (re-export)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkme.so")
+
+MODE_EXACT, MODE_FUNDED = 0, 1
+KME_OK = 0
+STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
+          7: "FAILED"}
+ABI_VERSION = 1
+
+TRADE_DTYPE = np.dtype([("maker_oid", "<i8"), ("maker_aid", "<i8"), ("maker_sid", "<i8"),
+                        ("maker_price", "<i4"), ("size", "<i4")])
+TOB_DTYPE = np.dtype([("bid_px", "<i4"), ("ask_px", "<i4"), ("bid_qty", "<i4"), ("ask_qty", "<i4")])
+assert TRADE_DTYPE.itemsize == 32
+
+
+class kme_config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("mode", C.c_uint32), ("max_symbols", C.c_uint32),
+                ("max_accounts", C.c_uint32), ("max_epoch", C.c_uint32), ("max_trades", C.c_uint32),
+                ("max_resting", C.c_uint64), ("ledger_capacity", C.c_uint64), ("device", C.c_int32),
+                ("flags", C.c_uint32)]
+
+
+class kme_orders(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("action", "oid", "aid", "sid", "price", "size")]
+
+
+class kme_epoch_result(C.Structure):
+    _fields_ = [("out_action", C.c_void_p), ("out_size", C.c_void_p), ("out_prev", C.c_void_p),
+                ("out_flags", C.c_void_p), ("trade_off", C.c_void_p), ("trades", C.c_void_p),
+                ("trades_cap", C.c_uint32)]
+
+
+class kme_epoch_status(C.Structure):
+    _fields_ = [("status", C.c_int32), ("detail", C.c_int32), ("error_index", C.c_int64),
+                ("n_inputs", C.c_uint32), ("n_trades", C.c_uint32), ("n_orders", C.c_uint64),
+                ("n_rests", C.c_uint64), ("n_maker_visits", C.c_uint64), ("n_cancel_ok", C.c_uint64)]
+
+
+FORWARD_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t)
+COMMIT_FN = C.CFUNCTYPE(None, C.c_void_p)
+
+# Every symbol include/kme.h and include/kme_processor.h declare (checked by tests/test_abi.py).
+EXPORTS = [
+    "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
+    "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
+    "kme_top_of_book", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
+    "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str",
+    "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
+    "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
+]
+
+_lib = None
+
+
+def lib():
+    """libkme.so with argtypes set.  Raises if the HIP extension was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libkme.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.  Loading torch first
+    # makes libkme's NEEDED libamdhip64.so.7 resolve to that already-loaded copy (same SONAME);
+    # loading libkme first would map a second HIP/HSA runtime and neither would see the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, st, u32, i32, i64 = C.c_void_p, C.c_int, C.c_uint32, C.c_int32, C.c_int64
+    sig = {
+        "kme_create": (st, [C.POINTER(kme_config), C.POINTER(vp)]),
+        "kme_destroy": (st, [vp]),
+        "kme_set_stream": (st, [vp, vp]),
+        "kme_submit_epoch": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result),
+                                  C.POINTER(kme_epoch_status)]),
+        "kme_submit_epoch_device": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result)]),
+        "kme_wait": (st, [vp, C.POINTER(kme_epoch_status)]),
+        "kme_device_results": (st, [vp, C.POINTER(kme_epoch_result)]),
+        "kme_snapshot_books": (st, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "kme_snapshot_ledger": (st, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "kme_free": (None, [vp]),
+        "kme_top_of_book": (st, [vp, vp]),
+        "kme_phase_times": (st, [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
+        "kme_phase_name": (C.c_char_p, [C.c_int]),
+        "kme_enable_timing": (st, [vp, C.c_int]),
+        "kme_tape_json": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
+                               C.POINTER(C.c_size_t)]),
+        "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
+                                     C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
+        "kme_shard_of": (u32, [i64, u32]),
+        "kme_strerror": (C.c_char_p, [C.c_int]),
+        "kme_domain_str": (C.c_char_p, [C.c_int]),
+        "kme_processor_create": (st, [C.POINTER(kme_config), u32, FORWARD_FN, COMMIT_FN, vp, C.POINTER(vp)]),
+        "kme_processor_process_json": (st, [vp, C.c_char_p, C.c_size_t]),
+        "kme_processor_process": (st, [vp, i32, i64, i64, i64, i32, i32]),
+        "kme_processor_punctuate": (st, [vp]),
+        "kme_processor_close": (st, [vp]),
+        "kme_processor_last_status": (st, [vp, C.POINTER(kme_epoch_status)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class KmeError(RuntimeError):
+    def __init__(self, status: int, what: str = "", st: kme_epoch_status | None = None):
+        L = lib()
+        detail = st.detail if st is not None else 0
+        msg = f"{STATUS.get(status, status)}: {L.kme_strerror(status).decode()}"
+        if detail:
+            msg += f" [{L.kme_domain_str(detail).decode()}]"
+        if st is not None and st.error_index >= 0:
+            msg += f" at input {st.error_index}"
+        if what:
+            msg = f"{what}: {msg}"
+        super().__init__(msg)
+        self.status, self.detail = status, detail
+        self.index = st.error_index if st is not None else -1
+
+
+def _np_ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+def _soa(orders: Orders):
+    cols = dict(action=np.ascontiguousarray(orders.action, np.int32), oid=np.ascontiguousarray(orders.oid, np.int64),
+                aid=np.ascontiguousarray(orders.aid, np.int64), sid=np.ascontiguousarray(orders.sid, np.int64),
+                price=np.ascontiguousarray(orders.price, np.int32), size=np.ascontiguousarray(orders.size, np.int32))
+    s = kme_orders(*[C.c_void_p(cols[k].ctypes.data) for k in ("action", "oid", "aid", "sid", "price", "size")])
+    return s, cols
+
+
+@dataclass
+class EpochResult:
+    """Per-input OUT fields and the ordered trades of one processed epoch (kme_epoch_result)."""
+    out_action: np.ndarray
+    out_size: np.ndarray
+    out_prev: np.ndarray
+    out_flags: np.ndarray
+    trade_off: np.ndarray
+    trades: np.ndarray
+    status: kme_epoch_status
+
+    def tape_json(self, orders: Orders) -> str:
+        """The MatchOut tape as consumer.js prints it (consumer.js:19), via kme_tape_json."""
+        L = lib()
+        s, keep = _soa(orders)
+        r = kme_epoch_result(_np_ptr(self.out_action), _np_ptr(self.out_size), _np_ptr(self.out_prev),
+                             _np_ptr(self.out_flags), _np_ptr(self.trade_off), _np_ptr(self.trades),
+                             len(self.trades))
+        n = C.c_size_t(0)
+        L.kme_tape_json(C.byref(s), len(orders), C.byref(r), None, 0, C.byref(n))
+        buf = C.create_string_buffer(n.value + 1)
+        rc = L.kme_tape_json(C.byref(s), len(orders), C.byref(r), buf, n.value + 1, C.byref(n))
+        if rc:
+            raise KmeError(rc, "kme_tape_json")
+        del keep
+        return buf.raw[: n.value].decode()
+
+
+def default_config(mode: int, max_symbols: int, max_epoch: int, max_resting: int, max_trades: int | None = None,
+                   max_accounts: int = 0, ledger_capacity: int = 1 << 16, device: int = 0) -> kme_config:
+    return kme_config(ABI_VERSION, mode, max_symbols, max_accounts, max_epoch,
+                      max_trades if max_trades is not None else max(4 * max_epoch, 1 << 16),
+                      max_resting, ledger_capacity, device, 0)
+
+
+class Engine:
+    """One device engine (kme_create).  `process` = host-buffer epochs (synchronous)."""
+
+    def __init__(self, cfg: kme_config):
+        L = lib()
+        self._L = L
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = L.kme_create(C.byref(cfg), C.byref(h))
+        if rc:
+            raise KmeError(rc, "kme_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.kme_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process(self, orders: Orders) -> EpochResult:
+        n = len(orders)
+        s, keep = _soa(orders)
+        cap = max(1, int(self.cfg.max_trades))
+        res = EpochResult(np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.uint8),
+                          np.zeros(n + 1, np.uint32), np.zeros(cap, TRADE_DTYPE), kme_epoch_status())
+        r = kme_epoch_result(_np_ptr(res.out_action), _np_ptr(res.out_size), _np_ptr(res.out_prev),
+                             _np_ptr(res.out_flags), _np_ptr(res.trade_off), _np_ptr(res.trades), cap)
+        st = kme_epoch_status()
+        rc = self._L.kme_submit_epoch(self._h, C.byref(s), n, C.byref(r), C.byref(st))
+        del keep
+        res.status = st
+        if rc:
+            raise KmeError(rc, "kme_submit_epoch", st)
+        res.trades = res.trades[: int(res.trade_off[n])].copy()
+        return res
+
+    # ---- device-resident epochs (bench): torch tensors or raw device pointers
+    def submit_device(self, ptrs: dict, n: int):
+        s = kme_orders(*[C.c_void_p(int(ptrs[k])) for k in ("action", "oid", "aid", "sid", "price", "size")])
+        rc = self._L.kme_submit_epoch_device(self._h, C.byref(s), n, None)
+        if rc:
+            raise KmeError(rc, "kme_submit_epoch_device")
+
+    def wait(self) -> kme_epoch_status:
+        st = kme_epoch_status()
+        rc = self._L.kme_wait(self._h, C.byref(st))
+        if rc:
+            raise KmeError(rc, "kme_wait", st)
+        return st
+
+    def set_stream(self, stream_ptr: int | None):
+        rc = self._L.kme_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None)
+        if rc:
+            raise KmeError(rc, "kme_set_stream")
+
+    def enable_timing(self, on: bool = True):
+        self._L.kme_enable_timing(self._h, 1 if on else 0)
+
+    def phase_times(self) -> dict:
+        ms = (C.c_float * 16)()
+        n = C.c_int(0)
+        self._L.kme_phase_times(self._h, ms, C.byref(n))
+        return {self._L.kme_phase_name(i).decode(): float(ms[i]) for i in range(n.value)}
+
+    def top_of_book(self, dev_ptr: int):
+        rc = self._L.kme_top_of_book(self._h, C.c_void_p(int(dev_ptr)))
+        if rc:
+            raise KmeError(rc, "kme_top_of_book")
+
+    def _text(self, fn) -> str:
+        p = C.c_void_p()
+        n = C.c_size_t(0)
+        rc = fn(self._h, C.byref(p), C.byref(n))
+        if rc:
+            raise KmeError(rc, fn.__name__)
+        try:
+            return C.string_at(p, n.value).decode()
+        finally:
+            self._L.kme_free(p)
+
+    def snapshot_books(self) -> str:
+        return self._text(self._L.kme_snapshot_books)
+
+    def snapshot_ledger(self) -> str:
+        return self._text(self._L.kme_snapshot_ledger)
+
+
+class Processor:
+    """kme_processor: the Processor<String, Order> mirror fed MatchIn JSON values.  Forwarded
+    records are collected as (key, value) string pairs, as the MatchOut sink would emit them."""
+
+    def __init__(self, cfg: kme_config, epoch_records: int):
+        L = lib()
+        self._L = L
+        self.records: list[tuple[str, str]] = []
+        self.commits = 0
+
+        def _fwd(user, key, value, n):
+            self.records.append((key.decode(), C.string_at(value, n).decode()))
+
+        def _commit(user):
+            self.commits += 1
+
+        self._fwd = FORWARD_FN(_fwd)
+        self._commit = COMMIT_FN(_commit)
+        h = C.c_void_p()
+        rc = L.kme_processor_create(C.byref(cfg), epoch_records, self._fwd, self._commit, None, C.byref(h))
+        if rc:
+            raise KmeError(rc, "kme_processor_create")
+        self._h = h
+
+    def process_json(self, value: str) -> int:
+        b = value.encode()
+        return self._L.kme_processor_process_json(self._h, b, len(b))
+
+    def punctuate(self) -> int:
+        return self._L.kme_processor_punctuate(self._h)
+
+    def close(self) -> int:
+        if not self._h:
+            return 0
+        rc = self._L.kme_processor_close(self._h)
+        self._h = None
+        return rc
+
+    def last_status(self) -> kme_epoch_status:
+        st = kme_epoch_status()
+        self._L.kme_processor_last_status(self._h, C.byref(st))
+        return st
+
+    def tape_text(self) -> str:
+        return "".join(f"{k} {v}\n" for k, v in self.records)
+
+
+def order_from_json(value: str):
+    """JsonDeserializer<Order> (KP:513-520) of one MatchIn value -> 6-tuple (no device needed)."""
+    L = lib()
+    a, p, z = C.c_int32(), C.c_int32(), C.c_int32()
+    o, ai, s = C.c_int64(), C.c_int64(), C.c_int64()
+    b = value.encode()
+    rc = L.kme_order_from_json(b, len(b), C.byref(a), C.byref(o), C.byref(ai), C.byref(s), C.byref(p), C.byref(z))
+    if rc:
+        raise KmeError(rc, "kme_order_from_json")
+    return (a.value, o.value, ai.value, s.value, p.value, z.value)
+
+
+def tape_json_from(orders: Orders, res: EpochResult) -> str:
+    return res.tape_json(orders)
+
+
+def shard_of(sid: int, n: int) -> int:
+    return int(lib().kme_shard_of(int(sid), int(n)))

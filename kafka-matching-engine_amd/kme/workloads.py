@@ -1,0 +1,362 @@
+"""Seeded synthetic order streams (BASELINE.json configs).
+
+All streams are SoA numpy arrays in the reference's `Order` shape (KP:451-456):
+action i32, oid i64, aid i64, sid i64, price i32, size i32.
+
+* ``exchange_test`` (C1) restates the load generator of /root/reference/exchange_test.js:18-36 and
+  genEvent (exchange_test.js:106-117) with a seeded PRNG (JS Math.random is unseeded).  It is NOT
+  funded: balances run dry and acceptance depends on the exact ledger (engine mode EXACT).
+* ``uniform`` (C2/C3), ``zipf`` (C4) and ``cancel_replace`` (C5) are funded streams: every account
+  receives enough cash that no BUY/SELL can fail the balance check (engine mode FUNDED).
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+ADD_SYMBOL, REMOVE_SYMBOL, BUY, SELL, CANCEL = 0, 1, 2, 3, 4
+BOUGHT, SOLD, REJECT = 5, 6, 7
+CREATE_BALANCE, TRANSFER, PAYOUT = 100, 101, 200
+MAX_SAFE_INTEGER = 2**53 - 1
+INT_MAX = 2**31 - 1
+
+
+@dataclass
+class Orders:
+    action: np.ndarray
+    oid: np.ndarray
+    aid: np.ndarray
+    sid: np.ndarray
+    price: np.ndarray
+    size: np.ndarray
+    # exchange_test.js sends cancel oids as JSON strings (exchange_test.js:98-101); purely a
+    # wire-format detail of the input JSON, the engine sees a long.
+    oid_is_string: np.ndarray | None = field(default=None)
+
+    def __len__(self) -> int:
+        return int(self.action.shape[0])
+
+    @staticmethod
+    def empty(n: int = 0) -> "Orders":
+        return Orders(np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64),
+                      np.zeros(n, np.int64), np.zeros(n, np.int32), np.zeros(n, np.int32),
+                      np.zeros(n, bool))
+
+    @staticmethod
+    def from_rows(rows) -> "Orders":
+        n = len(rows)
+        o = Orders.empty(n)
+        for i, r in enumerate(rows):
+            a, oid, aid, sid, price, size = r[:6]
+            o.action[i], o.oid[i], o.aid[i], o.sid[i], o.price[i], o.size[i] = a, oid, aid, sid, price, size
+            if len(r) > 6:
+                o.oid_is_string[i] = bool(r[6])
+        return o
+
+    def slice(self, a: int, b: int) -> "Orders":
+        s = None if self.oid_is_string is None else self.oid_is_string[a:b]
+        return Orders(self.action[a:b], self.oid[a:b], self.aid[a:b], self.sid[a:b],
+                      self.price[a:b], self.size[a:b], s)
+
+    @staticmethod
+    def concat(parts) -> "Orders":
+        parts = list(parts)
+        cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
+        strs = [p.oid_is_string if p.oid_is_string is not None else np.zeros(len(p), bool) for p in parts]
+        return Orders(cat("action").astype(np.int32), cat("oid").astype(np.int64),
+                      cat("aid").astype(np.int64), cat("sid").astype(np.int64),
+                      cat("price").astype(np.int32), cat("size").astype(np.int32),
+                      np.concatenate(strs))
+
+    def n_orders(self) -> int:
+        """Input order records (BUY/SELL/CANCEL): the unit of the headline metric."""
+        a = self.action
+        return int(np.count_nonzero((a == BUY) | (a == SELL) | (a == CANCEL)))
+
+    def to_json_lines(self) -> list[str]:
+        """JSON.stringify of createOrder (exchange_test.js:63-66): no next/prev fields."""
+        out = []
+        strs = self.oid_is_string
+        for i in range(len(self)):
+            oid = int(self.oid[i])
+            oid_j = json.dumps(str(oid)) if (strs is not None and strs[i]) else str(oid)
+            out.append('{"action":%d,"oid":%s,"aid":%d,"sid":%d,"price":%d,"size":%d}' % (
+                int(self.action[i]), oid_j, int(self.aid[i]), int(self.sid[i]),
+                int(self.price[i]), int(self.size[i])))
+        return out
+
+
+# ----------------------------------------------------------------------------- C1 (exchange_test.js)
+class _JsRandom:
+    """Math.random stand-in: seeded doubles in [0, 1)."""
+
+    def __init__(self, seed: int):
+        self._g = np.random.Generator(np.random.PCG64(seed))
+        self._buf = self._g.random(1 << 16)
+        self._i = 0
+
+    def random(self) -> float:
+        if self._i == len(self._buf):
+            self._buf = self._g.random(1 << 16)
+            self._i = 0
+        v = float(self._buf[self._i])
+        self._i += 1
+        return v
+
+
+def exchange_test(n_events: int = 100_000, seed: int = 1, num_accounts: int = 10,
+                  num_symbols: int = 3, rake: int = 3) -> Orders:
+    """exchange_test.js:18-36 + genEvent (106-117), argument evaluation order preserved."""
+    R = _JsRandom(seed)
+
+    def random_normal():  # exchange_test.js:48-53
+        u = 0.0
+        v = 0.0
+        while u == 0:
+            u = R.random()
+        while v == 0:
+            v = R.random()
+        return math.sqrt(-2.0 * math.log(u)) * math.cos(2.0 * math.pi * v)
+
+    def random_uniform(rng):  # :55-57
+        return math.floor(R.random() * rng)
+
+    def random_normal_param(mean, std):  # :59-61
+        return math.floor(random_normal() * std + mean)
+
+    rows = []
+    orders: dict[int, int] = {}  # JS `orders` object: oid -> aid
+    live: list[int] = []  # Object.keys(orders) in insertion order (oids >= 2^32 are not array indices)
+
+    def create_order(action, oid, aid, sid, price, size, oid_str=False):
+        rows.append((action, oid, aid, sid, price, size, oid_str))
+
+    def create_buy_sell(action):
+        aid = random_uniform(num_accounts)
+        sid = random_uniform(num_symbols)
+        price = random_normal_param(50, 10)
+        size = random_normal_param(50, 10)
+        oid = math.floor(R.random() * MAX_SAFE_INTEGER)
+        if oid not in orders:
+            live.append(oid)
+        orders[oid] = aid
+        create_order(action, oid, aid, sid, price, size)
+
+    for i in range(num_accounts):  # :23-28
+        create_order(CREATE_BALANCE, 0, i, 0, 0, 0)
+        create_order(TRANSFER, 0, i, 0, 0, random_normal_param(500 * 100, 250 * 100))
+    i = 0
+    while i < num_symbols / 2 + 1:  # :29-32
+        create_order(ADD_SYMBOL, 0, 0, i, 0, 0)
+        i += 1
+    for _ in range(n_events):  # :33-36 / genEvent :106-117
+        e = random_uniform(1000)
+        if e == 0:
+            create_order(ADD_SYMBOL, 0, 0, random_uniform(num_symbols), 0, 0)
+        elif e == 1:
+            sid = random_uniform(num_symbols)
+            success = random_uniform(2) == 0
+            if rake <= 100:  # createPayout (:76-79) sends action 4 (CANCEL), oid 0
+                create_order(CANCEL, 0, 0, sid * (1 if success else -1), 0, 100 - rake)
+        elif e in (2, 3):
+            aid = random_uniform(num_accounts)
+            create_order(TRANSFER, 0, aid, 0, 0, random_normal_param(0, 125 * 100))
+        elif 3 < e <= 335:
+            create_buy_sell(BUY)
+        elif 335 < e <= 667:
+            create_buy_sell(SELL)
+        else:  # createCancel (:97-104)
+            if not live:
+                create_order(CANCEL, 0, 0, 0, 0, 0)
+            else:
+                j = math.floor(R.random() * len(live))
+                key = live[j]
+                create_order(CANCEL, key, orders[key], 0, 0, 0, True)
+                del orders[key]
+                del live[j]
+    return Orders.from_rows(rows)
+
+
+# ----------------------------------------------------------------------------- funded streams
+def _unique_oids(n: int, base: int) -> np.ndarray:
+    """n distinct pseudo-random positive oids < 2^53 (odd multiplier: a bijection mod 2^53)."""
+    ctr = (np.arange(n, dtype=np.uint64) + np.uint64(base)) & np.uint64(MAX_SAFE_INTEGER)
+    x = (ctr * np.uint64(0x5DEECE66D) + np.uint64(0xB)) & np.uint64(MAX_SAFE_INTEGER)
+    x = np.where(x == 0, np.uint64(MAX_SAFE_INTEGER), x)
+    return x.astype(np.int64)
+
+
+def funded_setup(n_accounts: int, sids, aid_base: int = 0, transfers_per_account: int = 1) -> Orders:
+    """CREATE_BALANCE + TRANSFER(INT_MAX) per account, then ADD_SYMBOL per symbol."""
+    A = np.arange(n_accounts, dtype=np.int64) + aid_base
+    sids = np.asarray(sids, dtype=np.int64)
+    k = transfers_per_account
+    n = n_accounts * (1 + k) + len(sids)
+    o = Orders.empty(n)
+    per = 1 + k
+    idx = np.arange(n_accounts) * per
+    o.action[idx] = CREATE_BALANCE
+    o.aid[idx] = A
+    for j in range(k):
+        o.action[idx + 1 + j] = TRANSFER
+        o.aid[idx + 1 + j] = A
+        o.size[idx + 1 + j] = INT_MAX
+    s0 = n_accounts * per
+    o.action[s0:] = ADD_SYMBOL
+    o.sid[s0:] = sids
+    return o
+
+
+def _cancel_targets(action, aid, oid, rng) -> np.ndarray:
+    """For each CANCEL row: a uniformly chosen earlier BUY/SELL oid of the same account (0 if none)."""
+    n = len(action)
+    is_ord = (action == BUY) | (action == SELL)
+    is_can = action == CANCEL
+    order_by_acct = np.lexsort((np.arange(n), aid))  # stable by index within account
+    a_sorted = aid[order_by_acct]
+    ord_sorted = is_ord[order_by_acct].astype(np.int64)
+    cum = np.cumsum(ord_sorted)
+    grp_start = np.searchsorted(a_sorted, a_sorted, side="left")
+    cum_before_grp = np.where(grp_start > 0, cum[np.maximum(grp_start - 1, 0)], 0)
+    before = cum - ord_sorted - cum_before_grp  # BUY/SELL rows of this account before this row
+    ord_rows = order_by_acct[is_ord[order_by_acct]]  # BUY/SELL rows grouped by account, in order
+    ord_accts = aid[ord_rows]
+    out = np.zeros(n, np.int64)
+    can_pos = np.nonzero(is_can[order_by_acct])[0]
+    rows = order_by_acct[can_pos]
+    cnt = before[can_pos]
+    ok = cnt > 0
+    k = np.floor(rng.random(len(rows)) * cnt).astype(np.int64)
+    base = np.searchsorted(ord_accts, aid[rows], side="left")
+    tgt = np.where(ok, ord_rows[np.minimum(base + k, len(ord_rows) - 1)], 0)
+    out[rows] = np.where(ok, oid[tgt], 0)
+    return out
+
+
+def uniform(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: int = 1,
+            sid_base: int = 1, aid_base: int = 0, oid_base: int = 1, price_lo: int = 30,
+            price_hi: int = 75, mix=(0.34, 0.33, 0.33)) -> Orders:
+    """C2/C3: 34/33/33 BUY/SELL/CANCEL, sid uniform, price uniform [30,75] (the
+    H5-safe band), size floor(N(50,10)) clamped to [1,100], cancels of an earlier oid of the same
+    account."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    u = rng.random(n_orders)
+    action = np.where(u < mix[0], BUY, np.where(u < mix[0] + mix[1], SELL, CANCEL)).astype(np.int32)
+    aid = rng.integers(0, n_accounts, n_orders).astype(np.int64) + aid_base
+    sid = rng.integers(0, n_symbols, n_orders).astype(np.int64) + sid_base
+    price = rng.integers(price_lo, price_hi + 1, n_orders).astype(np.int32)
+    size = np.clip(np.floor(rng.normal(50, 10, n_orders)), 1, 100).astype(np.int32)
+    oid = _unique_oids(n_orders, oid_base)
+    is_can = action == CANCEL
+    oid = np.where(is_can, _cancel_targets(action, aid, oid, rng), oid)
+    sid = np.where(is_can, 0, sid)
+    price = np.where(is_can, 0, price).astype(np.int32)
+    size = np.where(is_can, 0, size).astype(np.int32)
+    return Orders(action, oid, aid, sid, price, size, np.zeros(n_orders, bool))
+
+
+def zipf(n_orders: int, n_symbols: int = 65536, n_accounts: int = 65536, s: float = 1.1,
+         seed: int = 1, sid_base: int = 1, aid_base: int = 0, oid_base: int = 1,
+         price_lo: int = 40, price_hi: int = 60) -> Orders:
+    """C4: Zipf(s) symbol popularity; a narrow price band keeps hot books deep (~1e4 resting
+    orders over <= 21 levels) -- the reference's book has at most 127 levels."""
+    o = uniform(n_orders, n_symbols, n_accounts, seed, sid_base, aid_base, oid_base, price_lo, price_hi,
+                mix=(0.36, 0.36, 0.28))
+    rng = np.random.Generator(np.random.PCG64(seed + 7919))
+    ranks = np.arange(1, n_symbols + 1, dtype=np.float64)
+    p = ranks ** (-s)
+    p /= p.sum()
+    perm = rng.permutation(n_symbols)  # hot symbols spread over the id space
+    draw = rng.choice(n_symbols, size=n_orders, p=p)
+    sid = perm[draw].astype(np.int64) + sid_base
+    o.sid = np.where(o.action == CANCEL, 0, sid)
+    return o
+
+
+def cancel_replace(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: int = 1,
+                   sid_base: int = 1, aid_base: int = 0, oid_base: int = 1) -> Orders:
+    """C5: 45% (CANCEL, new order of the same account) pairs = 90% of records, and 10% large
+    marketable orders (BUY@75 / SELL@30, size 5,000-50,000) that sweep many levels."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n_pairs = int(n_orders * 0.45)
+    n_big = n_orders - 2 * n_pairs
+    # background book: build with plain limit orders first, then the churn
+    n_units = n_pairs + n_big
+    kind = rng.permutation(np.r_[np.zeros(n_pairs, np.int8), np.ones(n_big, np.int8)])
+    n = n_pairs * 2 + n_big
+    action = np.empty(n, np.int32)
+    aid = np.empty(n, np.int64)
+    sid = np.zeros(n, np.int64)
+    price = np.zeros(n, np.int32)
+    size = np.zeros(n, np.int32)
+    unit_len = np.where(kind == 0, 2, 1)
+    start = np.r_[0, np.cumsum(unit_len)[:-1]]
+    ua = rng.integers(0, n_accounts, n_units).astype(np.int64) + aid_base
+    us = rng.integers(0, n_symbols, n_units).astype(np.int64) + sid_base
+    side = np.where(rng.random(n_units) < 0.5, BUY, SELL).astype(np.int32)
+    pp = start[kind == 0]
+    # cancel/replace pair: CANCEL then a fresh limit order from the same account
+    action[pp] = CANCEL
+    aid[pp] = ua[kind == 0]
+    action[pp + 1] = side[kind == 0]
+    aid[pp + 1] = ua[kind == 0]
+    sid[pp + 1] = us[kind == 0]
+    price[pp + 1] = rng.integers(30, 76, n_pairs)
+    size[pp + 1] = np.clip(np.floor(rng.normal(50, 10, n_pairs)), 1, 100)
+    bp = start[kind == 1]
+    bs = side[kind == 1]
+    action[bp] = bs
+    aid[bp] = ua[kind == 1]
+    sid[bp] = us[kind == 1]
+    price[bp] = np.where(bs == BUY, 75, 30)
+    size[bp] = rng.integers(5000, 50001, n_big)
+    oid = _unique_oids(n, oid_base)
+    is_can = action == CANCEL
+    oid = np.where(is_can, _cancel_targets(action, aid, oid, rng), oid)
+    return Orders(action, oid, aid, sid, price.astype(np.int32), size.astype(np.int32), np.zeros(n, bool))
+
+
+def funded_transfers_needed(n_orders: int, n_accounts: int, big: bool = False) -> int:
+    """TRANSFER(INT_MAX) count per account so that the conservative per-account reservation bound
+    (sum of max risks, refunds ignored) never exceeds the funding."""
+    per_acct = max(1, n_orders // max(1, n_accounts))
+    worst = per_acct * (50_000 * 70 if big else 100 * 100)
+    return max(1, int(math.ceil(2 * worst / INT_MAX)))
+
+
+def murmur2(data: bytes) -> int:
+    """Kafka's org.apache.kafka.common.utils.Utils.murmur2 (the default keyed partitioner)."""
+    length = len(data)
+    seed = 0x9747B28C
+    m = 0x5BD1E995
+    r = 24
+    h = (seed ^ length) & 0xFFFFFFFF
+    length4 = length // 4
+    for i in range(length4):
+        i4 = i * 4
+        k = (data[i4] & 0xFF) + ((data[i4 + 1] & 0xFF) << 8) + ((data[i4 + 2] & 0xFF) << 16) + ((data[i4 + 3] & 0xFF) << 24)
+        k = (k * m) & 0xFFFFFFFF
+        k ^= k >> r
+        k = (k * m) & 0xFFFFFFFF
+        h = (h * m) & 0xFFFFFFFF
+        h ^= k
+    rem = length % 4
+    if rem == 3:
+        h ^= (data[(length & ~3) + 2] & 0xFF) << 16
+    if rem >= 2:
+        h ^= (data[(length & ~3) + 1] & 0xFF) << 8
+    if rem >= 1:
+        h ^= data[length & ~3] & 0xFF
+        h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 15
+    return h
+
+
+def shard_of(sid: int, n_shards: int) -> int:
+    """toPositive(murmur2(utf8(decimal(|sid|)))) % n -- keyed like Kafka's default partitioner."""
+    return (murmur2(str(abs(int(sid))).encode()) & 0x7FFFFFFF) % n_shards

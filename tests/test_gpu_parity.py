@@ -1,0 +1,181 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the CPU restatement (oracle/).
+
+Bar: bit-exact MatchOut tape (byte-identical consumer.js text), bit-exact book stores, and in
+EXACT mode bit-exact ledger stores.  Sizes are ones the oracle finishes in well under a second.
+"""
+import numpy as np
+import pytest
+
+import hazards
+from kme import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _funded_engine(kme, G, accounts=4096, E=1 << 16, P=1 << 18):
+    return kme.Engine(kme.default_config(kme.MODE_FUNDED, max_symbols=G, max_epoch=E, max_resting=P,
+                                         max_accounts=accounts))
+
+
+def _exact_engine(kme, G=16, E=1 << 16, P=1 << 16):
+    return kme.Engine(kme.default_config(kme.MODE_EXACT, max_symbols=G, max_epoch=E, max_resting=P,
+                                         ledger_capacity=1 << 16))
+
+
+def _run_epochs(eng, orders, epoch):
+    text = []
+    for a in range(0, len(orders), epoch):
+        part = orders.slice(a, min(len(orders), a + epoch))
+        r = eng.process(part)
+        text.append(r.tape_json(part))
+    return "".join(text)
+
+
+def _first_diff(a: str, b: str) -> str:
+    la, lb = a.splitlines(), b.splitlines()
+    for k, (x, y) in enumerate(zip(la, lb)):
+        if x != y:
+            return f"line {k}: got {x!r} want {y!r}"
+    return f"length got {len(la)} want {len(lb)}"
+
+
+@pytest.mark.parametrize("seed,n_sym,epoch", [(1, 16, 4096), (2, 64, 1 << 14), (3, 1024, 1 << 16), (4, 3, 777)])
+def test_funded_uniform_tape_and_books(kme_mod, oracle_mod, seed, n_sym, epoch):
+    setup = W.funded_setup(512, range(1, n_sym + 1))
+    stream = W.uniform(60_000, n_symbols=n_sym, n_accounts=512, seed=seed)
+    allin = W.Orders.concat([setup, stream])
+    eng = _funded_engine(kme_mod, n_sym + 1, accounts=512)
+    got = _run_epochs(eng, allin, epoch)
+    o = oracle_mod.Oracle()
+    o.process(allin)
+    want = o.tape_text()
+    assert got == want, _first_diff(got, want)
+    assert eng.snapshot_books() == o.dump_books()
+
+
+def test_funded_cancel_replace_sweeps(kme_mod, oracle_mod):
+    n_sym, n_acc = 32, 256
+    stream = W.cancel_replace(20_000, n_symbols=n_sym, n_accounts=n_acc, seed=5)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1),
+                           transfers_per_account=W.funded_transfers_needed(len(stream), n_acc, big=True))
+    allin = W.Orders.concat([setup, stream])
+    eng = _funded_engine(kme_mod, n_sym + 1, accounts=n_acc)
+    got = _run_epochs(eng, allin, 5000)
+    o = oracle_mod.Oracle()
+    o.process(allin)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+
+
+def test_funded_zipf_hot_books(kme_mod, oracle_mod):
+    n_sym, n_acc = 512, 1024
+    stream = W.zipf(40_000, n_symbols=n_sym, n_accounts=n_acc, seed=9)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    allin = W.Orders.concat([setup, stream])
+    eng = _funded_engine(kme_mod, n_sym + 1, accounts=n_acc)
+    got = _run_epochs(eng, allin, 10_000)
+    o = oracle_mod.Oracle()
+    o.process(allin)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+
+
+@pytest.mark.parametrize("name", sorted(hazards.FUNDED_OK))
+def test_funded_hazards(kme_mod, oracle_mod, name):
+    orders = hazards.as_orders(hazards.streams()[name])
+    eng = _funded_engine(kme_mod, 8, accounts=16, E=1024, P=4096)
+    got = _run_epochs(eng, orders, 1024)
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+
+
+@pytest.mark.parametrize("name", sorted(hazards.streams()))
+@pytest.mark.parametrize("epoch", [3, 1024])
+def test_exact_hazards(kme_mod, oracle_mod, name, epoch):
+    orders = hazards.as_orders(hazards.streams()[name])
+    eng = _exact_engine(kme_mod, E=1024, P=4096)
+    got = _run_epochs(eng, orders, epoch)
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+
+
+@pytest.mark.parametrize("name,mode", [(n, m) for n in sorted(hazards.domain_streams()) for m in ("exact", "funded")
+                                       if not (m == "funded" and n == "price_126")])
+def test_domain_errors_match_reference_faults(kme_mod, oracle_mod, name, mode):
+    rows, detail = hazards.domain_streams()[name]
+    orders = hazards.as_orders(rows)
+    o = oracle_mod.Oracle()
+    with pytest.raises(oracle_mod.OracleError) as oe:
+        o.process(orders)
+    eng = _exact_engine(kme_mod, E=1024, P=4096) if mode == "exact" else _funded_engine(kme_mod, 8, 16, 1024, 4096)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        _run_epochs(eng, orders, 1024)
+    assert ke.value.status == 3 and ke.value.detail == detail
+    assert ke.value.index == oe.value.index
+
+
+@pytest.mark.parametrize("seed,epoch", [(1, 100_000), (2, 4096), (3, 997)])
+def test_exact_exchange_test_stream(kme_mod, oracle_mod, seed, epoch):
+    orders = W.exchange_test(30_000, seed=seed)
+    eng = _exact_engine(kme_mod, E=1 << 17, P=1 << 16)
+    got = _run_epochs(eng, orders, epoch)
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+
+
+def test_processor_json_roundtrip(kme_mod, oracle_mod):
+    """The Processor<String, Order> mirror fed the exchange_test.js wire format (string cancel
+    oids included) forwards exactly the reference's MatchOut records."""
+    orders = W.exchange_test(5_000, seed=11)
+    cfg = kme_mod.default_config(kme_mod.MODE_EXACT, max_symbols=8, max_epoch=2048, max_resting=1 << 14)
+    p = kme_mod.Processor(cfg, epoch_records=1000)
+    for line in orders.to_json_lines():
+        assert p.process_json(line) == 0
+    assert p.close() == 0
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    assert p.tape_text() == o.tape_text()
+    assert p.commits == (len(orders) + 999) // 1000
+
+
+def test_funded_unfunded_is_refused(kme_mod):
+    """Acceptance that depends on the ledger must not be decided in parallel."""
+    rows = hazards._setup(fund=100) + [(W.BUY, 1, 1, 1, 50, 10)]
+    eng = _funded_engine(kme_mod, 8, 16, 1024, 4096)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(hazards.as_orders(rows))
+    assert ke.value.status == 4
+
+
+def test_top_of_book(kme_mod, oracle_mod):
+    import torch
+
+    setup = W.funded_setup(64, range(1, 9))
+    stream = W.uniform(5000, n_symbols=8, n_accounts=64, seed=2)
+    eng = _funded_engine(kme_mod, 9, accounts=64)
+    eng.process(W.Orders.concat([setup, stream]))
+    tob = torch.zeros((9, 4), dtype=torch.int32, device="cuda")
+    eng.top_of_book(tob.data_ptr())
+    torch.cuda.synchronize()
+    eng.wait()
+    tob = tob.cpu().numpy()
+    # from the oracle's book dump: highest bid level of +g, lowest ask level of -g
+    o = oracle_mod.Oracle()
+    o.process(W.Orders.concat([setup, stream]))
+    books = {int(l.split()[1]): (int(l.split()[2]), int(l.split()[3])) for l in o.dump_books().splitlines()
+             if l.startswith("B ")}
+    for g in range(1, 9):
+        msb, lsb = books[g]
+        bits = [p for p in range(127) if ((lsb >> p) & 1 if p < 63 else (msb >> (p - 63)) & 1)]
+        assert tob[g, 0] == (max(bits) if bits else -1)
+        msb, lsb = books[-g]
+        bits = [p for p in range(127) if ((lsb >> p) & 1 if p < 63 else (msb >> (p - 63)) & 1)]
+        assert tob[g, 1] == (min(bits) if bits else -1)
