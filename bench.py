@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark of the matching hot path (BASELINE.json metric) on 1..N MI355X GPUs.
+
+One step = one epoch of E input records through the whole device pipeline (oid map, funded-ledger
+proof, cancel routing, radix partition by symbol group, per-group matching, trade compaction,
+oid-table upkeep, top-of-book snapshot; + an RCCL all-gather of top-of-book when N > 1).
+Inputs are resident in HBM before the timed region; outputs stay in HBM.
+
+Workload at N = 1: BASELINE.json configs[1] -- 1,024 symbols x 16M synthetic limit/cancel orders,
+uniform load (SURVEY.md §8d "C2").  For N > 1 every rank runs its own C2-shaped shard of symbols
+(weak scaling: symbol groups are independent), no collective in the data path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--epoch E] [--workload c2|c3|c4|c5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kafka-matching-engine_amd"))
+
+import torch  # noqa: E402  (first: one HIP runtime per process, see kme.lib)
+import torch.distributed as dist  # noqa: E402
+
+import kme  # noqa: E402
+from kme import workloads as W  # noqa: E402
+
+METRIC = "matched orders/sec (node) at 65,536 symbols; p99 epoch latency; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def algorithmic_bytes(st) -> int:
+    """SURVEY.md §8d byte model per epoch: 52 B per input record (36 B of Order information + 16 B
+    of result), 36 B per trade, 32 B per resting-order write, 32 B per maker node visited, 48 B per
+    successful cancel."""
+    return (52 * st.n_inputs + 36 * st.n_trades + 32 * st.n_rests + 32 * st.n_maker_visits
+            + 48 * st.n_cancel_ok)
+
+
+def make_workload(name: str, n_orders: int, rank: int):
+    seed = 1000 + rank
+    if name == "c2":
+        nsym, nacc = 1024, 4096
+        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        desc = "C2: 1,024 symbols x 16M uniform limit/cancel orders per GPU (BASELINE configs[1])"
+    elif name == "c3":
+        nsym, nacc = 8192, 8192
+        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        desc = "C3 shard: 65,536 symbols / 8 GPUs = 8,192 symbols per GPU, uniform"
+    elif name == "c4":
+        nsym, nacc = 8192, 8192
+        stream = W.zipf(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        desc = "C4 shard: Zipf(1.1) symbol popularity over 8,192 symbols per GPU, 21-level band"
+    elif name == "c5":
+        nsym, nacc = 1024, 4096
+        stream = W.cancel_replace(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        desc = "C5: 90% cancel/replace + 10% sweeping orders of 5k-50k, 1,024 symbols per GPU"
+    else:
+        raise SystemExit(f"unknown workload {name}")
+    setup = W.funded_setup(nacc, range(1, nsym + 1),
+                           transfers_per_account=W.funded_transfers_needed(n_orders, nacc, big=name == "c5"))
+    return setup, stream, nsym, nacc, desc
+
+
+def cpu_baseline(setup, stream, max_orders: int):
+    """The oracle (CPU restatement of KProcessor.MatchingEngine, single thread) on a bounded
+    prefix of the same stream.  The reference itself (Java/Kafka Streams) cannot run here."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    o = oracle.Oracle(keep_tape=False)
+    o.process(setup)
+    m = min(len(stream), max_orders)
+    part = stream.slice(0, m)
+    t0 = time.perf_counter()
+    o.process(part)
+    dt = time.perf_counter() - t0
+    n = part.n_orders()
+    return {"value": n / dt, "unit": "orders/s", "cores": 1, "kind": "port",
+            "sample": f"first {m:,} records ({n:,} BUY/SELL/CANCEL) of the same stream after setup, "
+                      f"C restatement of KProcessor.MatchingEngine with hash-map stores, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--epoch", type=int, default=1 << 20)
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    E = args.epoch
+    total = max(args.orders, (args.warmup + args.steps) * E)
+    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank)
+
+    cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
+                             max_resting=min(total, 1 << 30), max_trades=2 * E + (1 << 16),
+                             max_accounts=nacc, device=local_rank)
+    eng = kme.Engine(cfg)
+    stream_handle = torch.cuda.current_stream(dev).cuda_stream
+    eng.set_stream(stream_handle)
+    eng.enable_timing(True)
+    eng.process(setup)  # CREATE_BALANCE / TRANSFER / ADD_SYMBOL records (host path)
+
+    # inputs resident in HBM before timing
+    cols = {
+        "action": torch.from_numpy(stream.action).to(dev), "oid": torch.from_numpy(stream.oid).to(dev),
+        "aid": torch.from_numpy(stream.aid).to(dev), "sid": torch.from_numpy(stream.sid).to(dev),
+        "price": torch.from_numpy(stream.price).to(dev), "size": torch.from_numpy(stream.size).to(dev),
+    }
+    orders_per_epoch = [int(stream.slice(k * E, (k + 1) * E).n_orders()) for k in range(args.warmup + args.steps)]
+    tob = torch.zeros((nsym + 1, 4), dtype=torch.int32, device=dev)
+    tob_all = torch.zeros((world * (nsym + 1), 4), dtype=torch.int32, device=dev) if world > 1 else None
+
+    def epoch_ptrs(k):
+        return {name: t.data_ptr() + k * E * t.element_size() for name, t in cols.items()}
+
+    def run_epoch(k):
+        eng.submit_device(epoch_ptrs(k), E)
+        eng.top_of_book(tob.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(tob_all, tob)  # market-data snapshot over RCCL / xGMI
+        return eng.wait()
+
+    for k in range(args.warmup):
+        run_epoch(k)
+
+    lat, match_ms, bytes_alg, n_orders, n_trades = [], [], [], 0, 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        k = args.warmup + j
+        e0 = time.perf_counter()
+        st = run_epoch(k)
+        lat.append((time.perf_counter() - e0) * 1e3)
+        ph = eng.phase_times()
+        match_ms.append(ph["match"])
+        bytes_alg.append(algorithmic_bytes(st))
+        n_orders += int(st.n_orders)
+        n_trades += int(st.n_trades)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
+
+    stats = torch.tensor([elapsed, float(n_orders), float(n_trades)], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = stats[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        sums = stats[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed, n_orders_all, n_trades_all = float(t_max.item()), float(sums[0].item()), float(sums[1].item())
+    else:
+        n_orders_all, n_trades_all = float(n_orders), float(n_trades)
+
+    if rank == 0:
+        avg_match_s = float(np.mean(match_ms)) / 1e3
+        achieved = float(np.mean(bytes_alg)) / avg_match_s / 1e9 if avg_match_s > 0 else 0.0
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC,
+            "value": n_orders_all / elapsed,
+            "unit": "orders/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {"workload": desc, "symbols_per_gpu": nsym, "accounts": nacc, "epoch_records": E,
+                       "stream_records_per_gpu": total, "mode": "FUNDED (symbol groups in parallel)",
+                       "parallelism": f"symbol-sharded x{world}"},
+            "p99_epoch_ms": float(np.percentile(lat, 99)),
+            "p50_epoch_ms": float(np.percentile(lat, 50)),
+            "fills_per_s": 2 * n_trades_all / elapsed,
+            "trades_per_s": n_trades_all / elapsed,
+            "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
+            "roofline": {"kernel": "k_match", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",
+                         "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg))},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(setup, stream, args.cpu_sample)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,15 @@
 #pragma once
 #include <stdint.h>
 
+// Pointer members of the device structs live in the global address space (AS1) for the device
+// pass: same 64-bit layout as the host's plain pointers, but every access through them compiles to
+// global_load / global_store (not flat_*) even when the struct is read from HBM.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KG __attribute__((address_space(1)))
+#else
+#define KG
+#endif
+
 namespace kme {
 
 constexpr int NLEV = 128;          // price levels 0..126 (+1 pad)
@@ -82,52 +91,52 @@ struct DevState {
     int32_t G, mode, A, passes;
     uint32_t pool_cap, otab_mask, _pad0, ttmp_cap;
     uint32_t bal_mask, pos_mask, trades_cap, _pad;
-    GroupState* grp;
-    Level* lev;
-    Node* pool;
-    uint64_t* otab_key;
-    int32_t* otab_val;
+    KG GroupState* grp;
+    KG Level* lev;
+    KG Node* pool;
+    KG uint64_t* otab_key;
+    KG int32_t* otab_val;
     // FUNDED ledger
-    int64_t* acct_since;
-    int64_t* acct_lb;
-    int64_t* acct_need;
-    int64_t* acct_negx;
-    int64_t* acct_xfer;
+    KG int64_t* acct_since;
+    KG int64_t* acct_lb;
+    KG int64_t* acct_need;
+    KG int64_t* acct_negx;
+    KG int64_t* acct_xfer;
     // EXACT ledger
-    uint32_t* bal_state;
-    int64_t* bal_key;
-    int64_t* bal_val;
-    uint32_t* pos_state;
-    PosEntry* pos;
+    KG uint32_t* bal_state;
+    KG int64_t* bal_key;
+    KG int64_t* bal_val;
+    KG uint32_t* pos_state;
+    KG PosEntry* pos;
     // per-epoch scratch
-    uint64_t* emap_key;
-    int32_t* emap_val;
-    int32_t* route_grp;
-    int64_t* cancel_tgt;
-    int32_t* rest_slot;
-    uint8_t* acct_ok;
-    uint32_t* rkeys[2];
-    uint32_t* rvals[2];
-    uint32_t* ghist;
-    uint32_t* seg;
-    TradeTmp* ttmp;
-    unsigned long long* ctr;
+    KG uint64_t* emap_key;
+    KG int32_t* emap_val;
+    KG int32_t* route_grp;
+    KG int64_t* cancel_tgt;
+    KG int32_t* rest_slot;
+    KG uint8_t* acct_ok;
+    KG uint32_t* rkeys[2];
+    KG uint32_t* rvals[2];
+    KG uint32_t* ghist;
+    KG uint32_t* seg;
+    KG TradeTmp* ttmp;
+    KG unsigned long long* ctr;
 };
 
 struct EpochIO {
-    const int32_t* action;
-    const int64_t* oid;
-    const int64_t* aid;
-    const int64_t* sid;
-    const int32_t* price;
-    const int32_t* size;
-    int32_t* out_action;
-    int32_t* out_size;
-    int64_t* out_prev;
-    uint8_t* out_flags;
-    uint32_t* n_trades;
-    uint32_t* trade_off;
-    TradeRec* trades;
+    const KG int32_t* action;
+    const KG int64_t* oid;
+    const KG int64_t* aid;
+    const KG int64_t* sid;
+    const KG int32_t* price;
+    const KG int32_t* size;
+    KG int32_t* out_action;
+    KG int32_t* out_size;
+    KG int64_t* out_prev;
+    KG uint8_t* out_flags;
+    KG uint32_t* n_trades;
+    KG uint32_t* trade_off;
+    KG TradeRec* trades;
     uint32_t n;
     uint32_t trades_cap;
     int64_t seq_base;

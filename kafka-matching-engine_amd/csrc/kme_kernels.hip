@@ -172,7 +172,6 @@ KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
         unsigned long long prev = atomicCAS((unsigned long long*)&S.otab_key[h], 0ull, key);
         if (prev == 0) {
             S.otab_val[h] = slot;
-            atomicAdd(&S.ctr[C_OTAB_USED], 1ull);
             return true;
         }
         h = (h + 1) & S.otab_mask;
@@ -235,8 +234,8 @@ __global__ void k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
     if (lane_id() == 0 && nb) atomicAdd(&S.ctr[C_ORDERS], (unsigned long long)__popcll(nb));
 }
 
-KDEV void write_out(const EpochIO& io, uint32_t i, bool ok, int32_t size, bool has_prev, int64_t prev) {
-    io.out_action[i] = ok ? io.action[i] : (int32_t)REJECT;
+KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int32_t size, bool has_prev, int64_t prev) {
+    io.out_action[i] = ok ? action : (int32_t)REJECT;
     io.out_size[i] = size;
     io.out_prev[i] = has_prev ? prev : 0;
     io.out_flags[i] = has_prev ? (uint8_t)KME_OUT_HAS_PREV : (uint8_t)0;
@@ -283,7 +282,7 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
                     }
                 }
             }
-            write_out(io, j, ok, size, false, 0);
+            write_out(io, j, act, ok, size, false, 0);
             io.n_trades[j] = 0;
             __builtin_amdgcn_wave_barrier();
         }
@@ -361,7 +360,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     }
     S.route_grp[i] = grp;
     S.cancel_tgt[i] = tgt;
-    if (funded && direct) write_out(io, i, ok, io.size[i], false, 0);
+    if (funded && direct) write_out(io, i, a, ok, io.size[i], false, 0);
 }
 
 // ------------------------------------------------------------------ (1) stable radix partition
@@ -495,6 +494,47 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t* out, uint32_t L, con
 }
 
 // ------------------------------------------------------------------ (2) the matching core
+// One input record as the group / serial wavefront consumes it (wave-uniform, SGPR-resident).
+struct Rec {
+    uint32_t i;
+    int32_t action, price, size, acct_ok;
+    int64_t oid, aid, sid, tgt;
+};
+// 64 records staged across the lanes of a wavefront: lane l holds record k0 + l.  One gather per
+// 64 records replaces two dependent global round trips per record (perm[k], then the fields).
+struct Batch {
+    uint32_t i;
+    int32_t action, price, size, acct_ok;
+    int64_t oid, aid, sid, tgt;
+};
+KDEV int32_t rl32(int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
+KDEV int64_t rl64(int64_t v, int j) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+KDEV Batch load_batch(const DevState& S, const EpochIO& io, bool valid, uint32_t i, bool funded) {
+    Batch B;
+    B.i = i;
+    if (valid) {
+        B.action = io.action[i]; B.price = io.price[i]; B.size = io.size[i];
+        B.oid = io.oid[i]; B.aid = io.aid[i]; B.sid = io.sid[i];
+        B.tgt = S.cancel_tgt[i];
+        B.acct_ok = funded ? (int32_t)S.acct_ok[i] : 0;
+    } else {
+        B.action = -1; B.price = B.size = B.acct_ok = 0; B.oid = B.aid = B.sid = B.tgt = 0;
+    }
+    return B;
+}
+KDEV Rec pick(const Batch& B, int j) {
+    Rec r;
+    r.i = (uint32_t)rl32((int32_t)B.i, j);
+    r.action = rl32(B.action, j); r.price = rl32(B.price, j); r.size = rl32(B.size, j);
+    r.acct_ok = rl32(B.acct_ok, j);
+    r.oid = rl64(B.oid, j); r.aid = rl64(B.aid, j); r.sid = rl64(B.sid, j); r.tgt = rl64(B.tgt, j);
+    return r;
+}
+
 struct Taker {
     int32_t action, price, size, _pad;
     int64_t oid, aid, sid;
@@ -882,15 +922,16 @@ struct Core {
     }
 
     // ---------------- removeOrder, KP:289-323
-    KDEV bool remove_order(uint32_t i) {
-        const int64_t tgt = S.cancel_tgt[i];
+    KDEV bool remove_order(const Rec& r) {
+        const uint32_t i = r.i;
+        const int64_t tgt = r.tgt;
         int32_t slot = -1;
         if (tgt >= 0) slot = (int32_t)tgt;
         else if (tgt <= -2) slot = S.rest_slot[-(tgt + 2)];
         if (slot < 0) return false;
         const Node o = ld_node(slot);
-        if (!o.live || o.oid != io.oid[i]) return false;   // orders.get(oid) == null
-        if (o.aid != io.aid[i]) return false;              // order.aid != aid (KP:291)
+        if (!o.live || o.oid != r.oid) return false;       // orders.get(oid) == null
+        if (o.aid != r.aid) return false;                  // order.aid != aid (KP:291)
         if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK, i); return false; }
         const int64_t key = jlmul(o.sid, o.action == BUY ? 1 : -1);
         const int s = key < 0 ? 1 : 0;
@@ -927,11 +968,12 @@ struct Core {
     }
 
     // ---------------- one record of this group (MatchingEngine.process, KP:96-126)
-    KDEV void process(uint32_t i) {
-        const int32_t a = io.action[i];
+    KDEV void process(const Rec& r) {
+        const uint32_t i = r.i;
+        const int32_t a = r.action;
         bool ok = false, has_prev = false;
         int64_t prev_oid = 0;
-        int32_t out_size = io.size[i];
+        int32_t out_size = r.size;
         uint32_t ntr = 0;
         if (EXACT) io.trade_off[i] = tnext;
         switch (a) {
@@ -941,12 +983,12 @@ struct Core {
         case REMOVE_SYMBOL:
         case PAYOUT: {
             if (exists) {
-                if (remove_symbol_existing(io.sid[i]) == 2) { die(KME_E_DOMAIN, KME_D_HANG, i); return; }
+                if (remove_symbol_existing(r.sid) == 2) { die(KME_E_DOMAIN, KME_D_HANG, i); return; }
                 ok = false;                                 // removeAllOrders(sid) returned true
             } else {
                 ok = a == REMOVE_SYMBOL;
                 if (a == PAYOUT) {
-                    if (EXACT) payout_settle(io.sid[i], io.size[i], i);
+                    if (EXACT) payout_settle(r.sid, r.size, i);
                     else die(KME_E_UNSUPPORTED, KME_D_NONE, i);
                     if (dead) return;
                 }
@@ -958,12 +1000,12 @@ struct Core {
         case SELL: {
             if (!exists) break;                             // books.get(sid) == null
             Taker t;
-            t.action = a; t.price = io.price[i]; t.size = io.size[i]; t._pad = 0;
-            t.oid = io.oid[i]; t.aid = io.aid[i]; t.sid = io.sid[i];
+            t.action = a; t.price = r.price; t.size = r.size; t._pad = 0;
+            t.oid = r.oid; t.aid = r.aid; t.sid = r.sid;
             if (EXACT) {
                 if (!check_balance(t, i)) { if (dead) return; break; }
             } else {
-                if (!S.acct_ok[i]) break;                   // balances.get(aid) == null
+                if (!r.acct_ok) break;                      // balances.get(aid) == null
             }
             const bool filled = try_match(i, t, ntr);
             if (dead) return;
@@ -973,14 +1015,14 @@ struct Core {
             break;
         }
         case CANCEL:
-            ok = remove_order(i);
+            ok = remove_order(r);
             if (dead) return;
             break;
         default:
             break;
         }
         if (lane_id() == 0) {
-            write_out(io, i, ok, out_size, has_prev, prev_oid);
+            write_out(io, i, a, ok, out_size, has_prev, prev_oid);
             if (!EXACT) io.n_trades[i] = ntr;
         }
     }
@@ -1009,7 +1051,15 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     Core<false, true> c(S, io, cache, cmask);
     c.load_group(g);
     const uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
-    for (uint32_t k = b; k < e && !c.dead; ++k) c.process(perm[k]);
+    const int lane = lane_id();
+    for (uint32_t k0 = b; k0 < e && !c.dead; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool valid = k < e;
+        const Batch B = load_batch(S, io, valid, valid ? perm[k] : 0, true);
+        const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
+#pragma nounroll
+        for (int j = 0; j < nb && !c.dead; ++j) c.process(pick(B, j));
+    }
     c.close_trade_chunk();
     c.store_group();
     c.flush_stats();
@@ -1021,29 +1071,40 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     const EpochIO& io = *iop;
     if (failed(S.ctr)) return;
     Core<true, false> c(S, io, nullptr, nullptr);
-    for (uint32_t i = 0; i < io.n && !c.dead; ++i) {
-        const int32_t a = io.action[i];
-        int32_t grp = -1;
-        if (a == CANCEL) grp = S.route_grp[i];
-        else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) grp = group_of(io.sid[i], S.G);
-        if (grp >= 0) {
-            if (grp != c.g) { c.store_group(); c.load_group(grp); }
-            c.process(i);
-            continue;
+    const int lane = lane_id();
+    for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool valid = k < io.n;
+        const Batch B = load_batch(S, io, valid, valid ? k : 0, false);
+        const int32_t bgrp = valid ? S.route_grp[k] : -1;
+        const int nb = (int)(io.n - k0 < 64 ? io.n - k0 : 64);
+#pragma nounroll
+        for (int j = 0; j < nb && !c.dead; ++j) {
+            const Rec r = pick(B, j);
+            const uint32_t i = r.i;
+            const int32_t a = r.action;
+            int32_t grp = -1;
+            if (a == CANCEL) grp = rl32(bgrp, j);
+            else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) grp = group_of(r.sid, S.G);
+            if (grp >= 0) {
+                if (grp != c.g) { c.store_group(); c.load_group(grp); }
+                c.process(r);
+                continue;
+            }
+            // records without a symbol group
+            io.trade_off[i] = c.tnext;
+            bool ok = false;
+            switch (a) {
+            case CREATE_BALANCE: ok = c.create_balance(r.aid, i); break;
+            case TRANSFER: ok = c.transfer(r.aid, r.size); break;
+            case ADD_SYMBOL: c.die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, i); break;
+            case REMOVE_SYMBOL: ok = true; break;           // absent symbol: removeSymbol returns true
+            case PAYOUT: c.payout_settle(r.sid, r.size, i); break;
+            default: break;                                 // BUY/SELL on absent book, unknown cancel, unknown action
+            }
+            if (c.dead) break;
+            if (lane == 0) write_out(io, i, a, ok, r.size, false, 0);
         }
-        // records without a symbol group
-        io.trade_off[i] = c.tnext;
-        bool ok = false;
-        switch (a) {
-        case CREATE_BALANCE: ok = c.create_balance(io.aid[i], i); break;
-        case TRANSFER: ok = c.transfer(io.aid[i], io.size[i]); break;
-        case ADD_SYMBOL: c.die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, i); break;
-        case REMOVE_SYMBOL: ok = true; break;               // absent symbol: removeSymbol returns true
-        case PAYOUT: c.payout_settle(io.sid[i], io.size[i], i); break;
-        default: break;                                     // BUY/SELL on absent book, unknown cancel, unknown action
-        }
-        if (c.dead) break;
-        if (lane_id() == 0) write_out(io, i, ok, io.size[i], false, 0);
     }
     c.store_group();
     if (lane_id() == 0) {
@@ -1069,22 +1130,35 @@ __global__ void k_scatter(DevState S, EpochIO io, const uint32_t* total) {
 }
 
 // ------------------------------------------------------------------ oid-table maintenance
+// Orders that came to rest this epoch and are still live get an oid-table entry.  The used-slot
+// counter is bumped once per wavefront (a single hot counter would serialise every insert).
 __global__ void k_table(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= io.n) return;
-    const int32_t s = S.rest_slot[i];
-    if (s < 0) return;
-    const Node& nd = S.pool[s];
-    if (nd.live && nd.oid == io.oid[i]) {
-        if (!otab_insert(S, io.oid[i], s)) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, i);
+    bool ins = false;
+    if (i < io.n) {
+        const int32_t s = S.rest_slot[i];
+        if (s >= 0) {
+            const int64_t oid = io.oid[i];
+            if (S.pool[s].live && S.pool[s].oid == oid) {
+                ins = otab_insert(S, oid, s);
+                if (!ins) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, i);
+            }
+        }
     }
+    const unsigned long long b = __ballot(ins);
+    if (lane_id() == 0 && b) atomicAdd(&S.ctr[C_OTAB_USED], (unsigned long long)__popcll(b));
 }
 __global__ void k_otab_refill(DevState S, uint32_t nslots) {
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x) {
-        const Node& nd = S.pool[s];
-        if (nd.live) {
-            if (!otab_insert(S, nd.oid, (int32_t)s)) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t lim = (nslots + stride - 1) / stride * stride;   // whole wavefronts for the ballot
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < lim; s += stride) {
+        bool ins = false;
+        if (s < nslots && S.pool[s].live) {
+            ins = otab_insert(S, S.pool[s].oid, (int32_t)s);
+            if (!ins) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
         }
+        const unsigned long long b = __ballot(ins);
+        if (lane_id() == 0 && b) atomicAdd(&S.ctr[C_OTAB_USED], (unsigned long long)__popcll(b));
     }
 }
 

@@ -1,0 +1,146 @@
+"""CPU tests of the C ABI surface and the host-side logic of libkme.so (no device compute).
+
+* the shared object loads (no undefined symbols) and exports every function include/kme.h and
+  include/kme_processor.h declare;
+* struct layouts seen by C (gcc on the public headers) match the ctypes mirror;
+* the Jackson-compatible deserializer and the tape serializer (KP:477-521), the Kafka murmur2
+  partitioner;
+* creating an engine without a GPU fails loudly (no CPU fallback exists).
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from kme import workloads as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in ("kme.h", "kme_processor.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(kme_[a-z_]+)\s*\(", txt))
+    return names
+
+
+def test_library_loads_and_exports_every_declared_symbol(kme_mod):
+    lib = C.CDLL(kme_mod.LIB_PATH)  # raises on undefined symbols
+    declared = declared_functions()
+    assert declared == set(kme_mod.EXPORTS)
+    nm = subprocess.run(["nm", "-D", "--defined-only", kme_mod.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (kme_[a-z_]+)$", nm, flags=re.M))
+    missing = declared - exported
+    assert not missing, missing
+    for name in declared:
+        getattr(lib, name)
+
+
+def test_struct_layouts_match_the_header(kme_mod, tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kme.h"\n'
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(kme_config), sizeof(kme_orders),'
+                   'sizeof(kme_trade), sizeof(kme_epoch_result), sizeof(kme_epoch_status), sizeof(kme_tob),'
+                   'offsetof(kme_epoch_status, n_orders));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [C.sizeof(kme_mod.kme_config), C.sizeof(kme_mod.kme_orders), kme_mod.TRADE_DTYPE.itemsize,
+            C.sizeof(kme_mod.kme_epoch_result), C.sizeof(kme_mod.kme_epoch_status), kme_mod.TOB_DTYPE.itemsize,
+            kme_mod.kme_epoch_status.n_orders.offset]
+    assert got == want
+
+
+@pytest.mark.parametrize("text,want", [
+    ('{"action":2,"oid":123,"aid":1,"sid":0,"price":50,"size":49}', (2, 123, 1, 0, 50, 49)),
+    ('{"action":4,"oid":"8796093022208","aid":3,"sid":0,"price":0,"size":0}', (4, 8796093022208, 3, 0, 0, 0)),
+    ('{"action":2,"oid":5,"aid":1,"sid":-2,"price":50.9,"size":-3,"next":null,"prev":null}', (2, 5, 1, -2, 50, -3)),
+    ('{"aid":7}', (0, 0, 7, 0, 0, 0)),                                   # missing creator props -> 0
+    (' { "size" : "12" , "action" : 3 } ', (3, 0, 0, 0, 0, 12)),
+    ('{"action":2,"oid":9223372036854775807,"aid":-9223372036854775808,"sid":1,"price":2147483647,"size":-2147483648}',
+     (2, 9223372036854775807, -9223372036854775808, 1, 2147483647, -2147483648)),
+])
+def test_json_deserializer_follows_jackson_defaults(kme_mod, text, want):
+    assert kme_mod.order_from_json(text) == want
+
+
+@pytest.mark.parametrize("text,status", [
+    ('{"action":2,"oid":1,"bogus":1}', 1),              # FAIL_ON_UNKNOWN_PROPERTIES
+    ('{"action":true}', 1),
+    ('{"price":2147483648}', 1),                        # int overflow
+    ('{"oid":9223372036854775808}', 1),
+    ('{"action":2', 1),
+    ('{"action":2,"next":17}', 3),                      # linked input orders are outside the domain
+])
+def test_json_deserializer_rejects(kme_mod, text, status):
+    with pytest.raises(kme_mod.KmeError) as e:
+        kme_mod.order_from_json(text)
+    assert e.value.status == status
+
+
+def test_murmur2_partitioner_matches_python_restatement(kme_mod):
+    for sid in list(range(-50, 2000)) + [2**31, 2**40 + 7, -(2**62), 9223372036854775807]:
+        for n in (1, 2, 3, 4, 8, 13):
+            assert kme_mod.shard_of(sid, n) == W.shard_of(sid, n)
+
+
+def test_tape_serializer_layout(kme_mod):
+    """Hand-built result of one BUY that traded twice and rested; serialised like consumer.js."""
+    orders = W.Orders.from_rows([(2, 77, 3, 5, 60, 10)])
+    trades = np.zeros(2, kme_mod.TRADE_DTYPE)
+    trades[0] = (11, 1, 5, 55, 4)
+    trades[1] = (12, 2, 5, 58, 3)
+    res = kme_mod.EpochResult(np.array([2], np.int32), np.array([3], np.int32), np.array([66], np.int64),
+                              np.array([1], np.uint8), np.array([0, 2], np.uint32), trades, kme_mod.kme_epoch_status())
+    want = ('IN {"action":2,"oid":77,"aid":3,"sid":5,"price":60,"size":10,"next":null,"prev":null}\n'
+            'OUT {"action":6,"oid":11,"aid":1,"sid":5,"price":0,"size":4,"next":null,"prev":null}\n'
+            'OUT {"action":5,"oid":77,"aid":3,"sid":5,"price":5,"size":4,"next":null,"prev":null}\n'
+            'OUT {"action":6,"oid":12,"aid":2,"sid":5,"price":0,"size":3,"next":null,"prev":null}\n'
+            'OUT {"action":5,"oid":77,"aid":3,"sid":5,"price":2,"size":3,"next":null,"prev":null}\n'
+            'OUT {"action":2,"oid":77,"aid":3,"sid":5,"price":60,"size":3,"next":null,"prev":66}\n')
+    assert res.tape_json(orders) == want
+
+
+def test_tape_serializer_agrees_with_oracle_on_echo_records(kme_mod, oracle_mod):
+    """Records that never trade: the serializer's IN/OUT echo equals the oracle's Jackson output."""
+    rows = [(100, 0, 1, 0, 0, 0), (101, 0, 1, 0, 0, -5), (0, 0, 0, -3, 0, 0), (42, -1, -2, -3, -4, -5),
+            (4, 2**62, 1, 0, 0, 0)]
+    orders = W.Orders.from_rows(rows)
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    tape = o.tape()
+    outs = tape[tape["key"] == 1]
+    n = len(orders)
+    res = kme_mod.EpochResult(outs["action"].astype(np.int32), outs["size"].astype(np.int32), np.zeros(n, np.int64),
+                              np.zeros(n, np.uint8), np.zeros(n + 1, np.uint32), np.zeros(0, kme_mod.TRADE_DTYPE),
+                              kme_mod.kme_epoch_status())
+    assert res.tape_json(orders) == o.tape_text()
+
+
+def test_status_strings(kme_mod):
+    L = kme_mod.lib()
+    for s in range(8):
+        assert L.kme_strerror(s)
+    assert b"KP:341-353" in L.kme_domain_str(5)
+
+
+def test_engine_creation_fails_loudly_without_gpu(kme_mod):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(kme_mod.KmeError) as e:
+        kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, 8, 1024, 1024, max_accounts=8))
+    assert e.value.status == 6                                   # KME_E_HIP: no CPU fallback
+
+
+def test_invalid_config_rejected_before_touching_the_device(kme_mod):
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, 8, 1024, 1024, max_accounts=0)
+    with pytest.raises(kme_mod.KmeError) as e:
+        kme_mod.Engine(cfg)
+    assert e.value.status == 1

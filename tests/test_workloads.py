@@ -1,0 +1,64 @@
+"""Properties of the synthetic streams that the parity and bench runs rely on."""
+import numpy as np
+
+from kme import workloads as W
+
+
+def test_exchange_test_shape():
+    o = W.exchange_test(20_000, seed=2)
+    a = o.action
+    # setup: 10 x (CREATE_BALANCE, TRANSFER), then ADD_SYMBOL 0, 1, 2 (exchange_test.js:23-32)
+    assert list(a[:20:2]) == [W.CREATE_BALANCE] * 10 and list(a[1:20:2]) == [W.TRANSFER] * 10
+    assert list(a[20:23]) == [W.ADD_SYMBOL] * 3 and list(o.sid[20:23]) == [0, 1, 2]
+    ev = a[23:]
+    frac = {k: float(np.mean(ev == k)) for k in (W.BUY, W.SELL, W.CANCEL)}
+    assert abs(frac[W.BUY] - 0.332) < 0.02 and abs(frac[W.SELL] - 0.332) < 0.02
+    assert abs(frac[W.CANCEL] - 0.334) < 0.02
+    # cancels name an earlier order with its owner's aid, as a JSON string
+    first = {}
+    for i in range(23, len(o)):
+        if a[i] in (W.BUY, W.SELL):
+            first.setdefault(int(o.oid[i]), (i, int(o.aid[i])))
+        elif a[i] == W.CANCEL and o.oid[i] != 0:
+            j, aid = first[int(o.oid[i])]
+            assert j < i and aid == o.aid[i] and o.oid_is_string[i]
+
+
+def test_uniform_stream_properties():
+    o = W.uniform(200_000, n_symbols=64, n_accounts=256, seed=4)
+    bs = (o.action == W.BUY) | (o.action == W.SELL)
+    assert len(np.unique(o.oid[bs])) == bs.sum()                  # unique live oids
+    assert o.price[bs].min() >= 30 and o.price[bs].max() <= 75      # H5-safe band
+    assert o.size[bs].min() >= 1 and o.size[bs].max() <= 100
+    assert o.sid[bs].min() == 1 and o.sid[bs].max() == 64
+    pos = {int(x): i for i, x in enumerate(o.oid) if bs[i]}
+    can = np.nonzero(o.action == W.CANCEL)[0]
+    for i in can[:5000]:
+        if o.oid[i] == 0:
+            continue
+        j = pos[int(o.oid[i])]
+        assert j < i and o.aid[j] == o.aid[i]
+
+
+def test_cancel_replace_pairs_and_sweeps():
+    o = W.cancel_replace(50_000, n_symbols=32, n_accounts=64, seed=3)
+    c = np.nonzero(o.action == W.CANCEL)[0]
+    assert abs(len(c) / len(o) - 0.45) < 0.01
+    assert np.all(o.aid[c + 1] == o.aid[c]) and np.all(np.isin(o.action[c + 1], (W.BUY, W.SELL)))
+    big = (o.size >= 5000)
+    assert abs(big.mean() - 0.10) < 0.01
+    assert set(np.unique(o.price[big])) <= {30, 75}
+
+
+def test_zipf_is_skewed():
+    o = W.zipf(100_000, n_symbols=4096, n_accounts=1024, seed=1)
+    s = o.sid[o.action != W.CANCEL]
+    counts = np.bincount(s)
+    top = np.sort(counts)[::-1]
+    assert top[0] > 50 * np.median(counts[counts > 0])
+
+
+def test_funded_setup_covers_worst_case_reservations():
+    n, acc = 1_000_000, 64
+    k = W.funded_transfers_needed(n, acc, big=True)
+    assert k * W.INT_MAX >= 2 * (n // acc) * 50_000 * 70
