@@ -25,6 +25,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kafka-matching-engine_amd"))
 
+if "--stamps" in sys.argv:  # diagnostic build with in-kernel s_memtime stamps (never the bench line)
+    os.environ["KME_LIB"] = os.path.join(ROOT, "kafka-matching-engine_amd", "kme", "libkme_stamps.so")
+
 import torch  # noqa: E402  (first: one HIP runtime per process, see kme.lib)
 import torch.distributed as dist  # noqa: E402
 
@@ -97,6 +100,7 @@ def main():
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,6 +148,7 @@ def main():
         run_epoch(k)
 
     lat, match_ms, bytes_alg, n_orders, n_trades = [], [], [], 0, 0
+    mix = {"inputs": 0, "trades": 0, "rests": 0, "maker_visits": 0, "cancels_ok": 0}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -158,6 +163,9 @@ def main():
         bytes_alg.append(algorithmic_bytes(st))
         n_orders += int(st.n_orders)
         n_trades += int(st.n_trades)
+        for name, v in (("inputs", st.n_inputs), ("trades", st.n_trades), ("rests", st.n_rests),
+                     ("maker_visits", st.n_maker_visits), ("cancels_ok", st.n_cancel_ok)):
+            mix[name] += int(v)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -165,6 +173,26 @@ def main():
     elapsed = t1 - t0
     assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
 
+    if args.stamps:
+        d = eng.debug_counters().astype(np.float64)
+        tot = d.sum(axis=0)
+        names = ["batch_load", "buy_sell", "cancel", "other", "try_match", "rest", "out_lanes", "kernel", "n_buy_sell",
+                 "n_cancel"]
+        cyc = {n: tot[q] for q, n in enumerate(names)}
+        per = {"cycles_per_buy_sell": cyc["buy_sell"] / max(1, cyc["n_buy_sell"]),
+               "cycles_per_cancel": cyc["cancel"] / max(1, cyc["n_cancel"]),
+               "try_match_per_buy_sell": cyc["try_match"] / max(1, cyc["n_buy_sell"]),
+               "rest_per_buy_sell": cyc["rest"] / max(1, cyc["n_buy_sell"]),
+               "share_of_kernel": {n: cyc[n] / cyc["kernel"] for n in names[:7]},
+               "try_match_pre_loop_per_buy_sell": tot[10] / max(1, cyc["n_buy_sell"]),
+               "node_load_per_visit": tot[11] / max(1, tot[14]),
+               "emit_per_trade": tot[12] / max(1, tot[14]),
+               "post_trade_per_trade": tot[13] / max(1, tot[14]),
+               "alloc_per_rest": tot[15],
+               "visits": tot[14],
+               "kernel_cycles_per_wave_mean": cyc["kernel"] / max(1, int((d[:, 7] > 0).sum()))}
+        print(json.dumps({"stamps": per}), flush=True)
+        return
     stats = torch.tensor([elapsed, float(n_orders), float(n_trades)], dtype=torch.float64, device=dev)
     if world > 1:
         t_max = stats[0:1].clone()
@@ -204,6 +232,7 @@ def main():
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
+            "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             "roofline": {"kernel": "k_match", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",

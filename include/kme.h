@@ -194,6 +194,10 @@ kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, in
 /* Kafka's default keyed partitioner over decimal(|sid|) (murmur2, toPositive, % n). */
 uint32_t kme_shard_of(int64_t sid, uint32_t n_shards);
 
+/* Diagnostics: per-symbol-group words written by a -DKME_STAMPS build of the match kernel
+ * (in-kernel s_memtime stamps; zero in the product build).  Copies min(n, max_symbols * 16). */
+kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n);
+
 const char* kme_strerror(int status);
 const char* kme_domain_str(int detail);
 

@@ -121,6 +121,7 @@ struct DevState {
     KG uint32_t* seg;
     KG TradeTmp* ttmp;
     KG unsigned long long* ctr;
+    KG unsigned long long* dbg;     // diagnostic stamps (KME_STAMPS builds), G x 16 words
 };
 
 struct EpochIO {

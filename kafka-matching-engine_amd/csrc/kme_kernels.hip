@@ -44,7 +44,30 @@ KDEV int64_t lmin(int64_t a, int64_t b) { return a <= b ? a : b; }
 KDEV int32_t imin(int32_t a, int32_t b) { return a <= b ? a : b; }
 
 KDEV int lane_id() { return (int)(threadIdx.x & 63); }
-KDEV unsigned long long bcast64(unsigned long long v) { return (unsigned long long)__shfl((long long)v, 0); }
+
+// Diagnostic build only (-DKME_STAMPS): s_memtime stamps accumulated per category in SGPRs and
+// written to DevState::dbg at the end of k_match (cdna_hip_programming.md §7 "In-kernel stamps").
+// Quote the shares, not the run time, of that build.
+#ifdef KME_STAMPS
+KDEV unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define KST(x) x
+#else
+#define KST(x)
+#endif
+// Broadcast lane 0's value with readfirstlane (SGPR result): the compiler then knows it is
+// wave-uniform.  (__shfl lowers to ds_bpermute, whose result the divergence analysis treats as
+// per-lane; everything computed from it would turn into exec-masked VALU code.)
+KDEV unsigned long long bcast64(unsigned long long v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
 
 KDEV uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -508,6 +531,8 @@ struct Batch {
     int64_t oid, aid, sid, tgt;
 };
 KDEV int32_t rl32(int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
+// lane j of v := x (v_cmp + v_cndmask; x and j are wave-uniform)
+KDEV int32_t lane_put(int32_t x, int j, int32_t v) { return lane_id() == j ? x : v; }
 KDEV int64_t rl64(int64_t v, int j) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
@@ -540,6 +565,17 @@ struct Taker {
     int64_t oid, aid, sid;
 };
 
+// What process() decided for one record (the OUT echo fields and its trade count).
+struct Out {
+    int32_t action, size;
+    int64_t prev;
+    bool has_prev;
+    uint32_t ntr;
+};
+
+constexpr int FSTACK = 256;       // LDS free-slot stack of a group wavefront
+constexpr int DIRTY_WORDS = 64;   // 2048-bit per-batch filter of node slots written in the batch
+
 // Book state of the current symbol group, held in registers (bitmaps, free list) and, for the
 // parallel kernel, price levels staged in LDS on first touch and written back at the end.
 template <bool EXACT, bool LDS>
@@ -550,17 +586,25 @@ struct Core {
     int32_t g;
     int32_t exists;
     uint64_t b0l, b0m, b1l, b1m;      // bitmaps of book +g (side 0) and book -g (side 1)
-    uint64_t* cmask;                  // LDS [4]: cached-level masks (side * 2 + (p >= 64))
+    int32_t* fstack;                  // LDS free-slot stack (LDS == true)
+    int32_t fsp;
+    uint32_t* dirty;                  // LDS per-batch written-slot filter (LDS == true)
+    Node* nodepf;                     // LDS cancel-target nodes prefetched with the batch (LDS == true)
     int32_t free_head, chunk_next, chunk_end;
     Level* glev;
     uint32_t tnext, tend;             // FUNDED: trade scratch chunk; EXACT: running trade count
     unsigned long long s_trades, s_rests, s_visits, s_cancel;
     bool dead;
+#ifdef KME_STAMPS
+    unsigned long long acc[16];
+#endif
 
-    KDEV Core(const DevState& s, const EpochIO& e, Level* c, uint64_t* cm) : S(s), io(e), cache(c), cmask(cm) {
-        g = -1; exists = 0; b0l = b0m = b1l = b1m = 0;
+    KDEV Core(const DevState& s, const EpochIO& e, Level* c, int32_t* fs, uint32_t* dty, Node* npf)
+        : S(s), io(e), cache(c), fstack(fs), dirty(dty), nodepf(npf) {
+        g = -1; exists = 0; b0l = b0m = b1l = b1m = 0; fsp = 0;
         free_head = -1; chunk_next = chunk_end = 0; glev = nullptr;
         tnext = tend = 0; s_trades = s_rests = s_visits = s_cancel = 0; dead = false;
+        KST(for (int q = 0; q < 16; ++q) acc[q] = 0;)
     }
 
     KDEV void die(int status, int detail, int64_t idx) { raise_wave(S.ctr, status, detail, idx); dead = true; }
@@ -572,12 +616,34 @@ struct Core {
         b0l = G.bm0_lsb; b0m = G.bm0_msb; b1l = G.bm1_lsb; b1m = G.bm1_msb;
         free_head = G.free_head; chunk_next = G.chunk_next; chunk_end = G.chunk_end;
         glev = S.lev + (size_t)gg * 2 * NLEV;
-        if (LDS) { cmask[0] = 0; cmask[1] = 0; cmask[2] = 0; cmask[3] = 0; }
+        fsp = 0;
+        if (LDS) stage_levels(true);
+    }
+    // Occupied levels of both books move between HBM and LDS in one parallel pass (lane l takes
+    // prices l and l + 64); an unoccupied level's fields are dead until a rest rewrites them all.
+    KDEV void stage_levels(bool in) {
+        const int lane = lane_id();
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const uint64_t l = side ? b1l : b0l, m = side ? b1m : b0m;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int p = lane + 64 * h;
+                if (p <= 126 && check_bit(l, m, p)) {
+                    int4* c = reinterpret_cast<int4*>(&cache[side * NLEV + p]);
+                    int4* gl = reinterpret_cast<int4*>(&glev[side * NLEV + p]);
+                    if (in) { const int4 x0 = gl[0], x1 = gl[1]; c[0] = x0; c[1] = x1; }
+                    else { const int4 x0 = c[0], x1 = c[1]; gl[0] = x0; gl[1] = x1; }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
     KDEV void store_group() {
         if (g < 0) return;
         if (LDS) {
-            flush_mask(0, 0, cmask[0]); flush_mask(0, 64, cmask[1]); flush_mask(1, 0, cmask[2]); flush_mask(1, 64, cmask[3]);
+            stage_levels(false);
+            flush_free_stack();
         }
         {
             GroupState& G = S.grp[g];
@@ -586,38 +652,12 @@ struct Core {
             G.free_head = free_head; G.chunk_next = chunk_next; G.chunk_end = chunk_end;
         }
     }
-    KDEV void flush_mask(int side, int off, uint64_t m) {
-        // written back in parallel: lane l copies 16 B of level (l >> 1)
-        while (m) {
-            const int p0 = __builtin_ctzll(m);
-            m &= m - 1;
-            const int lane = lane_id();
-            if (lane < 2) {
-                const int4* src = reinterpret_cast<const int4*>(&cache[side * NLEV + off + p0]);
-                int4* dst = reinterpret_cast<int4*>(&glev[side * NLEV + off + p0]);
-                dst[lane] = src[lane];
-            }
-        }
-    }
-
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
     KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
     KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
 
     KDEV Level* lv(int side, int32_t p) {
-        if (!LDS) return &glev[side * NLEV + p];
-        const uint64_t bit = 1ull << (p & 63);
-        const int mi = side * 2 + (p >= 64 ? 1 : 0);
-        const uint64_t m = cmask[mi];
-        Level* dst = &cache[side * NLEV + p];
-        if (!(m & bit)) {
-            const int4* src = reinterpret_cast<const int4*>(&glev[side * NLEV + p]);
-            const int4 x0 = src[0], x1 = src[1];
-            reinterpret_cast<int4*>(dst)[0] = x0;
-            reinterpret_cast<int4*>(dst)[1] = x1;
-            cmask[mi] = m | bit;
-        }
-        return dst;
+        return LDS ? &cache[side * NLEV + p] : &glev[side * NLEV + p];
     }
 
     KDEV Node ld_node(int32_t s) const {
@@ -629,7 +669,10 @@ struct Core {
         return n;
     }
 
+    // Node slots: LDS stack of slots freed by this wavefront first (no dependent global load), then
+    // the group's global free list, then a chunk from the pool's bump counter.
     KDEV int32_t alloc_slot(int64_t idx) {
+        if (LDS && fsp > 0) return fstack[--fsp];
         if (free_head >= 0) {
             const int32_t s = free_head;
             free_head = S.pool[s].next;
@@ -647,8 +690,34 @@ struct Core {
     }
     KDEV void free_slot(int32_t s) {
         S.pool[s].live = 0;
+        mark_dirty(s);
+        if (LDS && fsp < FSTACK) {
+            fstack[fsp++] = s;
+            return;
+        }
         S.pool[s].next = free_head;
         free_head = s;
+    }
+    // The LDS stack joins the global free list when the group is written back: entry k links to
+    // entry k - 1, the bottom entry to the old list head (all lanes in parallel, stores only).
+    KDEV void flush_free_stack() {
+        if (!LDS || fsp == 0) return;
+        for (int k = lane_id(); k < fsp; k += 64) {
+            const int32_t sl = fstack[k];
+            S.pool[sl].next = k == 0 ? free_head : fstack[k - 1];
+        }
+        free_head = fstack[fsp - 1];
+        fsp = 0;
+    }
+    // Per-batch filter of node slots written since the batch's cancel-target prefetch.
+    KDEV void mark_dirty(int32_t s) {
+        if (!LDS) return;
+        if (lane_id() == 0)
+            __hip_atomic_fetch_or(&dirty[(s >> 5) & (DIRTY_WORDS - 1)], 1u << (s & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    KDEV bool is_dirty(int32_t s) const {
+        return (dirty[(s >> 5) & (DIRTY_WORDS - 1)] >> (s & 31)) & 1u;
     }
 
     // ---------------- exact ledger (EXACT only): device hash tables, one wavefront, plain loads
@@ -838,6 +907,7 @@ struct Core {
 
     // ---------------- tryMatch, KP:225-263
     KDEV bool try_match(uint32_t i, Taker& t, uint32_t& ntr) {
+        KST(unsigned long long tq = stamp();)
         const bool is_buy = t.action == BUY;
         const int64_t key = jlmul(t.sid, is_buy ? 1 : -1);
         const int os = jlneg(key) < 0 ? 1 : 0;           // opposite book (the same book for sid 0)
@@ -848,22 +918,33 @@ struct Core {
         Level* L = lv(os, pb);
         int32_t ms = L->head;
         if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
-        Node m = ld_node(ms);
-        s_visits++;
+        // A maker's price is the index of the level it rests in, so the loop test of KP:237 --
+        // ((size > 0 && isBuy) ? maker.price <= P : maker.price >= P), H3 -- needs no node load;
+        // the node is read only when a trade happens.
         const int32_t P = t.price;
-        // KP:237 parses as ((size > 0 && isBuy) ? maker.price <= P : maker.price >= P)  (H3)
-        while ((t.size > 0 && is_buy) ? m.price <= P : m.price >= P) {
+        int32_t mprice = pb;
+        bool head_moved = false;                             // ms is a later maker of level L
+        bool partial = false;                                // ms was partially filled
+        int32_t msize = 0;
+        KST(acc[10] += stamp() - tq; unsigned long long tpost = 0;)
+        while ((t.size > 0 && is_buy) ? mprice <= P : mprice >= P) {
+            KST(tq = stamp(); if (tpost) acc[13] += tq - tpost; tpost = 0;)
+            const Node m = ld_node(ms);
+            KST(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long tl = stamp(); acc[11] += tl - tq; acc[14] += 1;)
+            s_visits++;
             const int32_t ts = imin(t.size, m.size);
-            m.size = jisub(m.size, ts);
+            msize = jisub(m.size, ts);
             t.size = jisub(t.size, ts);
             emit(i, ntr++, m, ts);
+            KST(const unsigned long long te = stamp(); acc[12] += te - tl;)
             if (EXACT) {
                 fill_order(is_buy ? SOLD : BOUGHT, m.aid, m.sid, 0, ts, i);                       // maker fill
                 if (!dead) fill_order(is_buy ? BOUGHT : SOLD, t.aid, t.sid, jisub(t.price, m.price), ts, i);  // taker fill
             }
             if (dead) return false;
             L->qty -= ts;
-            if (m.size != 0) break;
+            KST(tpost = te;)
+            if (msize != 0) { partial = true; break; }
             L->count -= 1;
             free_slot(ms);                                   // orders.delete (KP:243)
             if (m.next < 0) {                                // level exhausted (KP:244-253)
@@ -874,17 +955,24 @@ struct Core {
                 if (!check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET, i); return false; }
                 L = lv(os, pb);
                 ms = L->head;
+                mprice = pb;
+                head_moved = false;
             } else {
                 ms = m.next;
+                mprice = m.price;
+                head_moved = true;
             }
             if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
-            m = ld_node(ms);
-            s_visits++;
         }
-        // buckets.put(bp, (makerPointer, last)); makerOrder.prev = null; orders.put (KP:259-261)
-        L->head = ms;
-        S.pool[ms].prev = -1;
-        S.pool[ms].size = m.size;
+        KST(if (tpost) acc[13] += stamp() - tpost;)
+        // buckets.put(bp, (makerPointer, last)); makerOrder.prev = null; orders.put (KP:259-261).
+        // For an untouched level head all three are no-ops and are skipped.
+        if (head_moved) {
+            L->head = ms;
+            S.pool[ms].prev = -1;
+        }
+        if (partial) S.pool[ms].size = msize;
+        if (head_moved || partial) mark_dirty(ms);
         return t.size == 0;
     }
 
@@ -895,7 +983,9 @@ struct Core {
         uint64_t lo = bl(s), hi = bm(s);                     // books.get(sid) again (KP:205)
         const int32_t p = t.price;
         if (p < 0 || p > 126) { die(KME_E_DOMAIN, KME_D_PRICE, i); return; }
+        KST(const unsigned long long ta = stamp();)
         const int32_t slot = alloc_slot(i);
+        KST(acc[15] += stamp() - ta;)
         if (dead) return;
         Level* L = lv(s, p);
         int32_t nprev = -1;
@@ -908,6 +998,7 @@ struct Core {
         } else {                                             // append at the tail (KP:213-219)
             const int32_t tl = L->tail;
             S.pool[tl].next = slot;
+            mark_dirty(tl);
             has_prev = true;
             prev_oid = L->tail_oid;
             nprev = tl;
@@ -917,19 +1008,21 @@ struct Core {
         nd->oid = t.oid; nd->aid = t.aid; nd->sid = t.sid; nd->prev_oid = prev_oid;
         nd->size = t.size; nd->next = -1; nd->prev = nprev; nd->group = g;
         nd->price = p; nd->action = t.action; nd->live = 1; nd->_pad = 0;
+        mark_dirty(slot);
         S.rest_slot[i] = slot;
         s_rests++;
     }
 
     // ---------------- removeOrder, KP:289-323
-    KDEV bool remove_order(const Rec& r) {
+    KDEV bool remove_order(const Rec& r, int j) {
         const uint32_t i = r.i;
         const int64_t tgt = r.tgt;
         int32_t slot = -1;
         if (tgt >= 0) slot = (int32_t)tgt;
         else if (tgt <= -2) slot = S.rest_slot[-(tgt + 2)];
         if (slot < 0) return false;
-        const Node o = ld_node(slot);
+        // the batch prefetched pre-epoch targets into LDS; valid unless written since
+        const Node o = (LDS && j >= 0 && tgt >= 0 && !is_dirty(slot)) ? nodepf[j] : ld_node(slot);
         if (!o.live || o.oid != r.oid) return false;       // orders.get(oid) == null
         if (o.aid != r.aid) return false;                  // order.aid != aid (KP:291)
         if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK, i); return false; }
@@ -943,14 +1036,18 @@ struct Core {
         } else if (o.prev < 0) {
             L->head = o.next;
             S.pool[o.next].prev = -1;
+            mark_dirty(o.next);
         } else if (o.next < 0) {
             L->tail = o.prev;
             L->tail_oid = o.prev_oid;
             S.pool[o.prev].next = -1;
+            mark_dirty(o.prev);
         } else {
             S.pool[o.prev].next = o.next;
             S.pool[o.next].prev = o.prev;
             S.pool[o.next].prev_oid = o.prev_oid;
+            mark_dirty(o.prev);
+            mark_dirty(o.next);
         }
         L->count -= 1;
         L->qty -= o.size;
@@ -968,13 +1065,15 @@ struct Core {
     }
 
     // ---------------- one record of this group (MatchingEngine.process, KP:96-126)
-    KDEV void process(const Rec& r) {
+    KDEV Out process(const Rec& r, int j) {
         const uint32_t i = r.i;
         const int32_t a = r.action;
         bool ok = false, has_prev = false;
         int64_t prev_oid = 0;
         int32_t out_size = r.size;
         uint32_t ntr = 0;
+        Out out;
+        out.action = a; out.size = r.size; out.prev = 0; out.has_prev = false; out.ntr = 0;
         if (EXACT) io.trade_off[i] = tnext;
         switch (a) {
         case ADD_SYMBOL:                                    // addSymbol, KP:184-191
@@ -983,14 +1082,14 @@ struct Core {
         case REMOVE_SYMBOL:
         case PAYOUT: {
             if (exists) {
-                if (remove_symbol_existing(r.sid) == 2) { die(KME_E_DOMAIN, KME_D_HANG, i); return; }
+                if (remove_symbol_existing(r.sid) == 2) { die(KME_E_DOMAIN, KME_D_HANG, i); return out; }
                 ok = false;                                 // removeAllOrders(sid) returned true
             } else {
                 ok = a == REMOVE_SYMBOL;
                 if (a == PAYOUT) {
                     if (EXACT) payout_settle(r.sid, r.size, i);
                     else die(KME_E_UNSUPPORTED, KME_D_NONE, i);
-                    if (dead) return;
+                    if (dead) return out;
                 }
             }
             if (a == PAYOUT) ok = false;                    // result ignored (KP:113-115)
@@ -1003,28 +1102,33 @@ struct Core {
             t.action = a; t.price = r.price; t.size = r.size; t._pad = 0;
             t.oid = r.oid; t.aid = r.aid; t.sid = r.sid;
             if (EXACT) {
-                if (!check_balance(t, i)) { if (dead) return; break; }
+                if (!check_balance(t, i)) { if (dead) return out; break; }
             } else {
                 if (!r.acct_ok) break;                      // balances.get(aid) == null
             }
+            KST(const unsigned long long t0 = stamp();)
             const bool filled = try_match(i, t, ntr);
-            if (dead) return;
-            if (!filled) { rest(i, t, has_prev, prev_oid); if (dead) return; }
+            KST(const unsigned long long t1 = stamp(); acc[4] += t1 - t0;)
+            if (dead) return out;
+            if (!filled) { rest(i, t, has_prev, prev_oid); if (dead) return out; }
+            KST(acc[5] += stamp() - t1;)
             ok = true;
             out_size = t.size;
             break;
         }
         case CANCEL:
-            ok = remove_order(r);
-            if (dead) return;
+            ok = remove_order(r, j);
+            if (dead) return out;
             break;
         default:
             break;
         }
-        if (lane_id() == 0) {
-            write_out(io, i, a, ok, out_size, has_prev, prev_oid);
-            if (!EXACT) io.n_trades[i] = ntr;
-        }
+        out.action = ok ? a : (int32_t)REJECT;
+        out.size = out_size;
+        out.prev = has_prev ? prev_oid : 0;
+        out.has_prev = has_prev;
+        out.ntr = ntr;
+        return out;
     }
 
     KDEV void flush_stats() {
@@ -1040,7 +1144,9 @@ struct Core {
 // (2) FUNDED: one wavefront per symbol group, the group's records in arrival order.
 __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
     __shared__ Level cache[2 * NLEV];
-    __shared__ uint64_t cmask[4];
+    __shared__ int32_t fstack[FSTACK];
+    __shared__ uint32_t dirty[DIRTY_WORDS];
+    __shared__ Node nodepf[64];
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     const int32_t g = blockIdx.x;
@@ -1048,21 +1154,65 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e) return;
     if (failed(S.ctr)) return;
-    Core<false, true> c(S, io, cache, cmask);
+    Core<false, true> c(S, io, cache, fstack, dirty, nodepf);
     c.load_group(g);
     const uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
     const int lane = lane_id();
+    KST(const unsigned long long tk0 = stamp();)
     for (uint32_t k0 = b; k0 < e && !c.dead; k0 += 64) {
+        KST(const unsigned long long tb0 = stamp();)
         const uint32_t k = k0 + lane;
         const bool valid = k < e;
         const Batch B = load_batch(S, io, valid, valid ? perm[k] : 0, true);
+        // cancels of orders resting since an earlier epoch: fetch the target node with the batch
+        dirty[lane] = 0;
+        if (valid && B.action == CANCEL && B.tgt >= 0) {
+            const int4* src = reinterpret_cast<const int4*>(&S.pool[B.tgt]);
+            int4* dst = reinterpret_cast<int4*>(&nodepf[lane]);
+            const int4 x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];
+            dst[0] = x0; dst[1] = x1; dst[2] = x2; dst[3] = x3;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
+        // per-record OUT fields collect in lane j of these registers; one store per field per batch
+        int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_flag = 0, o_ntr = 0;
+        KST(c.acc[0] += stamp() - tb0;)
 #pragma nounroll
-        for (int j = 0; j < nb && !c.dead; ++j) c.process(pick(B, j));
+        for (int j = 0; j < nb && !c.dead; ++j) {
+            KST(const unsigned long long tr0 = stamp();)
+            const Rec rr = pick(B, j);
+            const Out o = c.process(rr, j);
+            KST(const unsigned long long tr1 = stamp();
+                const int cat = (rr.action == BUY || rr.action == SELL) ? 1 : (rr.action == CANCEL ? 2 : 3);
+                if (cat == 1) { c.acc[1] += tr1 - tr0; c.acc[8] += 1; }
+                else if (cat == 2) { c.acc[2] += tr1 - tr0; c.acc[9] += 1; }
+                else c.acc[3] += tr1 - tr0;)
+            o_act = lane_put(o.action, j, o_act);
+            o_size = lane_put(o.size, j, o_size);
+            o_plo = lane_put((int32_t)(uint32_t)o.prev, j, o_plo);
+            o_phi = lane_put((int32_t)(uint32_t)((uint64_t)o.prev >> 32), j, o_phi);
+            o_flag = lane_put(o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0, j, o_flag);
+            o_ntr = lane_put((int32_t)o.ntr, j, o_ntr);
+            KST(c.acc[6] += stamp() - tr1;)
+        }
+        if (lane < nb && !c.dead) {
+            const uint32_t i = B.i;
+            io.out_action[i] = o_act;
+            io.out_size[i] = o_size;
+            io.out_prev[i] = (int64_t)(((uint64_t)(uint32_t)o_phi << 32) | (uint32_t)o_plo);
+            io.out_flags[i] = (uint8_t)o_flag;
+            io.n_trades[i] = (uint32_t)o_ntr;
+        }
     }
     c.close_trade_chunk();
     c.store_group();
     c.flush_stats();
+#ifdef KME_STAMPS
+    c.acc[7] = stamp() - tk0;
+    if (lane == 0)
+        for (int q = 0; q < 16; ++q) S.dbg[(size_t)g * 16 + q] = c.acc[q];
+#endif
 }
 
 // EXACT: one wavefront, the whole epoch in arrival order, every store exact.
@@ -1070,7 +1220,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     if (failed(S.ctr)) return;
-    Core<true, false> c(S, io, nullptr, nullptr);
+    Core<true, false> c(S, io, nullptr, nullptr, nullptr, nullptr);
     const int lane = lane_id();
     for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
         const uint32_t k = k0 + lane;
@@ -1088,7 +1238,13 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
             else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) grp = group_of(r.sid, S.G);
             if (grp >= 0) {
                 if (grp != c.g) { c.store_group(); c.load_group(grp); }
-                c.process(r);
+                const Out o = c.process(r, -1);
+                if (!c.dead && lane == 0) {
+                    io.out_action[i] = o.action;
+                    io.out_size[i] = o.size;
+                    io.out_prev[i] = o.prev;
+                    io.out_flags[i] = o.has_prev ? (uint8_t)KME_OUT_HAS_PREV : (uint8_t)0;
+                }
                 continue;
             }
             // records without a symbol group

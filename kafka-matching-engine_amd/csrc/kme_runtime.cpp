@@ -204,6 +204,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.ghist, 256 * ntiles + 2 * (E / 2048 + 16) + 4096);
     ALLOC(S.seg, (size_t)G + 2);
     ALLOC(S.ctr, C_NCTR);
+    ALLOC(S.dbg, (size_t)G * 16);
+    HIP_TRY(hipMemsetAsync(S.dbg, 0, (size_t)G * 16 * sizeof(unsigned long long), e->stream));
     // epoch buffers
     ALLOC(e->d_action, E); ALLOC(e->d_price, E); ALLOC(e->d_size, E);
     ALLOC(e->d_oid, E); ALLOC(e->d_aid, E); ALLOC(e->d_sid, E);
@@ -382,6 +384,14 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     }
     if (st) *st = s;
     return (kme_status)s.status;
+}
+
+kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n) {
+    if (!e || !out) return KME_E_INVALID;
+    const size_t cap = (size_t)e->cfg.max_symbols * 16;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(out, e->S.dbg, std::min(n, cap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return KME_OK;
 }
 
 kme_status kme_device_results(kme_engine* e, kme_epoch_result* r) {

@@ -20,7 +20,7 @@ import numpy as np
 from .workloads import Orders  # noqa: F401  (re-export)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkme.so")
+LIB_PATH = os.environ.get("KME_LIB") or os.path.join(_HERE, "libkme.so")
 
 MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
@@ -65,7 +65,7 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str",
+    "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
 ]
@@ -110,6 +110,7 @@ def lib():
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
         "kme_shard_of": (u32, [i64, u32]),
+        "kme_debug_counters": (st, [vp, vp, C.c_size_t]),
         "kme_strerror": (C.c_char_p, [C.c_int]),
         "kme_domain_str": (C.c_char_p, [C.c_int]),
         "kme_processor_create": (st, [C.POINTER(kme_config), u32, FORWARD_FN, COMMIT_FN, vp, C.POINTER(vp)]),
@@ -278,6 +279,13 @@ class Engine:
             return C.string_at(p, n.value).decode()
         finally:
             self._L.kme_free(p)
+
+    def debug_counters(self) -> np.ndarray:
+        out = np.zeros(int(self.cfg.max_symbols) * 16, np.uint64)
+        rc = self._L.kme_debug_counters(self._h, C.c_void_p(out.ctypes.data), out.size)
+        if rc:
+            raise KmeError(rc, "kme_debug_counters")
+        return out.reshape(-1, 16)
 
     def snapshot_books(self) -> str:
         return self._text(self._L.kme_snapshot_books)
