@@ -82,7 +82,10 @@ typedef struct kme_config {
     uint64_t max_resting;      /* order-node pool capacity (resting orders, the Orders store) */
     uint64_t ledger_capacity;  /* EXACT: hash capacity of Balances and of Positions */
     int32_t device;            /* HIP device ordinal */
-    uint32_t flags;            /* reserved, 0 */
+    uint32_t credit_shards;    /* FUNDED: number of symbol shards an account's credit is split over
+                                  (0 or 1 = one engine).  Each shard proves its own orders against
+                                  floor(credit / n) and ceil(debit / n), so the shards' reservations
+                                  together never exceed the account's cash. */
 } kme_config;
 
 /* One epoch of input records, structure-of-arrays (Order fields KP:451-456).  The reference's

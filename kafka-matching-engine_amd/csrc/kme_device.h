@@ -89,7 +89,7 @@ constexpr uint64_t OID_SALT = 0x8000000000000000ull;   // stored key = oid ^ SAL
 
 struct DevState {
     int32_t G, mode, A, passes;
-    uint32_t pool_cap, otab_mask, _pad0, ttmp_cap;
+    uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;
     uint32_t bal_mask, pos_mask, trades_cap, _pad;
     KG GroupState* grp;
     KG Level* lev;

@@ -295,10 +295,18 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
                 if (S.acct_since[aid] < seq) {
                     const int64_t lbs = S.acct_since[aid] < io.seq_base ? S.acct_lb[aid] : 0;
                     const int64_t cons = lbs - S.acct_need[aid] - S.acct_negx[aid];
-                    if (cons >= (int64_t)jineg(size)) {
+                    // transfer rejects when balance < -size as a Java int (KP:142).  With credit_div
+                    // shards this shard proves its part of that threshold (ceil of a positive one,
+                    // truncation of a negative one) and books floor(credit / d) or ceil(debit / d),
+                    // so the shards' bounds never sum above the account's cash.
+                    const int64_t d = S.credit_div;
+                    const int64_t thr = (int64_t)jineg(size);
+                    const int64_t thr_share = thr > 0 ? (thr + d - 1) / d : thr / d;
+                    const int64_t share = size >= 0 ? (int64_t)size / d : -((-(int64_t)size + d - 1) / d);
+                    if (cons >= thr_share) {
                         ok = true;
-                        S.acct_xfer[aid] += size;
-                        if (size < 0) S.acct_negx[aid] -= size;
+                        S.acct_xfer[aid] += share;
+                        if (share < 0) S.acct_negx[aid] -= share;
                     } else {
                         raise_wave(S.ctr, KME_E_UNFUNDED, KME_D_NONE, j);
                         return;

@@ -137,6 +137,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         return KME_E_INVALID;
     if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28)))
         return KME_E_INVALID;
+    if (cfg->credit_shards > (1u << 16) || (cfg->mode == KME_MODE_EXACT && cfg->credit_shards > 1))
+        return KME_E_INVALID;
     kme_engine* e = new kme_engine();
     e->cfg = *cfg;
     e->device = cfg->device;
@@ -161,6 +163,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.pool_cap = (uint32_t)P;
     e->otab_cap = pow2_at_least(std::max<uint64_t>(2 * P, 1024));
     S.otab_mask = (uint32_t)(e->otab_cap - 1);
+    S.credit_div = cfg->credit_shards > 1 ? cfg->credit_shards : 1;
     S.trades_cap = cfg->max_trades;
     const uint64_t ttmp_cap = funded ? (uint64_t)cfg->max_trades + (uint64_t)(G + 64) * TRADE_CHUNK : 1;
     if (ttmp_cap >= (1ull << 32)) { kme_destroy(e); return KME_E_INVALID; }

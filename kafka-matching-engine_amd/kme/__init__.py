@@ -38,7 +38,7 @@ class kme_config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("mode", C.c_uint32), ("max_symbols", C.c_uint32),
                 ("max_accounts", C.c_uint32), ("max_epoch", C.c_uint32), ("max_trades", C.c_uint32),
                 ("max_resting", C.c_uint64), ("ledger_capacity", C.c_uint64), ("device", C.c_int32),
-                ("flags", C.c_uint32)]
+                ("credit_shards", C.c_uint32)]
 
 
 class kme_orders(C.Structure):
