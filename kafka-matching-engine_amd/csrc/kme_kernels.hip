@@ -538,6 +538,8 @@ struct Batch {
     int32_t action, price, size, acct_ok;
     int64_t oid, aid, sid, tgt;
 };
+// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding (vmcnt bits 3:0 and 15:14)
+constexpr int VMCNT0 = 0x0F70;
 KDEV int32_t rl32(int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
 // lane j of v := x (v_cmp + v_cndmask; x and j are wave-uniform)
 KDEV int32_t lane_put(int32_t x, int j, int32_t v) { return lane_id() == j ? x : v; }
@@ -578,6 +580,7 @@ struct Out {
     int32_t action, size;
     int64_t prev;
     bool has_prev;
+    bool rested;          // the order came to rest (counted per batch, not per record)
     uint32_t ntr;
 };
 
@@ -601,7 +604,6 @@ struct Core {
     int32_t free_head, chunk_next, chunk_end;
     Level* glev;
     uint32_t tnext, tend;             // FUNDED: trade scratch chunk; EXACT: running trade count
-    unsigned long long s_trades, s_rests, s_visits, s_cancel;
     bool dead;
 #ifdef KME_STAMPS
     unsigned long long acc[16];
@@ -611,7 +613,7 @@ struct Core {
         : S(s), io(e), cache(c), fstack(fs), dirty(dty), nodepf(npf) {
         g = -1; exists = 0; b0l = b0m = b1l = b1m = 0; fsp = 0;
         free_head = -1; chunk_next = chunk_end = 0; glev = nullptr;
-        tnext = tend = 0; s_trades = s_rests = s_visits = s_cancel = 0; dead = false;
+        tnext = tend = 0; dead = false;
         KST(for (int q = 0; q < 16; ++q) acc[q] = 0;)
     }
 
@@ -677,11 +679,29 @@ struct Core {
         return n;
     }
 
-    // Node slots: LDS stack of slots freed by this wavefront first (no dependent global load), then
-    // the group's global free list, then a chunk from the pool's bump counter.
+    // Node slots.  Parallel kernel (LDS): an LDS stack of free slots; the group's free slots kept
+    // between epochs are a list of BLOCKS, each a free 64-byte slot holding up to FBLK - 1 more
+    // free slot ids (word 0 = next block, word 1 = count, words 2.. = ids; word 14 = Node::live
+    // stays 0).  One load refills the stack with a whole block.  Serial kernel: a plain list
+    // linked through Node::next.  Last resort: a chunk from the pool's bump counter.
+    static constexpr int FBLK = 13;
     KDEV int32_t alloc_slot(int64_t idx) {
-        if (LDS && fsp > 0) return fstack[--fsp];
-        if (free_head >= 0) {
+        if (LDS) {
+            if (fsp > 0) return fstack[--fsp];
+            if (free_head >= 0) {
+                const int32_t blk = free_head;
+                const int lane = lane_id();
+                const int32_t w = lane < 2 + FBLK - 1 ? reinterpret_cast<const int32_t*>(&S.pool[blk])[lane] : 0;
+                const int32_t nxt = __builtin_amdgcn_readlane(w, 0);
+                const int32_t cnt = __builtin_amdgcn_readlane(w, 1);
+                if (lane >= 2 && lane < 2 + cnt) fstack[lane - 2] = w;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                fsp = cnt;
+                free_head = nxt;
+                return blk;
+            }
+        } else if (free_head >= 0) {
             const int32_t s = free_head;
             free_head = S.pool[s].next;
             return s;
@@ -699,23 +719,37 @@ struct Core {
     KDEV void free_slot(int32_t s) {
         S.pool[s].live = 0;
         mark_dirty(s);
-        if (LDS && fsp < FSTACK) {
+        if (LDS) {
+            if (fsp == FSTACK) spill_blocks(FSTACK - FBLK, FSTACK);
             fstack[fsp++] = s;
             return;
         }
         S.pool[s].next = free_head;
         free_head = s;
     }
-    // The LDS stack joins the global free list when the group is written back: entry k links to
-    // entry k - 1, the bottom entry to the old list head (all lanes in parallel, stores only).
+    // Writes stack entries [b, e) as blocks of FBLK slots (the last slot of each block holds the
+    // others' ids), chained onto the group's block list; all lanes in parallel, stores only.
+    KDEV void spill_blocks(int b, int e) {
+        const int n = e - b;
+        const int nblk = (n + FBLK - 1) / FBLK;
+        for (int k = lane_id(); k < nblk * 14; k += 64) {
+            const int blk = k / 14, word = k - blk * 14;
+            const int base = b + blk * FBLK;
+            const int cnt = imin(FBLK, e - base);                // slots in this block incl. itself
+            const int32_t host = fstack[base + cnt - 1];
+            int32_t v;
+            if (word == 0) v = blk == 0 ? free_head : fstack[base - 1];   // previous block's host
+            else if (word == 1) v = cnt - 1;
+            else v = word - 2 < cnt - 1 ? fstack[base + word - 2] : -1;
+            reinterpret_cast<int32_t*>(&S.pool[host])[word] = v;
+        }
+        free_head = fstack[b + (nblk - 1) * FBLK + imin(FBLK, e - (b + (nblk - 1) * FBLK)) - 1];
+        fsp = b;
+    }
+    // The LDS stack joins the group's block list when the group is written back.
     KDEV void flush_free_stack() {
         if (!LDS || fsp == 0) return;
-        for (int k = lane_id(); k < fsp; k += 64) {
-            const int32_t sl = fstack[k];
-            S.pool[sl].next = k == 0 ? free_head : fstack[k - 1];
-        }
-        free_head = fstack[fsp - 1];
-        fsp = 0;
+        spill_blocks(0, fsp);
     }
     // Per-batch filter of node slots written since the batch's cancel-target prefetch.
     KDEV void mark_dirty(int32_t s) {
@@ -905,7 +939,6 @@ struct Core {
             }
             tnext++;
         }
-        s_trades++;
     }
     KDEV void close_trade_chunk() {
         if (EXACT) return;
@@ -914,6 +947,24 @@ struct Core {
     }
 
     // ---------------- tryMatch, KP:225-263
+    // The level being swept lives in registers (head, count, qty) and is written back once when
+    // the sweep stops inside it; a level swept empty is not written at all (its bit is cleared and
+    // an unoccupied level's fields are dead until a rest rewrites them).  A maker's price is the
+    // index of its level, so the loop test of KP:237 -- ((size > 0 && isBuy) ? maker.price <= P :
+    // maker.price >= P), H3 -- needs no node load, and the next maker's node is requested before
+    // the stores of the current trade (vmcnt is in order: a load issued after stores waits for
+    // them).
+    KDEV bool crosses(bool is_buy, int32_t size, int32_t mprice, int32_t P) const {
+        return (size > 0 && is_buy) ? mprice <= P : mprice >= P;
+    }
+    // executeTrade (KP:265-274): the trade record, and in EXACT mode both fillOrder calls.
+    KDEV void trade(uint32_t i, uint32_t& ntr, const Node& m, const Taker& t, int32_t ts, bool is_buy) {
+        emit(i, ntr++, m, ts);
+        if (EXACT && !dead) {
+            fill_order(is_buy ? SOLD : BOUGHT, m.aid, m.sid, 0, ts, i);                              // maker fill
+            if (!dead) fill_order(is_buy ? BOUGHT : SOLD, t.aid, t.sid, jisub(t.price, m.price), ts, i);  // taker fill
+        }
+    }
     KDEV bool try_match(uint32_t i, Taker& t, uint32_t& ntr) {
         KST(unsigned long long tq = stamp();)
         const bool is_buy = t.action == BUY;
@@ -923,65 +974,71 @@ struct Core {
         int32_t pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
         if (pb == -1) return false;
         if (!check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET, i); return false; }
-        Level* L = lv(os, pb);
-        int32_t ms = L->head;
-        if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
-        // A maker's price is the index of the level it rests in, so the loop test of KP:237 --
-        // ((size > 0 && isBuy) ? maker.price <= P : maker.price >= P), H3 -- needs no node load;
-        // the node is read only when a trade happens.
         const int32_t P = t.price;
-        int32_t mprice = pb;
+        if (!crosses(is_buy, t.size, pb, P)) return t.size == 0;
+        Level* L = lv(os, pb);
+        int32_t ms = L->head, lcnt = L->count;
+        int64_t lqty = L->qty;
+        if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
+        Node m = ld_node(ms);
         bool head_moved = false;                             // ms is a later maker of level L
-        bool partial = false;                                // ms was partially filled
-        int32_t msize = 0;
-        KST(acc[10] += stamp() - tq; unsigned long long tpost = 0;)
-        while ((t.size > 0 && is_buy) ? mprice <= P : mprice >= P) {
-            KST(tq = stamp(); if (tpost) acc[13] += tq - tpost; tpost = 0;)
-            const Node m = ld_node(ms);
-            KST(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long tl = stamp(); acc[11] += tl - tq; acc[14] += 1;)
-            s_visits++;
+        KST(acc[10] += stamp() - tq;)
+        for (;;) {
+            KST(tq = stamp(); acc[14] += 1;)
             const int32_t ts = imin(t.size, m.size);
-            msize = jisub(m.size, ts);
+            const int32_t msize = jisub(m.size, ts);
             t.size = jisub(t.size, ts);
-            emit(i, ntr++, m, ts);
-            KST(const unsigned long long te = stamp(); acc[12] += te - tl;)
-            if (EXACT) {
-                fill_order(is_buy ? SOLD : BOUGHT, m.aid, m.sid, 0, ts, i);                       // maker fill
-                if (!dead) fill_order(is_buy ? BOUGHT : SOLD, t.aid, t.sid, jisub(t.price, m.price), ts, i);  // taker fill
+            lqty -= ts;
+            if (msize != 0) {                                // maker stays, partially filled (KP:255-261)
+                trade(i, ntr, m, t, ts, is_buy);
+                if (dead) return false;
+                S.pool[ms].size = msize;
+                if (head_moved) { L->head = ms; S.pool[ms].prev = -1; }
+                mark_dirty(ms);
+                L->count = lcnt; L->qty = lqty;
+                KST(acc[13] += stamp() - tq;)
+                return t.size == 0;
             }
-            if (dead) return false;
-            L->qty -= ts;
-            KST(tpost = te;)
-            if (msize != 0) { partial = true; break; }
-            L->count -= 1;
-            free_slot(ms);                                   // orders.delete (KP:243)
-            if (m.next < 0) {                                // level exhausted (KP:244-253)
+            lcnt -= 1;                                       // maker consumed: orders.delete (KP:243)
+            int32_t nms;
+            bool same_level = m.next >= 0;
+            if (same_level) {
+                nms = m.next;
+                if (!crosses(is_buy, t.size, m.price, P)) {  // stops before the next maker of L
+                    trade(i, ntr, m, t, ts, is_buy);
+                    if (dead) return false;
+                    free_slot(ms);
+                    L->head = nms; S.pool[nms].prev = -1; mark_dirty(nms);
+                    L->count = lcnt; L->qty = lqty;
+                    KST(acc[13] += stamp() - tq;)
+                    return t.size == 0;
+                }
+            } else {                                         // level exhausted (KP:244-253)
                 unset_bit(lo, hi, m.price);
                 set_bm(os, lo, hi);
                 pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
-                if (pb == -1) return t.size == 0;
-                if (!check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET, i); return false; }
+                const bool go = pb != -1 && check_bit(lo, hi, pb) && crosses(is_buy, t.size, pb, P);
+                if (!go) {
+                    trade(i, ntr, m, t, ts, is_buy);
+                    if (dead) return false;
+                    free_slot(ms);
+                    if (pb != -1 && !check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET, i); return false; }
+                    KST(acc[13] += stamp() - tq;)
+                    return t.size == 0;
+                }
                 L = lv(os, pb);
-                ms = L->head;
-                mprice = pb;
-                head_moved = false;
-            } else {
-                ms = m.next;
-                mprice = m.price;
-                head_moved = true;
+                nms = L->head; lcnt = L->count; lqty = L->qty;
+                if (nms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
             }
-            if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
+            const Node nm = ld_node(nms);                   // in flight during this trade's stores
+            trade(i, ntr, m, t, ts, is_buy);
+            if (dead) return false;
+            free_slot(ms);
+            head_moved = same_level;
+            m = nm;
+            ms = nms;
+            KST(acc[12] += stamp() - tq;)
         }
-        KST(if (tpost) acc[13] += stamp() - tpost;)
-        // buckets.put(bp, (makerPointer, last)); makerOrder.prev = null; orders.put (KP:259-261).
-        // For an untouched level head all three are no-ops and are skipped.
-        if (head_moved) {
-            L->head = ms;
-            S.pool[ms].prev = -1;
-        }
-        if (partial) S.pool[ms].size = msize;
-        if (head_moved || partial) mark_dirty(ms);
-        return t.size == 0;
     }
 
     // ---------------- addOrder, KP:200-223 (after the book-exists and balance checks)
@@ -1018,7 +1075,6 @@ struct Core {
         nd->price = p; nd->action = t.action; nd->live = 1; nd->_pad = 0;
         mark_dirty(slot);
         S.rest_slot[i] = slot;
-        s_rests++;
     }
 
     // ---------------- removeOrder, KP:289-323
@@ -1061,7 +1117,6 @@ struct Core {
         L->qty -= o.size;
         free_slot(slot);
         if (EXACT) post_remove_adjustments(o, i);
-        s_cancel++;
         return !dead;
     }
 
@@ -1081,7 +1136,7 @@ struct Core {
         int32_t out_size = r.size;
         uint32_t ntr = 0;
         Out out;
-        out.action = a; out.size = r.size; out.prev = 0; out.has_prev = false; out.ntr = 0;
+        out.action = a; out.size = r.size; out.prev = 0; out.has_prev = false; out.rested = false; out.ntr = 0;
         if (EXACT) io.trade_off[i] = tnext;
         switch (a) {
         case ADD_SYMBOL:                                    // addSymbol, KP:184-191
@@ -1118,7 +1173,7 @@ struct Core {
             const bool filled = try_match(i, t, ntr);
             KST(const unsigned long long t1 = stamp(); acc[4] += t1 - t0;)
             if (dead) return out;
-            if (!filled) { rest(i, t, has_prev, prev_oid); if (dead) return out; }
+            if (!filled) { rest(i, t, has_prev, prev_oid); if (dead) return out; out.rested = true; }
             KST(acc[5] += stamp() - t1;)
             ok = true;
             out_size = t.size;
@@ -1139,14 +1194,6 @@ struct Core {
         return out;
     }
 
-    KDEV void flush_stats() {
-        if (lane_id() == 0) {
-            if (s_trades) atomicAdd(&S.ctr[C_TRADES], s_trades);
-            if (s_rests) atomicAdd(&S.ctr[C_RESTS], s_rests);
-            if (s_visits) atomicAdd(&S.ctr[C_VISITS], s_visits);
-            if (s_cancel) atomicAdd(&S.ctr[C_CANCEL_OK], s_cancel);
-        }
-    }
 };
 
 // (2) FUNDED: one wavefront per symbol group, the group's records in arrival order.
@@ -1166,6 +1213,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     c.load_group(g);
     const uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
     const int lane = lane_id();
+    uint32_t n_rest = 0, n_cancel = 0;
     KST(const unsigned long long tk0 = stamp();)
     for (uint32_t k0 = b; k0 < e && !c.dead; k0 += 64) {
         KST(const unsigned long long tb0 = stamp();)
@@ -1182,6 +1230,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        // The batch registers are read with readlane inside the record loop.  Waiting for them here
+        // once keeps the waitcnt pass from placing a vmcnt(0) at the loop header, which would make
+        // every record wait for all stores of the record before it (stores share vmcnt on gfx9).
+        __builtin_amdgcn_s_waitcnt(VMCNT0);
         const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
         // per-record OUT fields collect in lane j of these registers; one store per field per batch
         int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_flag = 0, o_ntr = 0;
@@ -1200,22 +1252,27 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             o_size = lane_put(o.size, j, o_size);
             o_plo = lane_put((int32_t)(uint32_t)o.prev, j, o_plo);
             o_phi = lane_put((int32_t)(uint32_t)((uint64_t)o.prev >> 32), j, o_phi);
-            o_flag = lane_put(o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0, j, o_flag);
+            o_flag = lane_put((o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0) | (o.rested ? 2 : 0), j, o_flag);
             o_ntr = lane_put((int32_t)o.ntr, j, o_ntr);
             KST(c.acc[6] += stamp() - tr1;)
         }
+        n_rest += (uint32_t)__popcll(__ballot(lane < nb && (o_flag & 2)));
+        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && B.action == CANCEL && o_act == CANCEL));
         if (lane < nb && !c.dead) {
             const uint32_t i = B.i;
             io.out_action[i] = o_act;
             io.out_size[i] = o_size;
             io.out_prev[i] = (int64_t)(((uint64_t)(uint32_t)o_phi << 32) | (uint32_t)o_plo);
-            io.out_flags[i] = (uint8_t)o_flag;
+            io.out_flags[i] = (uint8_t)(o_flag & KME_OUT_HAS_PREV);
             io.n_trades[i] = (uint32_t)o_ntr;
         }
     }
     c.close_trade_chunk();
     c.store_group();
-    c.flush_stats();
+    if (lane == 0) {
+        if (n_rest) atomicAdd(&S.ctr[C_RESTS], (unsigned long long)n_rest);
+        if (n_cancel) atomicAdd(&S.ctr[C_CANCEL_OK], (unsigned long long)n_cancel);
+    }
 #ifdef KME_STAMPS
     c.acc[7] = stamp() - tk0;
     if (lane == 0)
@@ -1230,6 +1287,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     if (failed(S.ctr)) return;
     Core<true, false> c(S, io, nullptr, nullptr, nullptr, nullptr);
     const int lane = lane_id();
+    uint32_t n_rest = 0, n_cancel = 0;
     for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
         const uint32_t k = k0 + lane;
         const bool valid = k < io.n;
@@ -1247,6 +1305,8 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
             if (grp >= 0) {
                 if (grp != c.g) { c.store_group(); c.load_group(grp); }
                 const Out o = c.process(r, -1);
+                n_rest += o.rested;
+                n_cancel += a == CANCEL && o.action == CANCEL;
                 if (!c.dead && lane == 0) {
                     io.out_action[i] = o.action;
                     io.out_size[i] = o.size;
@@ -1273,8 +1333,9 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     c.store_group();
     if (lane_id() == 0) {
         io.trade_off[io.n] = c.tnext;
-        S.ctr[C_TRADES] += c.s_trades; S.ctr[C_RESTS] += c.s_rests;
-        S.ctr[C_VISITS] += c.s_visits; S.ctr[C_CANCEL_OK] += c.s_cancel;
+        S.ctr[C_TRADES] = c.tnext;
+        S.ctr[C_RESTS] = n_rest;
+        S.ctr[C_CANCEL_OK] = n_cancel;
     }
 }
 
@@ -1296,6 +1357,7 @@ __global__ void k_scatter(DevState S, EpochIO io, const uint32_t* total) {
 // ------------------------------------------------------------------ oid-table maintenance
 // Orders that came to rest this epoch and are still live get an oid-table entry.  The used-slot
 // counter is bumped once per wavefront (a single hot counter would serialise every insert).
+// Oid-table entries for the orders of this epoch that are still resting.
 __global__ void k_table(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ins = false;

@@ -358,7 +358,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_trades = (uint32_t)c[C_TRADES];
     s.n_orders = c[C_ORDERS];
     s.n_rests = c[C_RESTS];
-    s.n_maker_visits = c[C_VISITS];
+    s.n_maker_visits = c[C_TRADES];               // every maker visit is one trade (KP:238-242)
     s.n_cancel_ok = c[C_CANCEL_OK];
     if (c[C_ERR] != ~0ull) {
         s.status = (int32_t)(c[C_ERR] & 0xFF);

@@ -1,0 +1,58 @@
+"""Per-launch HBM traffic of one kernel from rocprofv3 --pmc passes (tools/pmc_round.sh output).
+
+FETCH_SIZE and WRITE_SIZE (KiB per dispatch) come from separate passes (FETCH_SIZE uses 3 of the 4
+TCC slots, WRITE_SIZE 2).  Following MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950 tallies 128-B
+memory requests at 64 B, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is taken as reported.  Both
+count Infinity-Cache (MALL) hits too, so this is L2-miss traffic, an upper bound on HBM bytes.
+
+usage: python tools/pmc_summary.py <pmc dir> <kernel regex> <out.json> [skip_first_n]
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def counters(d, kernel_re):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if not re.search(kernel_re, row.get("Kernel_Name", "")):
+                    continue
+                name = row["Counter_Name"]
+                disp = int(row.get("Dispatch_Id", 0))
+                vals.setdefault(name, {}).setdefault(disp, 0.0)
+                vals[name][disp] += float(row["Counter_Value"])
+    return vals
+
+
+def main():
+    d, kre, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    allv = {}
+    for sub in sorted(glob.glob(os.path.join(d, "p*"))):
+        if os.path.isdir(sub):
+            for k, v in counters(sub, kre).items():
+                allv[k] = v
+    res = {"kernel_regex": kre, "source": os.path.relpath(d)}
+    for k, per in sorted(allv.items()):
+        xs = [per[i] for i in sorted(per)][skip:]
+        if xs:
+            res[k] = {"mean_per_dispatch": sum(xs) / len(xs), "dispatches": len(xs)}
+    f = res.get("FETCH_SIZE", {}).get("mean_per_dispatch")
+    w = res.get("WRITE_SIZE", {}).get("mean_per_dispatch")
+    if f is not None and w is not None:
+        res["read_bytes_per_launch"] = 2 * f * 1024
+        res["write_bytes_per_launch"] = w * 1024
+        res["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
+        res["note"] = "FETCH_SIZE doubled per the gfx950 calibration; MALL hits included (upper bound)"
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
