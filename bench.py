@@ -36,6 +36,7 @@ from kme import workloads as W  # noqa: E402
 
 METRIC = "matched orders/sec (node) at 65,536 symbols; p99 epoch latency; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+C3_SYMBOLS, C3_ACCOUNTS = 65536, 65536  # BASELINE configs[2] / SURVEY §8d C3
 
 
 def algorithmic_bytes(st) -> int:
@@ -46,20 +47,21 @@ def algorithmic_bytes(st) -> int:
             + 48 * st.n_cancel_ok)
 
 
-def make_workload(name: str, n_orders: int, rank: int):
+def make_workload(name: str, n_orders: int, rank: int, world: int):
     seed = 1000 + rank
     if name == "c2":
         nsym, nacc = 1024, 4096
         stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
         desc = "C2: 1,024 symbols x 16M uniform limit/cancel orders per GPU (BASELINE configs[1])"
     elif name == "c3":
-        nsym, nacc = 8192, 8192
+        nsym, nacc = C3_SYMBOLS // world, C3_ACCOUNTS
         stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
-        desc = "C3 shard: 65,536 symbols / 8 GPUs = 8,192 symbols per GPU, uniform"
+        desc = (f"C3: 65,536 symbols symbol-sharded over {world} GPU(s) = {nsym:,} symbols per GPU, "
+                f"uniform limit/cancel orders (BASELINE configs[2])")
     elif name == "c4":
-        nsym, nacc = 8192, 8192
+        nsym, nacc = C3_SYMBOLS // world, C3_ACCOUNTS
         stream = W.zipf(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
-        desc = "C4 shard: Zipf(1.1) symbol popularity over 8,192 symbols per GPU, 21-level band"
+        desc = f"C4: Zipf(1.1) symbol popularity, 65,536 symbols over {world} GPU(s), 21-level band"
     elif name == "c5":
         nsym, nacc = 1024, 4096
         stream = W.cancel_replace(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
@@ -113,7 +115,7 @@ def main():
 
     E = args.epoch
     total = max(args.orders, (args.warmup + args.steps) * E)
-    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank)
+    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world)
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
                              max_resting=min(total, 1 << 30), max_trades=2 * E + (1 << 16),
