@@ -175,24 +175,25 @@ def main():
     elapsed = t1 - t0
     assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
 
-    if args.stamps:
-        d = eng.debug_counters().astype(np.float64)
-        tot = d.sum(axis=0)
-        names = ["batch_load", "buy_sell", "cancel", "other", "try_match", "rest", "out_lanes", "kernel", "n_buy_sell",
-                 "n_cancel"]
-        cyc = {n: tot[q] for q, n in enumerate(names)}
-        per = {"cycles_per_buy_sell": cyc["buy_sell"] / max(1, cyc["n_buy_sell"]),
-               "cycles_per_cancel": cyc["cancel"] / max(1, cyc["n_cancel"]),
-               "try_match_per_buy_sell": cyc["try_match"] / max(1, cyc["n_buy_sell"]),
-               "rest_per_buy_sell": cyc["rest"] / max(1, cyc["n_buy_sell"]),
-               "share_of_kernel": {n: cyc[n] / cyc["kernel"] for n in names[:7]},
-               "try_match_pre_loop_per_buy_sell": tot[10] / max(1, cyc["n_buy_sell"]),
-               "node_load_per_visit": tot[11] / max(1, tot[14]),
-               "emit_per_trade": tot[12] / max(1, tot[14]),
-               "post_trade_per_trade": tot[13] / max(1, tot[14]),
-               "alloc_per_rest": tot[15],
-               "visits": tot[14],
-               "kernel_cycles_per_wave_mean": cyc["kernel"] / max(1, int((d[:, 7] > 0).sum()))}
+    if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
+        d = eng.debug_counters().astype(np.float64).reshape(-1, 32).sum(axis=0)
+        names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",
+                 "n_trade_rec", "n_rest_rec", "n_cancel_rec", "maker_wait", "n_maker", "victim_wait", "n_victim",
+                 "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre"]
+        v = dict(zip(names, d))
+        per = {"share_of_kernel": {n: v[n] / v["kernel"] for n in ("group_in", "batch", "trade_rec", "rest_rec",
+                                                                     "cancel_rec", "other_rec", "group_out", "flush")},
+               "cycles_per_trade_rec": v["trade_rec"] / max(1, v["n_trade_rec"]),
+               "cycles_per_rest_rec": v["rest_rec"] / max(1, v["n_rest_rec"]),
+               "cycles_per_cancel_rec": v["cancel_rec"] / max(1, v["n_cancel_rec"]),
+               "maker_wait_per_load": v["maker_wait"] / max(1, v["n_maker"]),
+               "makers_per_trade_rec": v["n_maker"] / max(1, v["n_trade_rec"]),
+               "victim_wait_per_load": v["victim_wait"] / max(1, v["n_victim"]),
+               "victim_loads_per_cancel": v["n_victim"] / max(1, v["n_cancel_rec"]),
+               "rest_parts_per_rest": {n: v[n] / max(1, v["n_rest_rec"]) for n in ("rest_alloc", "rest_level", "rest_node", "tm_pre_norest")},
+               "rec_pick_per_rec": v["rec_pick"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
+               "rec_total_per_rec": v["rec_out"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
+               "counts": {n: v[n] for n in ("n_trade_rec", "n_rest_rec", "n_cancel_rec", "n_maker", "n_victim")}}
         print(json.dumps({"stamps": per}), flush=True)
         return
     stats = torch.tensor([elapsed, float(n_orders), float(n_trades)], dtype=torch.float64, device=dev)

@@ -198,7 +198,8 @@ kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, in
 uint32_t kme_shard_of(int64_t sid, uint32_t n_shards);
 
 /* Diagnostics: per-symbol-group words written by a -DKME_STAMPS build of the match kernel
- * (in-kernel s_memtime stamps; zero in the product build).  Copies min(n, max_symbols * 16). */
+ * (in-kernel s_memtime stamps; zero in the product build).  Copies min(n, max_symbols * 32). */
+#define KME_DBG_WORDS 32
 kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n);
 
 const char* kme_strerror(int status);

@@ -7,7 +7,7 @@
 //                        shared book, H4): existence, two 128-bit level bitmaps (the Books values,
 //                        KP:38-41), the group's node free list and bump chunk.
 //   Level[G][2][128]     one per (book side, price level) = the Buckets store (KP:42-45): FIFO
-//                        head/tail node slots, resting count and quantity, tail oid.
+//                        head/tail node slots, resting quantity, tail oid.
 //   Node[P]              order-node pool = the Orders store (KP:46-49), one 64-byte line per order.
 //   oid table            open-addressing oid -> node slot (lazy deletion: entries are validated
 //                        against the node, stale ones are dropped at rebuild).
@@ -37,7 +37,7 @@ enum Action : int32_t {
 
 struct alignas(32) Level {         // one bucket (KP:379-389)
     int32_t head, tail;            // node slots, -1 = none
-    int32_t count, _pad;
+    int32_t _pad[2];
     int64_t qty;                   // sum of resting sizes (sweep scan, top of book)
     int64_t tail_oid;              // oid of the tail node (OUT.prev on append, KP:217)
 };
@@ -73,24 +73,32 @@ static_assert(sizeof(TradeTmp) == 40, "TradeTmp");
 
 struct PosEntry { int64_t k0, k1, v0, v1; };   // Positions: UUID(aid,sid) -> UUID(amount,available)
 
-// Counters block (u64 words).
+// Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
+// counters never contend for one L2 line.
 enum Ctr : int {
     C_ERR = 0,         // (index << 16) | (detail << 8) | status; UINT64_MAX = none
     C_TRADES, C_RESTS, C_VISITS, C_CANCEL_OK, C_ORDERS,
-    C_TTMP,            // trade scratch records reserved
+    C_TTMP,            // trade scratch records reserved in the overflow region
     C_POOL_BUMP,       // pool slots handed out in chunks
     C_OTAB_USED,       // non-empty oid-table slots
     C_ACCT_OPS,        // FUNDED: account records in the epoch
     C_BAL_USED, C_POS_USED,
     C_NCTR = 16
 };
+constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
+constexpr int ci(int k) { return k * CTR_STRIDE; }
+// Trade scratch shards (k_match -> k_scatter): shard s = group & (TSHARDS - 1) reserves records
+// in its own region [s * tshard_cap, (s + 1) * tshard_cap) through its own counter line; a shard
+// that runs full spills to the overflow region behind them (counter C_TTMP).
+constexpr int TSHARDS = 256;
+enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2 };
 
 constexpr uint64_t OID_SALT = 0x8000000000000000ull;   // stored key = oid ^ SALT, 0 = empty
 
 struct DevState {
     int32_t G, mode, A, passes;
-    uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;
-    uint32_t bal_mask, pos_mask, trades_cap, _pad;
+    uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
+    uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
     KG GroupState* grp;
     KG Level* lev;
     KG Node* pool;
@@ -119,8 +127,9 @@ struct DevState {
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;
     KG uint32_t* seg;
-    KG TradeTmp* ttmp;
-    KG unsigned long long* ctr;
+    KG TradeTmp* ttmp;                // TSHARDS regions of tshard_cap, then the overflow region
+    KG unsigned long long* tsh;       // TSHARDS x CTR_STRIDE words (TShardWord in each line)
+    KG unsigned long long* ctr;       // C_NCTR x CTR_STRIDE words
     KG unsigned long long* dbg;     // diagnostic stamps (KME_STAMPS builds), G x 16 words
 };
 

@@ -80,13 +80,15 @@ KDEV uint64_t err_code(int status, int detail, int64_t idx) {
     return (ix << 16) | ((uint64_t)(detail & 0xFF) << 8) | (uint64_t)(status & 0xFF);
 }
 KDEV void raise_thread(unsigned long long* ctr, int status, int detail, int64_t idx) {
-    atomicMin(&ctr[C_ERR], (unsigned long long)err_code(status, detail, idx));
+    atomicMin(&ctr[ci(C_ERR)], (unsigned long long)err_code(status, detail, idx));
 }
 KDEV void raise_wave(unsigned long long* ctr, int status, int detail, int64_t idx) {
-    if (lane_id() == 0) atomicMin(&ctr[C_ERR], (unsigned long long)err_code(status, detail, idx));
+    // every lane issues the (idempotent) atomicMin: a lane-0 branch here, inside the matching
+    // loops, makes the compiler treat their exits as divergent (uniform state moves to VGPRs)
+    atomicMin(&ctr[ci(C_ERR)], (unsigned long long)err_code(status, detail, idx));
 }
 KDEV bool failed(const unsigned long long* ctr) {
-    return __hip_atomic_load(&ctr[C_ERR], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ~0ull;
+    return __hip_atomic_load(&ctr[ci(C_ERR)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ~0ull;
 }
 
 // ------------------------------------------------------------------ the book bit scans (KP:359-416)
@@ -250,11 +252,11 @@ __global__ void k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
                 }
             }
         } else if (funded && (a == CREATE_BALANCE || a == TRANSFER)) {
-            atomicAdd(&S.ctr[C_ACCT_OPS], 1ull);
+            atomicAdd(&S.ctr[ci(C_ACCT_OPS)], 1ull);
         }
     }
     const unsigned long long nb = __ballot(is_order);
-    if (lane_id() == 0 && nb) atomicAdd(&S.ctr[C_ORDERS], (unsigned long long)__popcll(nb));
+    if (lane_id() == 0 && nb) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)__popcll(nb));
 }
 
 KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int32_t size, bool has_prev, int64_t prev) {
@@ -268,7 +270,7 @@ KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int3
 // createBalance KP:131-138; transfer KP:140-146 with the balance replaced by the reservation
 // bound: a debit is accepted only when it provably passes, otherwise KME_E_UNFUNDED.
 __global__ void k_ledger_funded(DevState S, EpochIO io) {
-    if (S.ctr[C_ACCT_OPS] == 0 || failed(S.ctr)) return;
+    if (S.ctr[ci(C_ACCT_OPS)] == 0 || failed(S.ctr)) return;
     const int lane = lane_id();
     for (uint32_t base = 0; base < io.n; base += 64) {
         const uint32_t i = base + lane;
@@ -524,97 +526,55 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t* out, uint32_t L, con
     }
 }
 
-// ------------------------------------------------------------------ (2) the matching core
-// One input record as the group / serial wavefront consumes it (wave-uniform, SGPR-resident).
-struct Rec {
-    uint32_t i;
-    int32_t action, price, size, acct_ok;
-    int64_t oid, aid, sid, tgt;
-};
-// 64 records staged across the lanes of a wavefront: lane l holds record k0 + l.  One gather per
-// 64 records replaces two dependent global round trips per record (perm[k], then the fields).
-struct Batch {
-    uint32_t i;
-    int32_t action, price, size, acct_ok;
-    int64_t oid, aid, sid, tgt;
-};
+// ------------------------------------------------------------------ record staging helpers
 // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding (vmcnt bits 3:0 and 15:14)
 constexpr int VMCNT0 = 0x0F70;
 KDEV int32_t rl32(int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
-// lane j of v := x (v_cmp + v_cndmask; x and j are wave-uniform)
-KDEV int32_t lane_put(int32_t x, int j, int32_t v) { return lane_id() == j ? x : v; }
 KDEV int64_t rl64(int64_t v, int j) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-KDEV Batch load_batch(const DevState& S, const EpochIO& io, bool valid, uint32_t i, bool funded) {
-    Batch B;
-    B.i = i;
-    if (valid) {
-        B.action = io.action[i]; B.price = io.price[i]; B.size = io.size[i];
-        B.oid = io.oid[i]; B.aid = io.aid[i]; B.sid = io.sid[i];
-        B.tgt = S.cancel_tgt[i];
-        B.acct_ok = funded ? (int32_t)S.acct_ok[i] : 0;
-    } else {
-        B.action = -1; B.price = B.size = B.acct_ok = 0; B.oid = B.aid = B.sid = B.tgt = 0;
-    }
-    return B;
-}
-KDEV Rec pick(const Batch& B, int j) {
-    Rec r;
-    r.i = (uint32_t)rl32((int32_t)B.i, j);
-    r.action = rl32(B.action, j); r.price = rl32(B.price, j); r.size = rl32(B.size, j);
-    r.acct_ok = rl32(B.acct_ok, j);
-    r.oid = rl64(B.oid, j); r.aid = rl64(B.aid, j); r.sid = rl64(B.sid, j); r.tgt = rl64(B.tgt, j);
-    return r;
-}
+// One input record as a wavefront consumes it (wave-uniform, SGPR-resident).
+struct Rec {
+    uint32_t i;
+    int32_t action, price, size, acct_ok;
+    int64_t oid, aid, sid, tgt;
+    int32_t lane;                 // lane of the record in its batch
+};
+// What process() decided for one record (the OUT echo fields and its trade count).
+struct Out {
+    int32_t action, size;
+    int64_t prev;
+    bool has_prev;
+    bool rested;                  // the order came to rest (counted per batch, not per record)
+    uint32_t ntr;
+};
 
 struct Taker {
     int32_t action, price, size, _pad;
     int64_t oid, aid, sid;
 };
 
-// What process() decided for one record (the OUT echo fields and its trade count).
-struct Out {
-    int32_t action, size;
-    int64_t prev;
-    bool has_prev;
-    bool rested;          // the order came to rest (counted per batch, not per record)
-    uint32_t ntr;
-};
-
-constexpr int FSTACK = 256;       // LDS free-slot stack of a group wavefront
-constexpr int DIRTY_WORDS = 64;   // 2048-bit per-batch filter of node slots written in the batch
-
-// Book state of the current symbol group, held in registers (bitmaps, free list) and, for the
-// parallel kernel, price levels staged in LDS on first touch and written back at the end.
-template <bool EXACT, bool LDS>
+// EXACT mode (k_serial): the whole epoch in arrival order on one wavefront, every store -- the
+// book stores and the Balances / Positions ledger -- exact.  The current symbol group's bitmaps
+// and free list are held in registers; levels and nodes are read and written in HBM.
 struct Core {
+    static constexpr bool EXACT = true;
     const DevState& S;
     const EpochIO& io;
-    Level* cache;                     // LDS [2][NLEV] (LDS == true)
     int32_t g;
     int32_t exists;
     uint64_t b0l, b0m, b1l, b1m;      // bitmaps of book +g (side 0) and book -g (side 1)
-    int32_t* fstack;                  // LDS free-slot stack (LDS == true)
-    int32_t fsp;
-    uint32_t* dirty;                  // LDS per-batch written-slot filter (LDS == true)
-    Node* nodepf;                     // LDS cancel-target nodes prefetched with the batch (LDS == true)
     int32_t free_head, chunk_next, chunk_end;
     Level* glev;
-    uint32_t tnext, tend;             // FUNDED: trade scratch chunk; EXACT: running trade count
+    uint32_t tnext;                   // running trade count of the epoch
     bool dead;
-#ifdef KME_STAMPS
-    unsigned long long acc[16];
-#endif
 
-    KDEV Core(const DevState& s, const EpochIO& e, Level* c, int32_t* fs, uint32_t* dty, Node* npf)
-        : S(s), io(e), cache(c), fstack(fs), dirty(dty), nodepf(npf) {
-        g = -1; exists = 0; b0l = b0m = b1l = b1m = 0; fsp = 0;
+    KDEV Core(const DevState& s, const EpochIO& e) : S(s), io(e) {
+        g = -1; exists = 0; b0l = b0m = b1l = b1m = 0;
         free_head = -1; chunk_next = chunk_end = 0; glev = nullptr;
-        tnext = tend = 0; dead = false;
-        KST(for (int q = 0; q < 16; ++q) acc[q] = 0;)
+        tnext = 0; dead = false;
     }
 
     KDEV void die(int status, int detail, int64_t idx) { raise_wave(S.ctr, status, detail, idx); dead = true; }
@@ -626,35 +586,9 @@ struct Core {
         b0l = G.bm0_lsb; b0m = G.bm0_msb; b1l = G.bm1_lsb; b1m = G.bm1_msb;
         free_head = G.free_head; chunk_next = G.chunk_next; chunk_end = G.chunk_end;
         glev = S.lev + (size_t)gg * 2 * NLEV;
-        fsp = 0;
-        if (LDS) stage_levels(true);
-    }
-    // Occupied levels of both books move between HBM and LDS in one parallel pass (lane l takes
-    // prices l and l + 64); an unoccupied level's fields are dead until a rest rewrites them all.
-    KDEV void stage_levels(bool in) {
-        const int lane = lane_id();
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const uint64_t l = side ? b1l : b0l, m = side ? b1m : b0m;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int p = lane + 64 * h;
-                if (p <= 126 && check_bit(l, m, p)) {
-                    int4* c = reinterpret_cast<int4*>(&cache[side * NLEV + p]);
-                    int4* gl = reinterpret_cast<int4*>(&glev[side * NLEV + p]);
-                    if (in) { const int4 x0 = gl[0], x1 = gl[1]; c[0] = x0; c[1] = x1; }
-                    else { const int4 x0 = c[0], x1 = c[1]; gl[0] = x0; gl[1] = x1; }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
     }
     KDEV void store_group() {
         if (g < 0) return;
-        if (LDS) {
-            stage_levels(false);
-            flush_free_stack();
-        }
         {
             GroupState& G = S.grp[g];
             G.exists = exists;
@@ -667,7 +601,7 @@ struct Core {
     KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
 
     KDEV Level* lv(int side, int32_t p) {
-        return LDS ? &cache[side * NLEV + p] : &glev[side * NLEV + p];
+        return &glev[side * NLEV + p];
     }
 
     KDEV Node ld_node(int32_t s) const {
@@ -679,36 +613,17 @@ struct Core {
         return n;
     }
 
-    // Node slots.  Parallel kernel (LDS): an LDS stack of free slots; the group's free slots kept
-    // between epochs are a list of BLOCKS, each a free 64-byte slot holding up to FBLK - 1 more
-    // free slot ids (word 0 = next block, word 1 = count, words 2.. = ids; word 14 = Node::live
-    // stays 0).  One load refills the stack with a whole block.  Serial kernel: a plain list
-    // linked through Node::next.  Last resort: a chunk from the pool's bump counter.
-    static constexpr int FBLK = 13;
+    // Node slots: the group's free list linked through Node::next, else a chunk of the pool's
+    // bump counter.
     KDEV int32_t alloc_slot(int64_t idx) {
-        if (LDS) {
-            if (fsp > 0) return fstack[--fsp];
-            if (free_head >= 0) {
-                const int32_t blk = free_head;
-                const int lane = lane_id();
-                const int32_t w = lane < 2 + FBLK - 1 ? reinterpret_cast<const int32_t*>(&S.pool[blk])[lane] : 0;
-                const int32_t nxt = __builtin_amdgcn_readlane(w, 0);
-                const int32_t cnt = __builtin_amdgcn_readlane(w, 1);
-                if (lane >= 2 && lane < 2 + cnt) fstack[lane - 2] = w;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                fsp = cnt;
-                free_head = nxt;
-                return blk;
-            }
-        } else if (free_head >= 0) {
+        if (free_head >= 0) {
             const int32_t s = free_head;
             free_head = S.pool[s].next;
             return s;
         }
         if (chunk_next >= chunk_end) {
             unsigned long long c = 0;
-            if (lane_id() == 0) c = atomicAdd(&S.ctr[C_POOL_BUMP], (unsigned long long)POOL_CHUNK);
+            if (lane_id() == 0) c = atomicAdd(&S.ctr[ci(C_POOL_BUMP)], (unsigned long long)POOL_CHUNK);
             c = bcast64(c);
             if (c + POOL_CHUNK > S.pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL, idx); return -1; }
             chunk_next = (int32_t)c;
@@ -718,48 +633,8 @@ struct Core {
     }
     KDEV void free_slot(int32_t s) {
         S.pool[s].live = 0;
-        mark_dirty(s);
-        if (LDS) {
-            if (fsp == FSTACK) spill_blocks(FSTACK - FBLK, FSTACK);
-            fstack[fsp++] = s;
-            return;
-        }
         S.pool[s].next = free_head;
         free_head = s;
-    }
-    // Writes stack entries [b, e) as blocks of FBLK slots (the last slot of each block holds the
-    // others' ids), chained onto the group's block list; all lanes in parallel, stores only.
-    KDEV void spill_blocks(int b, int e) {
-        const int n = e - b;
-        const int nblk = (n + FBLK - 1) / FBLK;
-        for (int k = lane_id(); k < nblk * 14; k += 64) {
-            const int blk = k / 14, word = k - blk * 14;
-            const int base = b + blk * FBLK;
-            const int cnt = imin(FBLK, e - base);                // slots in this block incl. itself
-            const int32_t host = fstack[base + cnt - 1];
-            int32_t v;
-            if (word == 0) v = blk == 0 ? free_head : fstack[base - 1];   // previous block's host
-            else if (word == 1) v = cnt - 1;
-            else v = word - 2 < cnt - 1 ? fstack[base + word - 2] : -1;
-            reinterpret_cast<int32_t*>(&S.pool[host])[word] = v;
-        }
-        free_head = fstack[b + (nblk - 1) * FBLK + imin(FBLK, e - (b + (nblk - 1) * FBLK)) - 1];
-        fsp = b;
-    }
-    // The LDS stack joins the group's block list when the group is written back.
-    KDEV void flush_free_stack() {
-        if (!LDS || fsp == 0) return;
-        spill_blocks(0, fsp);
-    }
-    // Per-batch filter of node slots written since the batch's cancel-target prefetch.
-    KDEV void mark_dirty(int32_t s) {
-        if (!LDS) return;
-        if (lane_id() == 0)
-            __hip_atomic_fetch_or(&dirty[(s >> 5) & (DIRTY_WORDS - 1)], 1u << (s & 31), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    KDEV bool is_dirty(int32_t s) const {
-        return (dirty[(s >> 5) & (DIRTY_WORDS - 1)] >> (s & 31)) & 1u;
     }
 
     // ---------------- exact ledger (EXACT only): device hash tables, one wavefront, plain loads
@@ -776,8 +651,8 @@ struct Core {
         uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
         while (S.bal_state[h] != 0) h = (h + 1) & S.bal_mask;
         S.bal_key[h] = aid; S.bal_val[h] = v; S.bal_state[h] = 1;
-        const unsigned long long used = S.ctr[C_BAL_USED] + 1;
-        S.ctr[C_BAL_USED] = used;
+        const unsigned long long used = S.ctr[ci(C_BAL_USED)] + 1;
+        S.ctr[ci(C_BAL_USED)] = used;
         if (used * 2 > (unsigned long long)S.bal_mask + 1) die(KME_E_CAPACITY, KME_D_CAP_LEDGER, idx);
     }
     KDEV int32_t pos_find(int64_t k0, int64_t k1, int32_t* free_slot_out) const {
@@ -810,8 +685,8 @@ struct Core {
             if (fs < 0) { die(KME_E_CAPACITY, KME_D_CAP_LEDGER, idx); return; }
             h = fs;
             if (S.pos_state[h] == 0) {
-                const unsigned long long used = S.ctr[C_POS_USED] + 1;
-                S.ctr[C_POS_USED] = used;
+                const unsigned long long used = S.ctr[ci(C_POS_USED)] + 1;
+                S.ctr[ci(C_POS_USED)] = used;
                 if (used * 4 > ((unsigned long long)S.pos_mask + 1) * 3) { die(KME_E_CAPACITY, KME_D_CAP_LEDGER, idx); return; }
             }
             S.pos[h].k0 = k0; S.pos[h].k1 = k1; S.pos_state[h] = 1;
@@ -915,58 +790,34 @@ struct Core {
     }
 
     // ---------------- trades
-    KDEV void emit(uint32_t i, uint32_t ord, const Node& m, int32_t ts) {
-        if (EXACT) {
-            if (tnext >= io.trades_cap) { die(KME_E_CAPACITY, KME_D_CAP_TRADES, i); return; }
-            if (lane_id() == 0) {
-                TradeRec& r = io.trades[tnext];
-                r.moid = m.oid; r.maid = m.aid; r.msid = m.sid; r.mprice = m.price; r.size = ts;
-            }
-            tnext++;
-        } else {
-            if (tnext >= tend) {
-                unsigned long long c = 0;
-                if (lane_id() == 0) c = atomicAdd(&S.ctr[C_TTMP], (unsigned long long)TRADE_CHUNK);
-                c = bcast64(c);
-                if (c + TRADE_CHUNK > S.ttmp_cap) { die(KME_E_CAPACITY, KME_D_CAP_TRADES, i); return; }
-                tnext = (uint32_t)c;
-                tend = (uint32_t)(c + TRADE_CHUNK);
-            }
-            if (lane_id() == 0) {
-                TradeTmp& r = S.ttmp[tnext];
-                r.t.moid = m.oid; r.t.maid = m.aid; r.t.msid = m.sid; r.t.mprice = m.price; r.t.size = ts;
-                r.seq = (int32_t)i; r.ord = (int32_t)ord;
-            }
-            tnext++;
+    // the trades go straight to their arrival-order slots: the epoch runs in one wavefront
+    KDEV void emit(uint32_t i, const Node& m, int32_t ts) {
+        if (tnext >= io.trades_cap) { die(KME_E_CAPACITY, KME_D_CAP_TRADES, i); return; }
+        if (lane_id() == 0) {
+            TradeRec& r = io.trades[tnext];
+            r.moid = m.oid; r.maid = m.aid; r.msid = m.sid; r.mprice = m.price; r.size = ts;
         }
-    }
-    KDEV void close_trade_chunk() {
-        if (EXACT) return;
-        for (uint32_t k = tnext + lane_id(); k < tend; k += 64) S.ttmp[k].seq = -1;
-        tnext = tend;
+        tnext++;
     }
 
     // ---------------- tryMatch, KP:225-263
-    // The level being swept lives in registers (head, count, qty) and is written back once when
-    // the sweep stops inside it; a level swept empty is not written at all (its bit is cleared and
-    // an unoccupied level's fields are dead until a rest rewrites them).  A maker's price is the
-    // index of its level, so the loop test of KP:237 -- ((size > 0 && isBuy) ? maker.price <= P :
-    // maker.price >= P), H3 -- needs no node load, and the next maker's node is requested before
-    // the stores of the current trade (vmcnt is in order: a load issued after stores waits for
-    // them).
+    // The loop test of KP:237 parses as ((size > 0 && isBuy) ? maker.price <= P : maker.price >= P)
+    // (H3).  The level being swept lives in registers and is written back once where the sweep
+    // stops; a level swept empty is not written (its bit is cleared, its fields are dead until a
+    // rest rewrites them).
     KDEV bool crosses(bool is_buy, int32_t size, int32_t mprice, int32_t P) const {
         return (size > 0 && is_buy) ? mprice <= P : mprice >= P;
     }
     // executeTrade (KP:265-274): the trade record, and in EXACT mode both fillOrder calls.
     KDEV void trade(uint32_t i, uint32_t& ntr, const Node& m, const Taker& t, int32_t ts, bool is_buy) {
-        emit(i, ntr++, m, ts);
-        if (EXACT && !dead) {
+        emit(i, m, ts);
+        ntr++;
+        if (!dead) {
             fill_order(is_buy ? SOLD : BOUGHT, m.aid, m.sid, 0, ts, i);                              // maker fill
             if (!dead) fill_order(is_buy ? BOUGHT : SOLD, t.aid, t.sid, jisub(t.price, m.price), ts, i);  // taker fill
         }
     }
     KDEV bool try_match(uint32_t i, Taker& t, uint32_t& ntr) {
-        KST(unsigned long long tq = stamp();)
         const bool is_buy = t.action == BUY;
         const int64_t key = jlmul(t.sid, is_buy ? 1 : -1);
         const int os = jlneg(key) < 0 ? 1 : 0;           // opposite book (the same book for sid 0)
@@ -977,14 +828,12 @@ struct Core {
         const int32_t P = t.price;
         if (!crosses(is_buy, t.size, pb, P)) return t.size == 0;
         Level* L = lv(os, pb);
-        int32_t ms = L->head, lcnt = L->count;
+        int32_t ms = L->head;
         int64_t lqty = L->qty;
         if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
         Node m = ld_node(ms);
         bool head_moved = false;                             // ms is a later maker of level L
-        KST(acc[10] += stamp() - tq;)
         for (;;) {
-            KST(tq = stamp(); acc[14] += 1;)
             const int32_t ts = imin(t.size, m.size);
             const int32_t msize = jisub(m.size, ts);
             t.size = jisub(t.size, ts);
@@ -994,12 +843,10 @@ struct Core {
                 if (dead) return false;
                 S.pool[ms].size = msize;
                 if (head_moved) { L->head = ms; S.pool[ms].prev = -1; }
-                mark_dirty(ms);
-                L->count = lcnt; L->qty = lqty;
-                KST(acc[13] += stamp() - tq;)
+                L->qty = lqty;
                 return t.size == 0;
             }
-            lcnt -= 1;                                       // maker consumed: orders.delete (KP:243)
+            // maker consumed: orders.delete (KP:243)
             int32_t nms;
             bool same_level = m.next >= 0;
             if (same_level) {
@@ -1008,9 +855,7 @@ struct Core {
                     trade(i, ntr, m, t, ts, is_buy);
                     if (dead) return false;
                     free_slot(ms);
-                    L->head = nms; S.pool[nms].prev = -1; mark_dirty(nms);
-                    L->count = lcnt; L->qty = lqty;
-                    KST(acc[13] += stamp() - tq;)
+                    L->head = nms; S.pool[nms].prev = -1;                    L->qty = lqty;
                     return t.size == 0;
                 }
             } else {                                         // level exhausted (KP:244-253)
@@ -1023,11 +868,10 @@ struct Core {
                     if (dead) return false;
                     free_slot(ms);
                     if (pb != -1 && !check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET, i); return false; }
-                    KST(acc[13] += stamp() - tq;)
                     return t.size == 0;
                 }
                 L = lv(os, pb);
-                nms = L->head; lcnt = L->count; lqty = L->qty;
+                nms = L->head; lqty = L->qty;
                 if (nms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER, i); return false; }
             }
             const Node nm = ld_node(nms);                   // in flight during this trade's stores
@@ -1037,7 +881,6 @@ struct Core {
             head_moved = same_level;
             m = nm;
             ms = nms;
-            KST(acc[12] += stamp() - tq;)
         }
     }
 
@@ -1048,45 +891,40 @@ struct Core {
         uint64_t lo = bl(s), hi = bm(s);                     // books.get(sid) again (KP:205)
         const int32_t p = t.price;
         if (p < 0 || p > 126) { die(KME_E_DOMAIN, KME_D_PRICE, i); return; }
-        KST(const unsigned long long ta = stamp();)
         const int32_t slot = alloc_slot(i);
-        KST(acc[15] += stamp() - ta;)
         if (dead) return;
         Level* L = lv(s, p);
         int32_t nprev = -1;
         has_prev = false;
         prev_oid = 0;
         if (!check_bit(lo, hi, p)) {                        // new bucket (oid, oid), set bit (KP:209-211)
-            L->head = slot; L->tail = slot; L->count = 1; L->qty = t.size; L->tail_oid = t.oid;
+            L->head = slot; L->tail = slot; L->qty = t.size; L->tail_oid = t.oid;
             set_bit(lo, hi, p);
             set_bm(s, lo, hi);
         } else {                                             // append at the tail (KP:213-219)
             const int32_t tl = L->tail;
             S.pool[tl].next = slot;
-            mark_dirty(tl);
             has_prev = true;
             prev_oid = L->tail_oid;
             nprev = tl;
-            L->tail = slot; L->tail_oid = t.oid; L->count += 1; L->qty += t.size;
+            L->tail = slot; L->tail_oid = t.oid; L->qty += t.size;
         }
         Node* nd = &S.pool[slot];
         nd->oid = t.oid; nd->aid = t.aid; nd->sid = t.sid; nd->prev_oid = prev_oid;
         nd->size = t.size; nd->next = -1; nd->prev = nprev; nd->group = g;
         nd->price = p; nd->action = t.action; nd->live = 1; nd->_pad = 0;
-        mark_dirty(slot);
         S.rest_slot[i] = slot;
     }
 
     // ---------------- removeOrder, KP:289-323
-    KDEV bool remove_order(const Rec& r, int j) {
+    KDEV bool remove_order(const Rec& r) {
         const uint32_t i = r.i;
         const int64_t tgt = r.tgt;
         int32_t slot = -1;
         if (tgt >= 0) slot = (int32_t)tgt;
         else if (tgt <= -2) slot = S.rest_slot[-(tgt + 2)];
         if (slot < 0) return false;
-        // the batch prefetched pre-epoch targets into LDS; valid unless written since
-        const Node o = (LDS && j >= 0 && tgt >= 0 && !is_dirty(slot)) ? nodepf[j] : ld_node(slot);
+        const Node o = ld_node(slot);
         if (!o.live || o.oid != r.oid) return false;       // orders.get(oid) == null
         if (o.aid != r.aid) return false;                  // order.aid != aid (KP:291)
         if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK, i); return false; }
@@ -1100,23 +938,18 @@ struct Core {
         } else if (o.prev < 0) {
             L->head = o.next;
             S.pool[o.next].prev = -1;
-            mark_dirty(o.next);
         } else if (o.next < 0) {
             L->tail = o.prev;
             L->tail_oid = o.prev_oid;
             S.pool[o.prev].next = -1;
-            mark_dirty(o.prev);
         } else {
             S.pool[o.prev].next = o.next;
             S.pool[o.next].prev = o.prev;
             S.pool[o.next].prev_oid = o.prev_oid;
-            mark_dirty(o.prev);
-            mark_dirty(o.next);
         }
-        L->count -= 1;
         L->qty -= o.size;
         free_slot(slot);
-        if (EXACT) post_remove_adjustments(o, i);
+        post_remove_adjustments(o, i);
         return !dead;
     }
 
@@ -1128,7 +961,7 @@ struct Core {
     }
 
     // ---------------- one record of this group (MatchingEngine.process, KP:96-126)
-    KDEV Out process(const Rec& r, int j) {
+    KDEV Out process(const Rec& r) {
         const uint32_t i = r.i;
         const int32_t a = r.action;
         bool ok = false, has_prev = false;
@@ -1137,7 +970,7 @@ struct Core {
         uint32_t ntr = 0;
         Out out;
         out.action = a; out.size = r.size; out.prev = 0; out.has_prev = false; out.rested = false; out.ntr = 0;
-        if (EXACT) io.trade_off[i] = tnext;
+        io.trade_off[i] = tnext;
         switch (a) {
         case ADD_SYMBOL:                                    // addSymbol, KP:184-191
             if (!exists) { exists = 1; b0l = b0m = b1l = b1m = 0; ok = true; }
@@ -1150,8 +983,7 @@ struct Core {
             } else {
                 ok = a == REMOVE_SYMBOL;
                 if (a == PAYOUT) {
-                    if (EXACT) payout_settle(r.sid, r.size, i);
-                    else die(KME_E_UNSUPPORTED, KME_D_NONE, i);
+                    payout_settle(r.sid, r.size, i);
                     if (dead) return out;
                 }
             }
@@ -1164,23 +996,16 @@ struct Core {
             Taker t;
             t.action = a; t.price = r.price; t.size = r.size; t._pad = 0;
             t.oid = r.oid; t.aid = r.aid; t.sid = r.sid;
-            if (EXACT) {
-                if (!check_balance(t, i)) { if (dead) return out; break; }
-            } else {
-                if (!r.acct_ok) break;                      // balances.get(aid) == null
-            }
-            KST(const unsigned long long t0 = stamp();)
+            if (!check_balance(t, i)) { if (dead) return out; break; }
             const bool filled = try_match(i, t, ntr);
-            KST(const unsigned long long t1 = stamp(); acc[4] += t1 - t0;)
             if (dead) return out;
             if (!filled) { rest(i, t, has_prev, prev_oid); if (dead) return out; out.rested = true; }
-            KST(acc[5] += stamp() - t1;)
             ok = true;
             out_size = t.size;
             break;
         }
         case CANCEL:
-            ok = remove_order(r, j);
+            ok = remove_order(r);
             if (dead) return out;
             break;
         default:
@@ -1196,12 +1021,552 @@ struct Core {
 
 };
 
+// ================================================================== (2)+(3) FUNDED matching
+// One 64-lane wavefront owns one symbol group |sid| for the epoch (books +g and -g, KP:184-191;
+// sid 0 is one shared book, H4) and runs MatchingEngine.process (KP:96-126) over the group's
+// records in arrival order.  The program is wave-uniform: every loaded value that steers control
+// flow goes through readfirstlane / readlane into an SGPR, so branches are scalar (s_cbranch on
+// SCC), never exec-masked.  Where the book lives:
+//   * price levels of both books (Buckets, KP:42-45) in LDS as structure of arrays over prices
+//     0..100 (the FUNDED price domain, checked by k_emap): occupied ones are staged in when the
+//     group starts and written back when it ends;
+//   * the two 128-bit level bitmaps (Books, KP:38-41), free-list heads and counters in SGPRs;
+//   * resting orders (Orders, KP:46-49) in the HBM node pool, one 64-byte line each, read only to
+//     trade against a maker or to cancel (a cancel's node is prefetched with its batch);
+//   * records arrive 64 at a time, one per lane; the OUT fields and the trades collect in lanes
+//     and leave in coalesced stores (one per field per batch, one per 64 trades).
+constexpr int LVP = 104;          // LDS level entries per book side: prices 0..100 (+ pad)
+constexpr int FSTK = 128;         // LDS free-slot stack
+constexpr int DIRTY_WORDS = 64;   // 2048-bit filter of node slots written since the batch prefetch
+constexpr int FBLK = 13;          // free slots per spilled free-list block (GroupWave::alloc_slot)
+
+struct GroupLds {
+    int2 ht[2 * LVP];             // head / tail node slot of level (side, price)
+    int64_t qty[2 * LVP];         // resting quantity (market data; the reference keeps none)
+    int64_t toid[2 * LVP];        // oid of the tail node = OUT.prev of an append (KP:213-217)
+    int32_t fstack[FSTK];
+    uint32_t dirty[DIRTY_WORDS];
+};
+
+KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// A whole 64-byte node into 16 SGPRs through the scalar memory path.  Vector loads and stores share
+// one in-order counter (vmcnt), so a vector load of a maker waits for every store the wavefront
+// issued before it; a scalar load is counted by lgkmcnt and does not.  glc: the scalar cache is
+// bypassed (read from L2), so the line is never stale w.r.t. this wavefront's completed vector
+// stores; nodes written since the last vmcnt(0) (the batch dirty filter) take the vector path.
+// The wait sits in the same asm block: the compiler does not track this lgkmcnt event.
+typedef int32_t v16i __attribute__((ext_vector_type(16)));
+KDEV v16i sload_node(const KG Node* p) {
+    const uint64_t a = bcast64((uint64_t)(uintptr_t)p);   // an SGPR pair even where the compiler
+    v16i r;                                                // would keep the address in VGPRs
+    asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(a) : "memory");
+    return r;
+}
+KDEV int64_t U64(int64_t v) { return (int64_t)bcast64((uint64_t)v); }
+KDEV int64_t mk64(int32_t lo, int32_t hi) { return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo); }
+KDEV int32_t lo32(int64_t v) { return (int32_t)(uint32_t)(uint64_t)v; }
+KDEV int32_t hi32(int64_t v) { return (int32_t)(uint32_t)((uint64_t)v >> 32); }
+
+// Overflow path of GroupWave::flush_trades: marks this reservation's share of the shard region
+// as holes and reserves n records in the overflow region; ~0 when that is full too.
+__device__ __attribute__((noinline)) uint64_t trade_overflow(KG TradeTmp* ttmp, KG unsigned long long* ctr, uint32_t tbase,
+                                                             uint32_t tshard_cap, uint32_t ttmp_cap, uint64_t base, uint32_t n) {
+    const int lane = lane_id();
+    if (base < tshard_cap && (uint64_t)lane < tshard_cap - base) ttmp[tbase + base + lane].seq = -1;
+    unsigned long long ob = 0;
+    if (lane == 0) ob = atomicAdd(&ctr[ci(C_TTMP)], (unsigned long long)n);
+    ob = bcast64(ob);
+    if (ob + n > ttmp_cap) return ~(uint64_t)0;
+    return (uint64_t)TSHARDS * tshard_cap + ob;
+}
+
+// A maker as tryMatch reads it (KP:236-241, 266): oid, aid, sid, size, next.  Lane q of the
+// wavefront loads 16-byte piece q of the 64-byte node; readlane picks the fields.
+struct Maker {
+    int64_t oid, aid, sid;
+    int32_t size, next;
+};
+// A resting order as removeOrder reads it (KP:290-323), already validated against the cancel.
+struct Victim {
+    int32_t ok;                   // live, same oid and same aid (KP:290-291)
+    int32_t side, price, size, next, prev;
+    int64_t prev_oid;
+};
+
+// 64 records staged across the lanes (lane l = record k0 + l of the group's segment), with the
+// node of each cancel's target prefetched: one gather per 64 records instead of dependent round
+// trips per record.
+struct Lanes {
+    uint32_t i;
+    int32_t action, price, size, acct_ok;
+    int64_t oid, aid, sid, tgt;
+    int32_t pf_slot, pf_ok, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8
+    int64_t pf_poid;
+};
+
+// Diagnostic stamp slots of the -DKME_STAMPS build (cycles unless named n_*), per group.
+enum Stamp : int {
+    ST_GROUP_IN = 0, ST_BATCH, ST_TRADE_REC, ST_REST_REC, ST_CANCEL_REC, ST_OTHER_REC, ST_GROUP_OUT, ST_KERNEL,
+    ST_N_TRADE_REC, ST_N_REST_REC, ST_N_CANCEL_REC, ST_MAKER_WAIT, ST_N_MAKER, ST_VICTIM_WAIT, ST_N_VICTIM, ST_FLUSH,
+    ST_REST_ALLOC, ST_REST_LEVEL, ST_REST_NODE, ST_REC_PICK, ST_REC_OUT, ST_TM_PRE, ST_REST_PRE,
+    ST_N = 32
+};
+
+struct GroupWave {
+    KG Node* pool;
+    KG Level* lev;                // this group's [2][NLEV] HBM levels
+    KG GroupState* gst;
+    KG TradeTmp* ttmp;
+    KG unsigned long long* ctr;
+    KG unsigned long long* tsh;       // this group's trade shard line
+    KG int32_t* rest_slot;
+    uint32_t pool_cap, ttmp_cap, tshard_cap, tbase;   // tbase: first record of the shard region
+    GroupLds& L;
+    const int lane, q;            // q = lane & 3: the node piece this lane loads / stores
+    int32_t g, exists;
+    uint64_t b0l, b0m, b1l, b1m;  // bitmaps of book +g (side 0) and book -g (side 1)
+    int32_t fsp, free_head, chunk_next, chunk_end;
+    int32_t tcnt;                 // trades collected in the lanes (lane k holds trade k)
+    int32_t t_oid0, t_oid1, t_aid0, t_aid1, t_sid0, t_sid1, t_px, t_sz, t_seq, t_ord;
+    uint32_t cur;                 // input index of the record being processed
+    bool dead;
+#ifdef KME_STAMPS
+    unsigned long long acc[ST_N];
+#endif
+
+    KDEV GroupWave(const DevState& S, GroupLds& lds, int32_t gg)
+        : pool(S.pool), lev(S.lev + (size_t)gg * 2 * NLEV), gst(S.grp + gg), ttmp(S.ttmp), ctr(S.ctr),
+          tsh(S.tsh + (size_t)(gg & (TSHARDS - 1)) * CTR_STRIDE), rest_slot(S.rest_slot), pool_cap(S.pool_cap),
+          ttmp_cap(S.ttmp_cap), tshard_cap(S.tshard_cap), tbase((uint32_t)(gg & (TSHARDS - 1)) * S.tshard_cap), L(lds),
+          lane(lane_id()),
+          q(lane_id() & 3), g(gg) {
+        exists = 0; b0l = b0m = b1l = b1m = 0;
+        fsp = 0; free_head = -1; chunk_next = chunk_end = 0;
+        tcnt = 0; t_oid0 = t_oid1 = t_aid0 = t_aid1 = t_sid0 = t_sid1 = t_px = t_sz = t_seq = t_ord = 0;
+        cur = 0; dead = false;
+        KST(for (int k = 0; k < ST_N; ++k) acc[k] = 0;)
+    }
+
+    KDEV void die(int status, int detail) { raise_wave(ctr, status, detail, (int64_t)cur); dead = true; }
+    KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
+    KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
+    KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
+    KDEV void sync_lds() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // ---------------- group state in and out
+    KDEV void load_group() {
+        const int4 v = reinterpret_cast<const KG int4*>(gst)[q];
+        b0l = (uint64_t)mk64(rl32(v.x, 0), rl32(v.y, 0)); b0m = (uint64_t)mk64(rl32(v.z, 0), rl32(v.w, 0));
+        b1l = (uint64_t)mk64(rl32(v.x, 1), rl32(v.y, 1)); b1m = (uint64_t)mk64(rl32(v.z, 1), rl32(v.w, 1));
+        exists = rl32(v.x, 2); free_head = rl32(v.y, 2); chunk_next = rl32(v.z, 2); chunk_end = rl32(v.w, 2);
+        stage_levels(true);
+    }
+    KDEV void store_group() {
+        stage_levels(false);
+        if (fsp > 0) spill_blocks(0, fsp);
+        const bool q0 = (q & 1) != 0, q1 = (q & 2) != 0;
+        const int32_t x = q1 ? exists : (q0 ? lo32((int64_t)b1l) : lo32((int64_t)b0l));
+        const int32_t y = q1 ? free_head : (q0 ? hi32((int64_t)b1l) : hi32((int64_t)b0l));
+        const int32_t z = q1 ? chunk_next : (q0 ? lo32((int64_t)b1m) : lo32((int64_t)b0m));
+        const int32_t w = q1 ? chunk_end : (q0 ? hi32((int64_t)b1m) : hi32((int64_t)b0m));
+        if (lane < 3) reinterpret_cast<KG int4*>(gst)[lane] = make_int4(x, y, z, w);
+    }
+    // Occupied levels of both books move between HBM (Level, 32 B) and LDS in one parallel pass:
+    // lane l takes prices l and l + 64.  An unoccupied level's fields are dead until a rest
+    // rewrites all of them, so only occupied ones move.
+    KDEV void stage_levels(bool in) {
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const uint64_t l = bl(side), m = bm(side);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int p = lane + 64 * h;
+                if (p <= 100 && check_bit(l, m, p)) {
+                    const int li = side * LVP + p;
+                    KG int4* gl = reinterpret_cast<KG int4*>(&lev[side * NLEV + p]);
+                    if (in) {
+                        const int4 x0 = gl[0], x1 = gl[1];
+                        L.ht[li] = make_int2(x0.x, x0.y);
+                        L.qty[li] = mk64(x1.x, x1.y);
+                        L.toid[li] = mk64(x1.z, x1.w);
+                    } else {
+                        const int2 ht = L.ht[li];
+                        const int64_t qt = L.qty[li], to = L.toid[li];
+                        gl[0] = make_int4(ht.x, ht.y, 0, 0);
+                        gl[1] = make_int4(lo32(qt), hi32(qt), lo32(to), hi32(to));
+                    }
+                }
+            }
+        }
+        sync_lds();
+    }
+
+    // ---------------- node slots
+    // Free slots: an LDS stack; the group's free slots kept between epochs are a list of BLOCKS,
+    // each a free 64-byte slot holding up to FBLK - 1 more free slot ids (word 0 = next block,
+    // word 1 = count, words 2.. = ids; word 14 = Node::live stays 0).  One load refills the stack
+    // with a whole block.  Last resort: a chunk of the pool's bump counter.
+    KDEV int32_t alloc_slot() {
+        if (fsp > 0) { --fsp; return U32(L.fstack[fsp]); }
+        if (free_head >= 0) {
+            const int32_t blk = free_head;
+            const int32_t w = lane < 2 + FBLK - 1 ? reinterpret_cast<const KG int32_t*>(&pool[blk])[lane] : 0;
+            const int32_t nxt = rl32(w, 0), cnt = rl32(w, 1);
+            if (lane >= 2 && lane < 2 + cnt) L.fstack[lane - 2] = w;
+            sync_lds();
+            fsp = cnt;
+            free_head = nxt;
+            return blk;
+        }
+        if (chunk_next >= chunk_end) {
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(&ctr[ci(C_POOL_BUMP)], (unsigned long long)POOL_CHUNK);
+            c = bcast64(c);
+            if (c + POOL_CHUNK > pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return -1; }
+            chunk_next = (int32_t)c;
+            chunk_end = (int32_t)(c + POOL_CHUNK);
+        }
+        return chunk_next++;
+    }
+    KDEV void free_slot(int32_t s) {
+        pool[s].live = 0;
+        mark_dirty(s);
+        if (fsp == FSTK) spill_blocks(FSTK - FBLK, FSTK);
+        L.fstack[fsp] = s;
+        ++fsp;
+    }
+    // Writes stack entries [b, e) as blocks of FBLK slots (the last slot of each block holds the
+    // others' ids), chained onto the group's block list; all lanes in parallel, stores only.
+    KDEV void spill_blocks(int b, int e) {
+        sync_lds();
+        const int n = e - b;
+        const int nblk = (n + FBLK - 1) / FBLK;
+        for (int k = lane; k < nblk * 14; k += 64) {
+            const int blk = k / 14, word = k - blk * 14;
+            const int base = b + blk * FBLK;
+            const int cnt = imin(FBLK, e - base);                // slots in this block incl. itself
+            const int32_t host = L.fstack[base + cnt - 1];
+            int32_t v;
+            if (word == 0) v = blk == 0 ? free_head : L.fstack[base - 1];   // previous block's host
+            else if (word == 1) v = cnt - 1;
+            else v = word - 2 < cnt - 1 ? L.fstack[base + word - 2] : -1;
+            reinterpret_cast<KG int32_t*>(&pool[host])[word] = v;
+        }
+        const int lb = b + (nblk - 1) * FBLK;
+        free_head = U32(L.fstack[lb + imin(FBLK, e - lb) - 1]);
+        fsp = b;
+    }
+    // Per-batch filter of node slots written since the batch's cancel-target prefetch (this wave
+    // is the only writer of its LDS, so a plain read-modify-write by all lanes is exact).
+    KDEV void mark_dirty(int32_t s) {
+        const int w = (s >> 5) & (DIRTY_WORDS - 1);
+        const uint32_t v = L.dirty[w];
+        L.dirty[w] = v | (1u << (s & 31));
+    }
+    KDEV bool is_dirty(int32_t s) const { return (U32((int32_t)L.dirty[(s >> 5) & (DIRTY_WORDS - 1)]) >> (s & 31)) & 1; }
+
+    KDEV Maker ld_maker(int32_t s) const {
+        Maker m;
+        if (!is_dirty(s)) {
+            const v16i v = sload_node(&pool[s]);
+            m.oid = mk64(v[0], v[1]); m.aid = mk64(v[2], v[3]); m.sid = mk64(v[4], v[5]);
+            m.size = v[8]; m.next = v[9];
+            return m;
+        }
+        const int4 v = reinterpret_cast<const KG int4*>(&pool[s])[q];
+        m.oid = mk64(rl32(v.x, 0), rl32(v.y, 0));
+        m.aid = mk64(rl32(v.z, 0), rl32(v.w, 0));
+        m.sid = mk64(rl32(v.x, 1), rl32(v.y, 1));
+        m.size = rl32(v.x, 2);
+        m.next = rl32(v.y, 2);
+        return m;
+    }
+
+    // ---------------- trades: lane k holds trade k until 64 are collected (or the group ends)
+    KDEV void emit(uint32_t ord, const Maker& m, int32_t mprice, int32_t ts) {
+        const bool me = lane == tcnt;
+        t_oid0 = me ? lo32(m.oid) : t_oid0; t_oid1 = me ? hi32(m.oid) : t_oid1;
+        t_aid0 = me ? lo32(m.aid) : t_aid0; t_aid1 = me ? hi32(m.aid) : t_aid1;
+        t_sid0 = me ? lo32(m.sid) : t_sid0; t_sid1 = me ? hi32(m.sid) : t_sid1;
+        t_px = me ? mprice : t_px; t_sz = me ? ts : t_sz;
+        t_seq = me ? (int32_t)cur : t_seq; t_ord = me ? (int32_t)ord : t_ord;
+        if (++tcnt == 64) flush_trades();
+    }
+    // Reserves tcnt records in the group's shard region through the shard's own counter line.  When
+    // the shard is full, the part of the region that reservation got ([base, cap)) is marked as
+    // holes and the batch goes to the overflow region (trade_overflow: out of line, because a
+    // second reservation site inline makes the compiler treat the enclosing loops' exits as
+    // divergent and demote their wave-uniform state to VGPRs).
+    KDEV void flush_trades() {
+        if (tcnt == 0) return;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&tsh[TS_USED], (unsigned long long)tcnt);
+        base = bcast64(base);
+        size_t pos = (size_t)tbase + base;
+        if (base + (unsigned long long)tcnt > tshard_cap) {
+            pos = (size_t)bcast64(trade_overflow(ttmp, ctr, tbase, tshard_cap, ttmp_cap, base, (uint32_t)tcnt));
+            if (pos == ~(size_t)0) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); tcnt = 0; return; }
+        }
+        if (lane < tcnt) {
+            KG int4* r = reinterpret_cast<KG int4*>(&ttmp[pos + lane]);
+            KG int2* r2 = reinterpret_cast<KG int2*>(&ttmp[pos + lane]);
+            r[0] = make_int4(t_oid0, t_oid1, t_aid0, t_aid1);
+            r[1] = make_int4(t_sid0, t_sid1, t_px, t_sz);
+            r2[4] = make_int2(t_seq, t_ord);
+        }
+        tcnt = 0;
+    }
+
+    // ---------------- tryMatch, KP:225-263 (FUNDED: sizes >= 0, prices 0..100)
+    // The loop test of KP:237 parses as ((size > 0 && isBuy) ? maker.price <= P : maker.price >= P)
+    // (H3).  A maker's price is the index of its level, so the test needs no node load; the level
+    // being swept stays in SGPRs and is written back once where the sweep stops; a level swept
+    // empty is not written at all (its bit is cleared).  The next maker's node is requested before
+    // the current trade's stores so that its wait does not include them (vmcnt is in order).
+    KDEV static bool crosses(bool is_buy, int32_t size, int32_t mprice, int32_t P) {
+        return (size > 0 && is_buy) ? mprice <= P : mprice >= P;
+    }
+    KDEV bool try_match(int32_t P, int32_t& tsize, bool is_buy, int os, uint32_t& ntr) {
+        uint64_t lo = bl(os), hi = bm(os);
+        int32_t pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+        if (pb == -1) return false;
+        if (!check_bit(lo, hi, pb)) { die(KME_E_DOMAIN, KME_D_NPE_BUCKET); return false; }
+        if (!crosses(is_buy, tsize, pb, P)) return tsize == 0;
+        int li = os * LVP + pb;
+        int32_t ms = U32(L.ht[li].x);
+        int64_t lqty = U64(L.qty[li]);
+        if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER); return false; }
+        KST(unsigned long long tw = stamp();)
+        Maker m = ld_maker(ms);
+        KST(acc[ST_MAKER_WAIT] += stamp() - tw; acc[ST_N_MAKER] += 1;)
+        bool head_moved = false;                             // ms is a later maker of level li
+        for (;;) {
+            const int32_t ts = imin(tsize, m.size);
+            const int32_t msize = jisub(m.size, ts);
+            tsize = jisub(tsize, ts);
+            lqty -= ts;
+            if (msize != 0) {                                // maker stays, partially filled (KP:255-261)
+                emit(ntr++, m, pb, ts);
+                pool[ms].size = msize;
+                if (head_moved) { L.ht[li].x = ms; pool[ms].prev = -1; }
+                mark_dirty(ms);
+                L.qty[li] = lqty;
+                return tsize == 0;
+            }
+            int32_t nms, npb = pb;                           // maker consumed: orders.delete (KP:243)
+            const bool same = m.next >= 0;
+            if (same) {
+                nms = m.next;
+                if (!crosses(is_buy, tsize, pb, P)) {        // stops before the next maker of the level
+                    emit(ntr++, m, pb, ts);
+                    free_slot(ms);
+                    L.ht[li].x = nms;
+                    pool[nms].prev = -1;
+                    mark_dirty(nms);
+                    L.qty[li] = lqty;
+                    return tsize == 0;
+                }
+            } else {                                         // level exhausted (KP:244-253)
+                unset_bit(lo, hi, pb);
+                set_bm(os, lo, hi);
+                npb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+                const bool go = npb != -1 && check_bit(lo, hi, npb) && crosses(is_buy, tsize, npb, P);
+                if (!go) {
+                    emit(ntr++, m, pb, ts);
+                    free_slot(ms);
+                    if (npb != -1 && !check_bit(lo, hi, npb)) die(KME_E_DOMAIN, KME_D_NPE_BUCKET);
+                    return tsize == 0;
+                }
+                li = os * LVP + npb;
+                nms = U32(L.ht[li].x);
+                lqty = U64(L.qty[li]);
+                if (nms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER); return false; }
+            }
+            KST(tw = stamp();)
+            const Maker nm = ld_maker(nms);                  // in flight during this trade's stores
+            emit(ntr++, m, pb, ts);
+            free_slot(ms);
+            KST(acc[ST_MAKER_WAIT] += stamp() - tw; acc[ST_N_MAKER] += 1;)
+            head_moved = same;
+            m = nm;
+            ms = nms;
+            pb = npb;
+        }
+    }
+
+    // ---------------- addOrder, KP:200-223 (after the book-exists and balance checks)
+    KDEV void rest(const Rec& r, int32_t tsize, Out& o) {
+        KST(unsigned long long ts0 = stamp();)
+        const int64_t key = jlmul(r.sid, r.action == BUY ? 1 : -1);
+        const int s = key < 0 ? 1 : 0;
+        uint64_t lo = bl(s), hi = bm(s);                     // books.get(sid) again (KP:205)
+        const int32_t p = r.price;                           // 0..100 (k_emap)
+        const int32_t slot = alloc_slot();
+        KST(unsigned long long ts1 = stamp(); acc[ST_REST_ALLOC] += ts1 - ts0;)
+        if (dead) return;
+        const int li = s * LVP + p;
+        int32_t nprev = -1;
+        int64_t poid = 0;
+        if (!check_bit(lo, hi, p)) {                        // new bucket (oid, oid), set bit (KP:209-211)
+            L.ht[li] = make_int2(slot, slot);
+            L.qty[li] = (int64_t)tsize;
+            L.toid[li] = r.oid;
+            set_bit(lo, hi, p);
+            set_bm(s, lo, hi);
+        } else {                                             // append at the tail (KP:213-219)
+            nprev = U32(L.ht[li].y);
+            poid = U64(L.toid[li]);
+            pool[nprev].next = slot;
+            mark_dirty(nprev);
+            L.ht[li].y = slot;
+            L.toid[li] = r.oid;
+            L.qty[li] = U64(L.qty[li]) + tsize;
+            o.has_prev = true;
+            o.prev = poid;
+        }
+        KST(unsigned long long ts2 = stamp(); acc[ST_REST_LEVEL] += ts2 - ts1;)
+        // the node: lane q < 4 stores 16-byte piece q (Node layout, kme_device.h).  Selected bit
+        // by bit: a compare chain on q becomes a switch whose default the compiler marks
+        // unreachable, a divergent loop exit that demotes the whole loop's state to VGPRs.
+        const bool q0 = (q & 1) != 0, q1 = (q & 2) != 0;
+        const int32_t x = q1 ? (q0 ? p : tsize) : (q0 ? lo32(r.sid) : lo32(r.oid));
+        const int32_t y = q1 ? (q0 ? r.action : -1) : (q0 ? hi32(r.sid) : hi32(r.oid));
+        const int32_t z = q1 ? (q0 ? 1 : nprev) : (q0 ? lo32(poid) : lo32(r.aid));
+        const int32_t w = q1 ? (q0 ? 0 : g) : (q0 ? hi32(poid) : hi32(r.aid));
+        if (lane < 4) reinterpret_cast<KG int4*>(&pool[slot])[lane] = make_int4(x, y, z, w);
+        mark_dirty(slot);
+        rest_slot[r.i] = slot;
+        o.rested = true;
+        KST(acc[ST_REST_NODE] += stamp() - ts2;)
+    }
+
+    // ---------------- removeOrder, KP:289-323
+    KDEV Victim ld_victim(int32_t s, int64_t oid, int64_t aid) const {
+        Victim o;
+        if (!is_dirty(s)) {
+            const v16i v = sload_node(&pool[s]);
+            const int32_t action = v[13];
+            o.ok = v[14] != 0 && mk64(v[0], v[1]) == oid && mk64(v[2], v[3]) == aid;
+            o.side = jlmul(mk64(v[4], v[5]), action == BUY ? 1 : -1) < 0 ? 1 : 0;
+            o.price = v[12];
+            o.size = v[8]; o.next = v[9]; o.prev = v[10];
+            o.prev_oid = mk64(v[6], v[7]);
+            return o;
+        }
+        const int4 v = reinterpret_cast<const KG int4*>(&pool[s])[q];
+        const int64_t noid = mk64(rl32(v.x, 0), rl32(v.y, 0)), naid = mk64(rl32(v.z, 0), rl32(v.w, 0));
+        const int64_t nsid = mk64(rl32(v.x, 1), rl32(v.y, 1));
+        const int32_t action = rl32(v.y, 3);
+        o.ok = rl32(v.z, 3) != 0 && noid == oid && naid == aid;
+        o.side = jlmul(nsid, action == BUY ? 1 : -1) < 0 ? 1 : 0;
+        o.price = rl32(v.x, 3);
+        o.size = rl32(v.x, 2); o.next = rl32(v.y, 2); o.prev = rl32(v.z, 2);
+        o.prev_oid = mk64(rl32(v.z, 1), rl32(v.w, 1));
+        return o;
+    }
+    KDEV bool cancel(const Rec& r, const Lanes& B) {
+        int32_t slot = -1;
+        if (r.tgt >= 0) slot = (int32_t)r.tgt;
+        else if (r.tgt <= -2) slot = U32(rest_slot[-(r.tgt + 2)]);
+        if (slot < 0) return false;                          // orders.get(oid) == null
+        Victim o;
+        if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
+            o.ok = rl32(B.pf_ok, r.lane);
+            const int32_t meta = rl32(B.pf_meta, r.lane);
+            o.price = meta & 0xFF; o.side = meta >> 8;
+            o.size = rl32(B.pf_size, r.lane); o.next = rl32(B.pf_next, r.lane); o.prev = rl32(B.pf_prev, r.lane);
+            o.prev_oid = rl64(B.pf_poid, r.lane);
+        } else {
+            KST(const unsigned long long tw = stamp();)
+            o = ld_victim(slot, r.oid, r.aid);
+            KST(acc[ST_VICTIM_WAIT] += stamp() - tw; acc[ST_N_VICTIM] += 1;)
+        }
+        if (!o.ok) return false;                             // missing, or order.aid != aid (KP:291)
+        if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK); return false; }
+        const int li = o.side * LVP + o.price;
+        if (o.prev < 0 && o.next < 0) {
+            uint64_t lo = bl(o.side), hi = bm(o.side);
+            unset_bit(lo, hi, o.price);
+            set_bm(o.side, lo, hi);
+        } else if (o.prev < 0) {
+            L.ht[li].x = o.next;
+            pool[o.next].prev = -1;
+            mark_dirty(o.next);
+        } else if (o.next < 0) {
+            L.ht[li].y = o.prev;
+            L.toid[li] = o.prev_oid;
+            pool[o.prev].next = -1;
+            mark_dirty(o.prev);
+        } else {
+            pool[o.prev].next = o.next;
+            pool[o.next].prev = o.prev;
+            pool[o.next].prev_oid = o.prev_oid;
+            mark_dirty(o.prev);
+            mark_dirty(o.next);
+        }
+        L.qty[li] = U64(L.qty[li]) - o.size;
+        free_slot(slot);
+        return !dead;
+    }
+
+    // ---------------- one record (MatchingEngine.process, KP:96-126)
+    KDEV Out process(const Rec& r, const Lanes& B) {
+        cur = r.i;
+        Out o;
+        o.action = r.action; o.size = r.size; o.prev = 0; o.has_prev = false; o.rested = false; o.ntr = 0;
+        bool ok = false;
+        switch (r.action) {
+        case ADD_SYMBOL:                                    // addSymbol, KP:184-191
+            if (!exists) { exists = 1; b0l = b0m = b1l = b1m = 0; ok = true; }
+            break;
+        case REMOVE_SYMBOL:
+        case PAYOUT:
+            if (exists) {                                   // removeSymbol, KP:193-198 / removeAllOrders KP:341-353
+                const int s = r.sid < 0 ? 1 : 0;
+                if (bl(s) != 0 || bm(s) != 0) { die(KME_E_DOMAIN, KME_D_HANG); return o; }
+            } else {
+                ok = r.action == REMOVE_SYMBOL;
+                if (r.action == PAYOUT) { die(KME_E_UNSUPPORTED, KME_D_NONE); return o; }
+            }
+            if (r.action == PAYOUT) ok = false;             // result ignored (KP:113-115)
+            break;
+        case BUY:
+        case SELL: {
+            if (!exists || !r.acct_ok) break;               // books.get(sid) == null / balances.get == null
+            const bool is_buy = r.action == BUY;
+            const int64_t key = jlmul(r.sid, is_buy ? 1 : -1);
+            const int os = jlneg(key) < 0 ? 1 : 0;          // opposite book (the same book for sid 0)
+            int32_t tsize = r.size;
+            uint32_t ntr = 0;
+            KST(unsigned long long tp0 = stamp();)
+            const bool filled = try_match(r.price, tsize, is_buy, os, ntr);
+            KST(unsigned long long tp1 = stamp(); if (ntr == 0) acc[ST_TM_PRE] += tp1 - tp0;)
+            o.ntr = ntr;
+            if (dead) return o;
+            if (!filled) { rest(r, tsize, o); if (dead) return o; }
+            ok = true;
+            o.size = tsize;
+            break;
+        }
+        case CANCEL:
+            ok = cancel(r, B);
+            if (dead) return o;
+            break;
+        default:
+            break;
+        }
+        o.action = ok ? r.action : (int32_t)REJECT;
+        return o;
+    }
+};
+
 // (2) FUNDED: one wavefront per symbol group, the group's records in arrival order.
 __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
-    __shared__ Level cache[2 * NLEV];
-    __shared__ int32_t fstack[FSTACK];
-    __shared__ uint32_t dirty[DIRTY_WORDS];
-    __shared__ Node nodepf[64];
+    __shared__ GroupLds lds;
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     const int32_t g = blockIdx.x;
@@ -1209,74 +1574,112 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e) return;
     if (failed(S.ctr)) return;
-    Core<false, true> c(S, io, cache, fstack, dirty, nodepf);
-    c.load_group(g);
-    const uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
+    KST(const unsigned long long tk0 = stamp();)
+    GroupWave w(S, lds, g);
+    w.load_group();
+    KST(w.acc[ST_GROUP_IN] += stamp() - tk0;)
+    const KG uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
+    const KG int64_t* ctgt = S.cancel_tgt;
+    const KG uint8_t* acct_ok = S.acct_ok;
+    const KG int32_t* rest_slot = S.rest_slot;
+    const KG Node* pool = S.pool;
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
-    KST(const unsigned long long tk0 = stamp();)
-    for (uint32_t k0 = b; k0 < e && !c.dead; k0 += 64) {
+    for (uint32_t k0 = b; k0 < e && !w.dead; k0 += 64) {
         KST(const unsigned long long tb0 = stamp();)
         const uint32_t k = k0 + lane;
         const bool valid = k < e;
-        const Batch B = load_batch(S, io, valid, valid ? perm[k] : 0, true);
-        // cancels of orders resting since an earlier epoch: fetch the target node with the batch
-        dirty[lane] = 0;
-        if (valid && B.action == CANCEL && B.tgt >= 0) {
-            const int4* src = reinterpret_cast<const int4*>(&S.pool[B.tgt]);
-            int4* dst = reinterpret_cast<int4*>(&nodepf[lane]);
-            const int4 x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];
-            dst[0] = x0; dst[1] = x1; dst[2] = x2; dst[3] = x3;
+        Lanes B;
+        B.i = valid ? perm[k] : 0;
+        if (valid) {
+            B.action = io.action[B.i]; B.price = io.price[B.i]; B.size = io.size[B.i];
+            B.oid = io.oid[B.i]; B.aid = io.aid[B.i]; B.sid = io.sid[B.i];
+            B.tgt = ctgt[B.i];
+            B.acct_ok = (int32_t)acct_ok[B.i];
+        } else {
+            B.action = -1; B.price = B.size = B.acct_ok = 0; B.oid = B.aid = B.sid = B.tgt = 0;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // The batch registers are read with readlane inside the record loop.  Waiting for them here
+        // cancels: the target node, if it came to rest before this batch (an earlier epoch, or an
+        // earlier batch of this group), is fetched now; valid unless written since (dirty filter)
+        const uint32_t i_first = (uint32_t)rl32((int32_t)B.i, 0);
+        B.pf_slot = -1;
+        if (valid && B.action == CANCEL) {
+            if (B.tgt >= 0) B.pf_slot = (int32_t)B.tgt;
+            else if (B.tgt <= -2 && (uint32_t)(-(B.tgt + 2)) < i_first) B.pf_slot = rest_slot[-(B.tgt + 2)];
+        }
+        B.pf_ok = 0; B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
+        if (B.pf_slot >= 0) {
+            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[B.pf_slot]);
+            const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
+            const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
+            B.pf_ok = c3.z != 0 && noid == B.oid && naid == B.aid;
+            B.pf_meta = c3.x | ((jlmul(nsid, c3.y == BUY ? 1 : -1) < 0 ? 1 : 0) << 8);
+            B.pf_poid = mk64(c1.z, c1.w);
+            B.pf_size = c2.x; B.pf_next = c2.y; B.pf_prev = c2.z;
+        }
+        lds.dirty[lane] = 0;
+        w.sync_lds();
+        // The lane registers are read with readlane inside the record loop.  Waiting for them here
         // once keeps the waitcnt pass from placing a vmcnt(0) at the loop header, which would make
         // every record wait for all stores of the record before it (stores share vmcnt on gfx9).
         __builtin_amdgcn_s_waitcnt(VMCNT0);
         const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
         // per-record OUT fields collect in lane j of these registers; one store per field per batch
         int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_flag = 0, o_ntr = 0;
-        KST(c.acc[0] += stamp() - tb0;)
+        KST(w.acc[ST_BATCH] += stamp() - tb0;)
 #pragma nounroll
-        for (int j = 0; j < nb && !c.dead; ++j) {
+        for (int j = 0; j < nb && !w.dead; ++j) {
             KST(const unsigned long long tr0 = stamp();)
-            const Rec rr = pick(B, j);
-            const Out o = c.process(rr, j);
-            KST(const unsigned long long tr1 = stamp();
-                const int cat = (rr.action == BUY || rr.action == SELL) ? 1 : (rr.action == CANCEL ? 2 : 3);
-                if (cat == 1) { c.acc[1] += tr1 - tr0; c.acc[8] += 1; }
-                else if (cat == 2) { c.acc[2] += tr1 - tr0; c.acc[9] += 1; }
-                else c.acc[3] += tr1 - tr0;)
-            o_act = lane_put(o.action, j, o_act);
-            o_size = lane_put(o.size, j, o_size);
-            o_plo = lane_put((int32_t)(uint32_t)o.prev, j, o_plo);
-            o_phi = lane_put((int32_t)(uint32_t)((uint64_t)o.prev >> 32), j, o_phi);
-            o_flag = lane_put((o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0) | (o.rested ? 2 : 0), j, o_flag);
-            o_ntr = lane_put((int32_t)o.ntr, j, o_ntr);
-            KST(c.acc[6] += stamp() - tr1;)
+            Rec r;
+            r.i = (uint32_t)rl32((int32_t)B.i, j);
+            r.action = rl32(B.action, j); r.price = rl32(B.price, j); r.size = rl32(B.size, j);
+            r.acct_ok = rl32(B.acct_ok, j);
+            r.oid = rl64(B.oid, j); r.aid = rl64(B.aid, j); r.sid = rl64(B.sid, j); r.tgt = rl64(B.tgt, j);
+            r.lane = j;
+            KST(w.acc[ST_REC_PICK] += stamp() - tr0;)
+            const Out o = w.process(r, B);
+#ifdef KME_STAMPS
+            {
+                const unsigned long long dt = stamp() - tr0;
+                const int cat = (r.action == BUY || r.action == SELL) ? (o.ntr ? 0 : 1) : (r.action == CANCEL ? 2 : 3);
+                w.acc[ST_TRADE_REC + cat] += dt;
+                if (cat < 3) w.acc[ST_N_TRADE_REC + cat] += 1;
+            }
+#endif
+            const bool me = lane == j;
+            o_act = me ? o.action : o_act;
+            o_size = me ? o.size : o_size;
+            o_plo = me ? lo32(o.prev) : o_plo;
+            o_phi = me ? hi32(o.prev) : o_phi;
+            o_flag = me ? ((o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0) | (o.rested ? 2 : 0)) : o_flag;
+            o_ntr = me ? (int32_t)o.ntr : o_ntr;
+            KST(w.acc[ST_REC_OUT] += stamp() - tr0;)
         }
         n_rest += (uint32_t)__popcll(__ballot(lane < nb && (o_flag & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < nb && B.action == CANCEL && o_act == CANCEL));
-        if (lane < nb && !c.dead) {
+        if (lane < nb && !w.dead) {
             const uint32_t i = B.i;
             io.out_action[i] = o_act;
             io.out_size[i] = o_size;
-            io.out_prev[i] = (int64_t)(((uint64_t)(uint32_t)o_phi << 32) | (uint32_t)o_plo);
+            io.out_prev[i] = mk64(o_plo, o_phi);
             io.out_flags[i] = (uint8_t)(o_flag & KME_OUT_HAS_PREV);
             io.n_trades[i] = (uint32_t)o_ntr;
         }
     }
-    c.close_trade_chunk();
-    c.store_group();
+    KST(const unsigned long long to0 = stamp();)
+    w.flush_trades();
+    KST(w.acc[ST_FLUSH] += stamp() - to0;)
+    w.store_group();
     if (lane == 0) {
-        if (n_rest) atomicAdd(&S.ctr[C_RESTS], (unsigned long long)n_rest);
-        if (n_cancel) atomicAdd(&S.ctr[C_CANCEL_OK], (unsigned long long)n_cancel);
+        if (n_rest) atomicAdd(&w.tsh[TS_RESTS], (unsigned long long)n_rest);
+        if (n_cancel) atomicAdd(&w.tsh[TS_CANCELS], (unsigned long long)n_cancel);
     }
 #ifdef KME_STAMPS
-    c.acc[7] = stamp() - tk0;
+    const unsigned long long tk1 = stamp();
+    w.acc[ST_GROUP_OUT] += tk1 - to0;
+    w.acc[ST_KERNEL] += tk1 - tk0;
     if (lane == 0)
-        for (int q = 0; q < 16; ++q) S.dbg[(size_t)g * 16 + q] = c.acc[q];
+        for (int q = 0; q < ST_N; ++q) S.dbg[(size_t)g * KME_DBG_WORDS + q] += w.acc[q];
 #endif
 }
 
@@ -1285,18 +1688,28 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     if (failed(S.ctr)) return;
-    Core<true, false> c(S, io, nullptr, nullptr, nullptr, nullptr);
+    Core c(S, io);
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
     for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
         const uint32_t k = k0 + lane;
         const bool valid = k < io.n;
-        const Batch B = load_batch(S, io, valid, valid ? k : 0, false);
-        const int32_t bgrp = valid ? S.route_grp[k] : -1;
+        // 64 records staged across the lanes, read with readlane (one gather per 64 records)
+        const uint32_t bi = valid ? k : 0;
+        const int32_t b_action = valid ? io.action[bi] : -1, b_price = valid ? io.price[bi] : 0;
+        const int32_t b_size = valid ? io.size[bi] : 0;
+        const int64_t b_oid = valid ? io.oid[bi] : 0, b_aid = valid ? io.aid[bi] : 0, b_sid = valid ? io.sid[bi] : 0;
+        const int64_t b_tgt = valid ? S.cancel_tgt[bi] : 0;
+        const int32_t bgrp = valid ? S.route_grp[bi] : -1;
         const int nb = (int)(io.n - k0 < 64 ? io.n - k0 : 64);
 #pragma nounroll
         for (int j = 0; j < nb && !c.dead; ++j) {
-            const Rec r = pick(B, j);
+            Rec r;
+            r.i = k0 + (uint32_t)j;
+            r.action = rl32(b_action, j); r.price = rl32(b_price, j); r.size = rl32(b_size, j);
+            r.acct_ok = 0;
+            r.oid = rl64(b_oid, j); r.aid = rl64(b_aid, j); r.sid = rl64(b_sid, j); r.tgt = rl64(b_tgt, j);
+            r.lane = j;
             const uint32_t i = r.i;
             const int32_t a = r.action;
             int32_t grp = -1;
@@ -1304,7 +1717,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
             else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) grp = group_of(r.sid, S.G);
             if (grp >= 0) {
                 if (grp != c.g) { c.store_group(); c.load_group(grp); }
-                const Out o = c.process(r, -1);
+                const Out o = c.process(r);
                 n_rest += o.rested;
                 n_cancel += a == CANCEL && o.action == CANCEL;
                 if (!c.dead && lane == 0) {
@@ -1333,25 +1746,48 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     c.store_group();
     if (lane_id() == 0) {
         io.trade_off[io.n] = c.tnext;
-        S.ctr[C_TRADES] = c.tnext;
-        S.ctr[C_RESTS] = n_rest;
-        S.ctr[C_CANCEL_OK] = n_cancel;
+        S.ctr[ci(C_TRADES)] = c.tnext;
+        S.ctr[ci(C_RESTS)] = n_rest;
+        S.ctr[ci(C_CANCEL_OK)] = n_cancel;
     }
 }
 
 // ------------------------------------------------------------------ (4) compaction
-__global__ void k_scatter(DevState S, EpochIO io, const uint32_t* total) {
-    const uint32_t cnt = (uint32_t)S.ctr[C_TTMP];
-    if (*total > io.trades_cap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, -1);
-        return;
+// Block s < TSHARDS moves shard s's trades, block TSHARDS the overflow region's, each to
+// trades[trade_off[seq] + ord] (arrival order); the shard blocks fold their rest / cancel counts
+// into the counters block and zero their line for the next epoch.
+__global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const uint32_t* total) {
+    const uint32_t s = blockIdx.x;
+    const bool fits = *total <= io.trades_cap;
+    if (s == 0 && threadIdx.x == 0) {
+        if (!fits) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, -1);
+        else S.ctr[ci(C_TRADES)] = *total;
     }
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
-        const TradeTmp r = S.ttmp[k];
-        if (r.seq < 0) continue;
-        io.trades[io.trade_off[r.seq] + (uint32_t)r.ord] = r.t;
+    size_t base;
+    uint32_t cnt;
+    if (s < TSHARDS) {
+        const unsigned long long used = S.tsh[(size_t)s * CTR_STRIDE + TS_USED];
+        base = (size_t)s * S.tshard_cap;
+        cnt = (uint32_t)(used < S.tshard_cap ? used : S.tshard_cap);
+    } else {
+        base = (size_t)TSHARDS * S.tshard_cap;
+        const unsigned long long used = S.ctr[ci(C_TTMP)];
+        cnt = (uint32_t)(used < S.ttmp_cap ? used : S.ttmp_cap);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) S.ctr[C_TRADES] = *total;
+    if (fits) {
+        for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+            const TradeTmp r = S.ttmp[base + k];
+            if (r.seq < 0) continue;
+            io.trades[io.trade_off[r.seq] + (uint32_t)r.ord] = r.t;
+        }
+    }
+    __syncthreads();
+    if (s < TSHARDS && threadIdx.x == 0) {
+        KG unsigned long long* line = S.tsh + (size_t)s * CTR_STRIDE;
+        if (line[TS_RESTS]) atomicAdd(&S.ctr[ci(C_RESTS)], line[TS_RESTS]);
+        if (line[TS_CANCELS]) atomicAdd(&S.ctr[ci(C_CANCEL_OK)], line[TS_CANCELS]);
+        line[TS_USED] = 0; line[TS_RESTS] = 0; line[TS_CANCELS] = 0;
+    }
 }
 
 // ------------------------------------------------------------------ oid-table maintenance
@@ -1372,7 +1808,7 @@ __global__ void k_table(DevState S, EpochIO io) {
         }
     }
     const unsigned long long b = __ballot(ins);
-    if (lane_id() == 0 && b) atomicAdd(&S.ctr[C_OTAB_USED], (unsigned long long)__popcll(b));
+    if (lane_id() == 0 && b) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)__popcll(b));
 }
 __global__ void k_otab_refill(DevState S, uint32_t nslots) {
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1384,7 +1820,7 @@ __global__ void k_otab_refill(DevState S, uint32_t nslots) {
             if (!ins) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
         }
         const unsigned long long b = __ballot(ins);
-        if (lane_id() == 0 && b) atomicAdd(&S.ctr[C_OTAB_USED], (unsigned long long)__popcll(b));
+        if (lane_id() == 0 && b) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)__popcll(b));
     }
 }
 
@@ -1477,7 +1913,7 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     uint32_t* total = bsum + nb + 1;
     launch_scan(io.n_trades, io.trade_off, io.n, bsum, total, st);
     (void)hipMemcpyAsync(io.trade_off + io.n, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(k_scatter, dim3(1024), dim3(256), 0, st, S, io, (const uint32_t*)total);
+    hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1), dim3(256), 0, st, S, io, (const uint32_t*)total);
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
@@ -1488,7 +1924,7 @@ void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st)
 }
 void launch_otab_rebuild(const DevState& S, hipStream_t st) {
     (void)hipMemsetAsync(S.otab_key, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);
-    (void)hipMemsetAsync(&S.ctr[C_OTAB_USED], 0, sizeof(unsigned long long), st);
+    (void)hipMemsetAsync(&S.ctr[ci(C_OTAB_USED)], 0, sizeof(unsigned long long), st);
     hipLaunchKernelGGL(k_otab_refill, dim3(2048), dim3(256), 0, st, S, S.pool_cap);
 }
 void launch_tob(const DevState& S, void* out, hipStream_t st) {

@@ -6,7 +6,6 @@
 namespace kme {
 
 constexpr int RADIX_TILE = 4096;     // inputs per partition tile (256 threads x 16)
-constexpr int TRADE_CHUNK = 64;      // trade-scratch records reserved per wavefront at a time
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
 
 // FUNDED pipeline

@@ -165,9 +165,14 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.otab_mask = (uint32_t)(e->otab_cap - 1);
     S.credit_div = cfg->credit_shards > 1 ? cfg->credit_shards : 1;
     S.trades_cap = cfg->max_trades;
-    const uint64_t ttmp_cap = funded ? (uint64_t)cfg->max_trades + (uint64_t)(G + 64) * TRADE_CHUNK : 1;
-    if (ttmp_cap >= (1ull << 32)) { kme_destroy(e); return KME_E_INVALID; }
-    S.ttmp_cap = (uint32_t)ttmp_cap;
+    // trade scratch: TSHARDS shard regions (2x the even share, so only skewed load spills) and an
+    // overflow region that alone holds an epoch's worth of trades
+    const uint64_t ttmp_ov = funded ? (uint64_t)cfg->max_trades + 64 : 1;
+    const uint64_t tshard_cap = funded ? std::max<uint64_t>(256, (2 * (uint64_t)cfg->max_trades + TSHARDS - 1) / TSHARDS) : 0;
+    const uint64_t ttmp_total = ttmp_ov + (uint64_t)TSHARDS * tshard_cap;
+    if (ttmp_total >= (1ull << 32)) { kme_destroy(e); return KME_E_INVALID; }
+    S.ttmp_cap = (uint32_t)ttmp_ov;
+    S.tshard_cap = (uint32_t)tshard_cap;
 
     ALLOC(S.grp, G);
     ALLOC(S.lev, (size_t)G * 2 * NLEV);
@@ -201,14 +206,15 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
         ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);
-        ALLOC(S.ttmp, ttmp_cap);
+        ALLOC(S.ttmp, ttmp_total);
+        ALLOC(S.tsh, (size_t)TSHARDS * CTR_STRIDE);
     }
     const uint64_t ntiles = (E + RADIX_TILE - 1) / RADIX_TILE;
     ALLOC(S.ghist, 256 * ntiles + 2 * (E / 2048 + 16) + 4096);
     ALLOC(S.seg, (size_t)G + 2);
-    ALLOC(S.ctr, C_NCTR);
-    ALLOC(S.dbg, (size_t)G * 16);
-    HIP_TRY(hipMemsetAsync(S.dbg, 0, (size_t)G * 16 * sizeof(unsigned long long), e->stream));
+    ALLOC(S.ctr, (size_t)C_NCTR * CTR_STRIDE);
+    ALLOC(S.dbg, (size_t)G * KME_DBG_WORDS);
+    HIP_TRY(hipMemsetAsync(S.dbg, 0, (size_t)G * KME_DBG_WORDS * sizeof(unsigned long long), e->stream));
     // epoch buffers
     ALLOC(e->d_action, E); ALLOC(e->d_price, E); ALLOC(e->d_size, E);
     ALLOC(e->d_oid, E); ALLOC(e->d_aid, E); ALLOC(e->d_sid, E);
@@ -217,14 +223,15 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(e->d_trades, cfg->max_trades);
     ALLOC(e->d_S, 1);
     ALLOC(e->d_io, 1);
-    HIP_TRY(hipHostMalloc((void**)&e->h_ctr, C_NCTR * sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&e->h_ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipHostMallocDefault));
 
     // initial store contents: every group absent, empty tables
     hipStream_t st = e->stream;
     HIP_TRY(hipMemsetAsync(S.otab_key, 0, e->otab_cap * sizeof(uint64_t), st));
     HIP_TRY(hipMemsetAsync(S.otab_val, 0xFF, e->otab_cap * sizeof(int32_t), st));
     HIP_TRY(hipMemsetAsync(S.pool, 0, P * sizeof(Node), st));
-    HIP_TRY(hipMemsetAsync(S.ctr, 0, C_NCTR * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(S.ctr, 0, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), st));
+    if (S.tsh) HIP_TRY(hipMemsetAsync(S.tsh, 0, (size_t)TSHARDS * CTR_STRIDE * sizeof(unsigned long long), st));
     if (funded) {
         HIP_TRY(hipMemsetAsync(S.acct_lb, 0, cfg->max_accounts * sizeof(int64_t), st));
         HIP_TRY(hipMemsetAsync(S.acct_need, 0, cfg->max_accounts * sizeof(int64_t), st));
@@ -293,9 +300,9 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     for (bool& u : e->ev_used) u = false;
 
     // per-epoch counters: error = none, stats = 0 (pool bump / table usage persist)
-    HIP_TRY(hipMemsetAsync(&S.ctr[C_ERR], 0xFF, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(&S.ctr[C_TRADES], 0, (C_TTMP - C_TRADES + 1) * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(&S.ctr[C_ACCT_OPS], 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ERR)], 0xFF, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_TRADES)], 0, (size_t)(ci(C_TTMP) - ci(C_TRADES) + 1) * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ACCT_OPS)], 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(S.emap_key, 0, emap_cap * sizeof(uint64_t), st));
 
     phase_begin(e, PH_EMAP);
@@ -329,7 +336,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     launch_table(S, io, st);
     phase_end(e, PH_TABLE);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->h_ctr, S.ctr, C_NCTR * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(e->h_ctr, S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     e->seq_base += n;
     e->last_n = n;
     e->pending = true;
@@ -355,15 +362,15 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     e->pending = false;
     const unsigned long long* c = e->h_ctr;
     s.n_inputs = e->last_n;
-    s.n_trades = (uint32_t)c[C_TRADES];
-    s.n_orders = c[C_ORDERS];
-    s.n_rests = c[C_RESTS];
-    s.n_maker_visits = c[C_TRADES];               // every maker visit is one trade (KP:238-242)
-    s.n_cancel_ok = c[C_CANCEL_OK];
-    if (c[C_ERR] != ~0ull) {
-        s.status = (int32_t)(c[C_ERR] & 0xFF);
-        s.detail = (int32_t)((c[C_ERR] >> 8) & 0xFF);
-        const uint64_t ix = c[C_ERR] >> 16;
+    s.n_trades = (uint32_t)c[ci(C_TRADES)];
+    s.n_orders = c[ci(C_ORDERS)];
+    s.n_rests = c[ci(C_RESTS)];
+    s.n_maker_visits = c[ci(C_TRADES)];               // every maker visit is one trade (KP:238-242)
+    s.n_cancel_ok = c[ci(C_CANCEL_OK)];
+    if (c[ci(C_ERR)] != ~0ull) {
+        s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
+        s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
+        const uint64_t ix = c[ci(C_ERR)] >> 16;
         s.error_index = ix == 0xFFFFFFFFFFFFull ? -1 : (int64_t)ix;
         e->failed = 1;
         e->fail_status = s.status;
@@ -376,12 +383,12 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
         }
     }
     // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild
-    if (!e->failed && c[C_OTAB_USED] * 2 > e->otab_cap) {
+    if (!e->failed && c[ci(C_OTAB_USED)] * 2 > e->otab_cap) {
         launch_otab_rebuild(e->S, e->stream);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, C_NCTR * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
-        if (e->h_ctr[C_ERR] != ~0ull || e->h_ctr[C_OTAB_USED] * 4 > e->otab_cap * 3) {
+        if (e->h_ctr[ci(C_ERR)] != ~0ull || e->h_ctr[ci(C_OTAB_USED)] * 4 > e->otab_cap * 3) {
             e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_OIDTAB;
         }
     }
@@ -391,7 +398,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
 
 kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n) {
     if (!e || !out) return KME_E_INVALID;
-    const size_t cap = (size_t)e->cfg.max_symbols * 16;
+    const size_t cap = (size_t)e->cfg.max_symbols * KME_DBG_WORDS;
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemcpy(out, e->S.dbg, std::min(n, cap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return KME_OK;
@@ -515,9 +522,9 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     const uint32_t G = e->cfg.max_symbols;
     std::vector<GroupState> grp(G);
     std::vector<Level> lev((size_t)G * 2 * NLEV);
-    unsigned long long ctr[C_NCTR];
+    unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    const uint64_t nslots = std::min<uint64_t>(ctr[C_POOL_BUMP], e->cfg.max_resting);
+    const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->cfg.max_resting);
     std::vector<Node> pool(nslots);
     HIP_TRY(hipMemcpy(grp.data(), e->S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(lev.data(), e->S.lev, lev.size() * sizeof(Level), hipMemcpyDeviceToHost));
@@ -545,7 +552,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
                     continue;
                 }
                 buckets.push_back({(int64_t)((uint64_t)key << 8) | p, pool[L.head].oid, pool[L.tail].oid});
-                // invariant walk: list links, count, quantity, tail oid
+                // invariant walk: list links, quantity, tail oid
                 int32_t s = L.head, prev = -1, cnt = 0;
                 int64_t qty = 0;
                 while (s >= 0 && (uint64_t)s < nslots && cnt <= (int32_t)nslots) {
@@ -561,7 +568,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
                     s = nd.next;
                 }
                 listed += cnt;
-                if (prev != L.tail || cnt != L.count || qty != L.qty || L.tail_oid != pool[L.tail].oid)
+                if (prev != L.tail || qty != L.qty || L.tail_oid != pool[L.tail].oid)
                     problems.push_back("X level bookkeeping mismatch at key " + std::to_string(key) + " price " + std::to_string(p));
             }
         }
