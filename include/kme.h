@@ -56,7 +56,7 @@ enum kme_domain {
     KME_D_PRICE = 7,         /* a resting price outside 0..126 aliases buckets across symbols (KP:379-416) */
     KME_D_DUP_OID = 8,       /* BUY/SELL reuses the oid of a live order (KP:221 would corrupt lists) */
     KME_D_FUNDED_RANGE = 9,  /* FUNDED mode: BUY/SELL price outside 0..100 or size < 0 */
-    KME_D_SENTINEL_OID = 10, /* oid equal to the reserved table sentinels (Long.MIN_VALUE, MIN_VALUE+1) */
+    KME_D_SENTINEL_OID = 10, /* reserved (no longer raised: the oid tables have no sentinel oids) */
     KME_D_CAP_POOL = 11, KME_D_CAP_OIDTAB = 12, KME_D_CAP_TRADES = 13, KME_D_CAP_SYMBOL = 14,
     KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17
 };

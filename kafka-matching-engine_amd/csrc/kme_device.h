@@ -9,8 +9,9 @@
 //   Level[G][2][128]     one per (book side, price level) = the Buckets store (KP:42-45): FIFO
 //                        head/tail node slots, resting quantity, tail oid.
 //   Node[P]              order-node pool = the Orders store (KP:46-49), one 64-byte line per order.
-//   oid table            open-addressing oid -> node slot (lazy deletion: entries are validated
-//                        against the node, stale ones are dropped at rebuild).
+//   oid table            open-addressing oid -> node slot, one packed u64 per entry (lazy
+//                        deletion: entries are validated against the node, stale ones are dropped
+//                        at rebuild).
 //   ledger               FUNDED: per-account existence + reservation bound; EXACT: Balances and
 //                        Positions as device hash tables (KP:30-37).
 #pragma once
@@ -93,7 +94,6 @@ constexpr int ci(int k) { return k * CTR_STRIDE; }
 constexpr int TSHARDS = 256;
 enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2 };
 
-constexpr uint64_t OID_SALT = 0x8000000000000000ull;   // stored key = oid ^ SALT, 0 = empty
 
 struct DevState {
     int32_t G, mode, A, passes;
@@ -102,8 +102,7 @@ struct DevState {
     KG GroupState* grp;
     KG Level* lev;
     KG Node* pool;
-    KG uint64_t* otab_key;
-    KG int32_t* otab_val;
+    KG uint64_t* otab;                // oid -> node slot, packed entries (kme_kernels.hip "oid tables")
     // FUNDED ledger
     KG int64_t* acct_since;
     KG int64_t* acct_lb;
@@ -117,8 +116,7 @@ struct DevState {
     KG uint32_t* pos_state;
     KG PosEntry* pos;
     // per-epoch scratch
-    KG uint64_t* emap_key;
-    KG int32_t* emap_val;
+    KG uint64_t* emap;                // oid -> input index of this epoch's BUY/SELL, packed entries
     KG int32_t* route_grp;
     KG int64_t* cancel_tgt;
     KG int32_t* rest_slot;

@@ -22,6 +22,8 @@
 // (values land in SGPRs); atomics are issued by lane 0 only and broadcast.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kme.h"
 #include "kme_device.h"
 #include "kme_launch.h"
@@ -176,68 +178,87 @@ KDEV int64_t wave_incl_scan_i64(int64_t v) {
 }
 
 // ------------------------------------------------------------------ oid tables
+// Both tables (oid -> resting node slot; oid -> input index of this epoch's BUY/SELL) are linear-
+// probing arrays of packed u64 entries ((fingerprint | 1) << 32 | value, 0 = empty): one 8-byte
+// word per probe, inserted with one CAS.  The fingerprint is a second hash of the oid; a match is
+// confirmed against the oid itself (the node's, or the epoch input's), so a fingerprint collision
+// costs a probe, never a wrong answer.  Stale node entries (lazy deletion) fail that check too.
+KDEV uint32_t oid_fp(int64_t oid) { return (uint32_t)(mix64((uint64_t)oid ^ 0x9e3779b97f4a7c15ull) >> 32) | 1u; }
+KDEV uint64_t hentry(uint32_t fp, uint32_t v) { return ((uint64_t)fp << 32) | v; }
+
 KDEV int32_t otab_lookup(const DevState& S, int64_t oid) {
-    const uint64_t key = (uint64_t)oid ^ OID_SALT;
+    const uint32_t fp = oid_fp(oid);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
     for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
-        uint64_t k = S.otab_key[h];
-        if (k == 0) return -1;
-        if (k == key) {
-            int32_t s = S.otab_val[h];
-            if (s >= 0 && S.pool[s].live && S.pool[s].oid == oid) return s;   // validate (lazy deletion)
+        const uint64_t e = S.otab[h];
+        if (e == 0) return -1;
+        if ((uint32_t)(e >> 32) == fp) {
+            const int32_t s = (int32_t)(uint32_t)e;
+            if (S.pool[s].live && S.pool[s].oid == oid) return s;
         }
         h = (h + 1) & S.otab_mask;
     }
     return -1;
 }
 KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
-    const unsigned long long key = (uint64_t)oid ^ OID_SALT;
+    const unsigned long long ent = hentry(oid_fp(oid), (uint32_t)slot);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
     for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
-        unsigned long long prev = atomicCAS((unsigned long long*)&S.otab_key[h], 0ull, key);
-        if (prev == 0) {
-            S.otab_val[h] = slot;
-            return true;
-        }
+        if (atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent) == 0) return true;
         h = (h + 1) & S.otab_mask;
     }
     return false;
 }
 KDEV int32_t emap_lookup(const DevState& S, const EpochIO& io, int64_t oid) {
-    const uint64_t key = (uint64_t)oid ^ OID_SALT;
+    const uint32_t fp = oid_fp(oid);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & io.emap_mask;
     for (uint32_t probes = 0; probes <= io.emap_mask; ++probes) {
-        uint64_t k = S.emap_key[h];
-        if (k == 0) return -1;
-        if (k == key) return S.emap_val[h];
+        const uint64_t e = S.emap[h];
+        if (e == 0) return -1;
+        if ((uint32_t)(e >> 32) == fp && io.oid[(uint32_t)e] == oid) return (int32_t)(uint32_t)e;
         h = (h + 1) & io.emap_mask;
     }
     return -1;
 }
 
 // ------------------------------------------------------------------ epoch kernels: emap / ledger / route
+// Sum of a per-thread count over a 256-thread block (DPP wave scans, then LDS); valid in thread 0.
+KDEV uint32_t block_sum_256(uint32_t v, uint32_t* red) {
+    const uint32_t w = wave_incl_scan_u32(v);
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    const uint32_t t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+// Grid of the streaming epoch kernels: enough 256-thread blocks to fill the chip several times,
+// each thread striding over the epoch; counters are summed per block and added once per block
+// (a counter hit by one atomic per wavefront serialises the whole kernel on its L2 line).
+constexpr uint32_t STREAM_BLOCKS = 2048;
+
 // BUY/SELL oid -> input index of this epoch; duplicate / sentinel oid checks; FUNDED: range domain
 // and per-account reservation need (max over adj of checkBalance's risk, KP:172-176).
-__global__ void k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *io_dev = io;   // the group / serial kernels read the epoch descriptor from HBM
-    bool is_order = false;
-    if (i < io.n) {
+__global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
+    __shared__ uint32_t red[4];
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 == 0) *io_dev = io;   // the group / serial kernels read the epoch descriptor from HBM
+    uint32_t n_orders = 0, n_acct = 0;
+    for (uint32_t i = t0; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
-        is_order = a == BUY || a == SELL || a == CANCEL;
+        n_orders += (a == BUY || a == SELL || a == CANCEL) ? 1u : 0u;
         if (a == BUY || a == SELL) {
             const int64_t oid = io.oid[i];
-            if (oid == INT64_MIN) {
-                raise_thread(S.ctr, KME_E_DOMAIN, KME_D_SENTINEL_OID, i);
-            } else {
-                const unsigned long long key = (uint64_t)oid ^ OID_SALT;
-                uint32_t h = (uint32_t)mix64((uint64_t)oid) & io.emap_mask;
-                for (uint32_t probes = 0; probes <= io.emap_mask; ++probes) {
-                    unsigned long long prev = atomicCAS((unsigned long long*)&S.emap_key[h], 0ull, key);
-                    if (prev == 0) { S.emap_val[h] = (int32_t)i; break; }
-                    if (prev == key) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i); break; }
-                    h = (h + 1) & io.emap_mask;
+            const uint32_t fp = oid_fp(oid);
+            const unsigned long long ent = hentry(fp, i);
+            uint32_t h = (uint32_t)mix64((uint64_t)oid) & io.emap_mask;
+            for (uint32_t probes = 0; probes <= io.emap_mask; ++probes) {
+                const unsigned long long prev = atomicCAS((unsigned long long*)&S.emap[h], 0ull, ent);
+                if (prev == 0) break;
+                if ((uint32_t)(prev >> 32) == fp && io.oid[(uint32_t)prev] == oid) {
+                    raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i > (uint32_t)prev ? i : (uint32_t)prev);
+                    break;
                 }
+                h = (h + 1) & io.emap_mask;
             }
             if (funded) {
                 const int32_t price = io.price[i], size = io.size[i];
@@ -252,11 +273,15 @@ __global__ void k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
                 }
             }
         } else if (funded && (a == CREATE_BALANCE || a == TRANSFER)) {
-            atomicAdd(&S.ctr[ci(C_ACCT_OPS)], 1ull);
+            ++n_acct;
         }
     }
-    const unsigned long long nb = __ballot(is_order);
-    if (lane_id() == 0 && nb) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)__popcll(nb));
+    const uint32_t no = block_sum_256(n_orders, red);
+    const uint32_t na = block_sum_256(n_acct, red);
+    if (threadIdx.x == 0) {
+        if (no) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)no);
+        if (na) atomicAdd(&S.ctr[ci(C_ACCT_OPS)], (unsigned long long)na);
+    }
 }
 
 KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int32_t size, bool has_prev, int64_t prev) {
@@ -1794,34 +1819,34 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
 // Orders that came to rest this epoch and are still live get an oid-table entry.  The used-slot
 // counter is bumped once per wavefront (a single hot counter would serialise every insert).
 // Oid-table entries for the orders of this epoch that are still resting.
-__global__ void k_table(DevState S, EpochIO io) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool ins = false;
-    if (i < io.n) {
+__global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io) {
+    __shared__ uint32_t red[4];
+    uint32_t n_ins = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t s = S.rest_slot[i];
         if (s >= 0) {
             const int64_t oid = io.oid[i];
             if (S.pool[s].live && S.pool[s].oid == oid) {
-                ins = otab_insert(S, oid, s);
-                if (!ins) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, i);
+                if (otab_insert(S, oid, s)) ++n_ins;
+                else raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, i);
             }
         }
     }
-    const unsigned long long b = __ballot(ins);
-    if (lane_id() == 0 && b) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)__popcll(b));
+    const uint32_t tot = block_sum_256(n_ins, red);
+    if (threadIdx.x == 0 && tot) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)tot);
 }
-__global__ void k_otab_refill(DevState S, uint32_t nslots) {
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const uint32_t lim = (nslots + stride - 1) / stride * stride;   // whole wavefronts for the ballot
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < lim; s += stride) {
-        bool ins = false;
-        if (s < nslots && S.pool[s].live) {
-            ins = otab_insert(S, S.pool[s].oid, (int32_t)s);
-            if (!ins) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
+// Rebuild: every live node of the pool's used prefix gets an entry.
+__global__ void __launch_bounds__(256) k_otab_refill(DevState S, uint32_t nslots) {
+    __shared__ uint32_t red[4];
+    uint32_t n_ins = 0;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x) {
+        if (S.pool[s].live) {
+            if (otab_insert(S, S.pool[s].oid, (int32_t)s)) ++n_ins;
+            else raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
         }
-        const unsigned long long b = __ballot(ins);
-        if (lane_id() == 0 && b) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)__popcll(b));
     }
+    const uint32_t tot = block_sum_256(n_ins, red);
+    if (threadIdx.x == 0 && tot) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)tot);
 }
 
 // ------------------------------------------------------------------ market data: top of book
@@ -1867,7 +1892,8 @@ __global__ void k_init_state(DevState S) {
 static inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st) {
-    hipLaunchKernelGGL(k_emap, dim3(cdiv(io.n > 0 ? io.n : 1, 256)), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);
+    const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
+    hipLaunchKernelGGL(k_emap, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);
 }
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_funded, dim3(1), dim3(64), 0, st, S, io);
@@ -1917,15 +1943,16 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
-    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_table, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);
 }
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev);
 }
-void launch_otab_rebuild(const DevState& S, hipStream_t st) {
-    (void)hipMemsetAsync(S.otab_key, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);
+void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
+    (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);
     (void)hipMemsetAsync(&S.ctr[ci(C_OTAB_USED)], 0, sizeof(unsigned long long), st);
-    hipLaunchKernelGGL(k_otab_refill, dim3(2048), dim3(256), 0, st, S, S.pool_cap);
+    const uint32_t n = std::min(used_slots, S.pool_cap);
+    hipLaunchKernelGGL(k_otab_refill, dim3(std::min<uint32_t>(cdiv(n > 0 ? n : 1, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, n);
 }
 void launch_tob(const DevState& S, void* out, hipStream_t st) {
     hipLaunchKernelGGL(k_tob, dim3(cdiv((uint32_t)S.G, 256)), dim3(256), 0, st, S, (kme_tob*)out);

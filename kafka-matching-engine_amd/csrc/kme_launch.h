@@ -21,7 +21,7 @@ void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
 // EXACT pipeline (emap + route shared)
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
 // maintenance
-void launch_otab_rebuild(const DevState& S, hipStream_t st);
+void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st);   // pool slots [0, used) hold every node
 void launch_tob(const DevState& S, void* out, hipStream_t st);
 void launch_init_state(const DevState& S, hipStream_t st);
 

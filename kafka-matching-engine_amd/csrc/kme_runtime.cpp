@@ -177,8 +177,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.grp, G);
     ALLOC(S.lev, (size_t)G * 2 * NLEV);
     ALLOC(S.pool, P);
-    ALLOC(S.otab_key, e->otab_cap);
-    ALLOC(S.otab_val, e->otab_cap);
+    ALLOC(S.otab, e->otab_cap);
     if (funded) {
         ALLOC(S.acct_since, cfg->max_accounts);
         ALLOC(S.acct_lb, cfg->max_accounts);
@@ -197,8 +196,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.pos, lc);
     }
     const uint64_t emap_cap = pow2_at_least(std::max<uint64_t>(2ull * E, 1024));
-    ALLOC(S.emap_key, emap_cap);
-    ALLOC(S.emap_val, emap_cap);
+    ALLOC(S.emap, emap_cap);
     ALLOC(S.route_grp, E);
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
@@ -227,8 +225,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
 
     // initial store contents: every group absent, empty tables
     hipStream_t st = e->stream;
-    HIP_TRY(hipMemsetAsync(S.otab_key, 0, e->otab_cap * sizeof(uint64_t), st));
-    HIP_TRY(hipMemsetAsync(S.otab_val, 0xFF, e->otab_cap * sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(S.otab, 0, e->otab_cap * sizeof(uint64_t), st));
     HIP_TRY(hipMemsetAsync(S.pool, 0, P * sizeof(Node), st));
     HIP_TRY(hipMemsetAsync(S.ctr, 0, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), st));
     if (S.tsh) HIP_TRY(hipMemsetAsync(S.tsh, 0, (size_t)TSHARDS * CTR_STRIDE * sizeof(unsigned long long), st));
@@ -303,7 +300,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ERR)], 0xFF, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_TRADES)], 0, (size_t)(ci(C_TTMP) - ci(C_TRADES) + 1) * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ACCT_OPS)], 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(S.emap_key, 0, emap_cap * sizeof(uint64_t), st));
+    HIP_TRY(hipMemsetAsync(S.emap, 0, emap_cap * sizeof(uint64_t), st));
 
     phase_begin(e, PH_EMAP);
     launch_emap(S, io, funded, e->d_io, st);
@@ -384,7 +381,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     }
     // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild
     if (!e->failed && c[ci(C_OTAB_USED)] * 2 > e->otab_cap) {
-        launch_otab_rebuild(e->S, e->stream);
+        launch_otab_rebuild(e->S, (uint32_t)std::min<uint64_t>(c[ci(C_POOL_BUMP)], e->S.pool_cap), e->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
