@@ -118,9 +118,11 @@ struct DevState {
     // per-epoch scratch
     KG uint64_t* emap;                // oid -> input index of this epoch's BUY/SELL, packed entries
     KG int32_t* route_grp;
-    KG int64_t* cancel_tgt;
+    KG int64_t* cancel_tgt;           // EXACT: cancel target (FUNDED: in the packed record)
     KG int32_t* rest_slot;
-    KG uint8_t* acct_ok;
+    KG int4* prec;                    // FUNDED: packed records, 32 B each (k_route -> k_match):
+                                      // w0 = action | price << 8 | acct_ok << 16 | (sid < 0) << 17,
+                                      // size, oid, aid, cancel target (slot | -(j + 2) | -1), 0
     KG uint32_t* rkeys[2];
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;

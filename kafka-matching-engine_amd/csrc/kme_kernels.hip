@@ -372,7 +372,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     int64_t tgt = -1;
     S.rest_slot[i] = -1;
     io.n_trades[i] = 0;
-    bool direct = false, ok = false;
+    bool direct = false, ok = false, acct_ok = false;
     switch (a) {
     case ADD_SYMBOL:
     case REMOVE_SYMBOL:
@@ -392,7 +392,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         if (otab_lookup(S, io.oid[i]) >= 0) raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i);
         if (funded && grp >= 0) {
             const int64_t aid = io.aid[i];
-            S.acct_ok[i] = (aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i) ? 1 : 0;
+            acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
         }
         break;
     }
@@ -417,8 +417,18 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         break;
     }
     S.route_grp[i] = grp;
-    S.cancel_tgt[i] = tgt;
-    if (funded && direct) write_out(io, i, a, ok, io.size[i], false, 0);
+    if (!funded) {
+        S.cancel_tgt[i] = tgt;
+        return;
+    }
+    if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
+    if (grp >= 0) {   // the record as k_match reads it (PRec)
+        const int64_t oid = io.oid[i], aid = io.aid[i];
+        const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
+        KG int4* p = &S.prec[2 * (size_t)i];
+        p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
+        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), (int32_t)tgt, 0);
+    }
 }
 
 // ------------------------------------------------------------------ (1) stable radix partition
@@ -1124,8 +1134,8 @@ struct Victim {
 // trips per record.
 struct Lanes {
     uint32_t i;
-    int32_t action, price, size, acct_ok;
-    int64_t oid, aid, sid, tgt;
+    int32_t w0, size, tgt;        // PRec word 0 (action | price << 8 | acct_ok << 16 | sid < 0 << 17)
+    int64_t oid, aid;
     int32_t pf_slot, pf_ok, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8
     int64_t pf_poid;
 };
@@ -1604,8 +1614,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     w.load_group();
     KST(w.acc[ST_GROUP_IN] += stamp() - tk0;)
     const KG uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
-    const KG int64_t* ctgt = S.cancel_tgt;
-    const KG uint8_t* acct_ok = S.acct_ok;
+    const KG int4* prec = S.prec;
     const KG int32_t* rest_slot = S.rest_slot;
     const KG Node* pool = S.pool;
     const int lane = lane_id();
@@ -1616,20 +1625,20 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         const bool valid = k < e;
         Lanes B;
         B.i = valid ? perm[k] : 0;
-        if (valid) {
-            B.action = io.action[B.i]; B.price = io.price[B.i]; B.size = io.size[B.i];
-            B.oid = io.oid[B.i]; B.aid = io.aid[B.i]; B.sid = io.sid[B.i];
-            B.tgt = ctgt[B.i];
-            B.acct_ok = (int32_t)acct_ok[B.i];
+        if (valid) {   // one 32-byte gather per record (PRec, written by k_route)
+            const int4 p0 = prec[2 * (size_t)B.i], p1 = prec[2 * (size_t)B.i + 1];
+            B.w0 = p0.x; B.size = p0.y;
+            B.oid = mk64(p0.z, p0.w); B.aid = mk64(p1.x, p1.y); B.tgt = p1.z;
         } else {
-            B.action = -1; B.price = B.size = B.acct_ok = 0; B.oid = B.aid = B.sid = B.tgt = 0;
+            B.w0 = 0xFF; B.size = 0; B.oid = B.aid = 0; B.tgt = -1;
         }
+        const int32_t b_action = B.w0 & 0xFF;
         // cancels: the target node, if it came to rest before this batch (an earlier epoch, or an
         // earlier batch of this group), is fetched now; valid unless written since (dirty filter)
         const uint32_t i_first = (uint32_t)rl32((int32_t)B.i, 0);
         B.pf_slot = -1;
-        if (valid && B.action == CANCEL) {
-            if (B.tgt >= 0) B.pf_slot = (int32_t)B.tgt;
+        if (valid && b_action == CANCEL) {
+            if (B.tgt >= 0) B.pf_slot = B.tgt;
             else if (B.tgt <= -2 && (uint32_t)(-(B.tgt + 2)) < i_first) B.pf_slot = rest_slot[-(B.tgt + 2)];
         }
         B.pf_ok = 0; B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
@@ -1657,9 +1666,13 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             KST(const unsigned long long tr0 = stamp();)
             Rec r;
             r.i = (uint32_t)rl32((int32_t)B.i, j);
-            r.action = rl32(B.action, j); r.price = rl32(B.price, j); r.size = rl32(B.size, j);
-            r.acct_ok = rl32(B.acct_ok, j);
-            r.oid = rl64(B.oid, j); r.aid = rl64(B.aid, j); r.sid = rl64(B.sid, j); r.tgt = rl64(B.tgt, j);
+            const int32_t w0 = rl32(B.w0, j);
+            r.action = w0 & 0xFF;
+            r.price = (w0 >> 8) & 0xFF;
+            r.acct_ok = (w0 >> 16) & 1;
+            r.sid = (w0 >> 17) & 1 ? -(int64_t)g : (int64_t)g;
+            r.size = rl32(B.size, j);
+            r.oid = rl64(B.oid, j); r.aid = rl64(B.aid, j); r.tgt = (int64_t)rl32(B.tgt, j);
             r.lane = j;
             KST(w.acc[ST_REC_PICK] += stamp() - tr0;)
             const Out o = w.process(r, B);
@@ -1681,7 +1694,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             KST(w.acc[ST_REC_OUT] += stamp() - tr0;)
         }
         n_rest += (uint32_t)__popcll(__ballot(lane < nb && (o_flag & 2)));
-        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && B.action == CANCEL && o_act == CANCEL));
+        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && b_action == CANCEL && o_act == CANCEL));
         if (lane < nb && !w.dead) {
             const uint32_t i = B.i;
             io.out_action[i] = o_act;

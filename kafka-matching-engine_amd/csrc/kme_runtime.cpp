@@ -200,7 +200,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.route_grp, E);
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
-    ALLOC(S.acct_ok, E);
+    if (funded) ALLOC(S.prec, 2 * (size_t)E);
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
         ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);
