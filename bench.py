@@ -6,11 +6,14 @@ proof, cancel routing, radix partition by symbol group, per-group matching, trad
 oid-table upkeep, top-of-book snapshot; + an RCCL all-gather of top-of-book when N > 1).
 Inputs are resident in HBM before the timed region; outputs stay in HBM.
 
-Workload at N = 1: BASELINE.json configs[1] -- 1,024 symbols x 16M synthetic limit/cancel orders,
-uniform load (SURVEY.md §8d "C2").  For N > 1 every rank runs its own C2-shaped shard of symbols
-(weak scaling: symbol groups are independent), no collective in the data path.
+Default workload: the metric's own configuration, C3 (BASELINE.json configs[2]):
+65,536 symbols symbol-sharded over the N ranks (65,536 / N symbols per GPU, so every N measures the
+same 65,536-symbol universe and N = 8 is exactly C3), 65,536 accounts, uniform limit / cancel
+orders; every rank processes its own stream, E = 2^22 records per epoch and step (per-GPU work per
+step is fixed: "weak" in records).  No collective in the data path; the top-of-book snapshot is
+all-gathered over RCCL per epoch.  --workload c2 runs configs[1] (1,024 symbols per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--epoch E] [--workload c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--epoch E] [--workload c3|c2|c4|c5]
 """
 from __future__ import annotations
 
@@ -47,14 +50,14 @@ def algorithmic_bytes(st) -> int:
             + 48 * st.n_cancel_ok)
 
 
-def make_workload(name: str, n_orders: int, rank: int, world: int):
+def make_workload(name: str, n_orders: int, rank: int, world: int, symbols: int = 0):
     seed = 1000 + rank
     if name == "c2":
         nsym, nacc = 1024, 4096
         stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
         desc = "C2: 1,024 symbols x 16M uniform limit/cancel orders per GPU (BASELINE configs[1])"
     elif name == "c3":
-        nsym, nacc = C3_SYMBOLS // world, C3_ACCOUNTS
+        nsym, nacc = (symbols or C3_SYMBOLS // world), C3_ACCOUNTS
         stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
         desc = (f"C3: 65,536 symbols symbol-sharded over {world} GPU(s) = {nsym:,} symbols per GPU, "
                 f"uniform limit/cancel orders (BASELINE configs[2])")
@@ -97,8 +100,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--epoch", type=int, default=1 << 20)
-    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--epoch", type=int, default=1 << 22)
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default 65,536 / N)")
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,7 +119,7 @@ def main():
 
     E = args.epoch
     total = max(args.orders, (args.warmup + args.steps) * E)
-    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world)
+    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world, args.symbols)
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
                              max_resting=min(total, 1 << 30), max_trades=2 * E + (1 << 16),

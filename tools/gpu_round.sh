@@ -1,19 +1,26 @@
 #!/bin/bash
-# One GPU round: parity tests, the bench line, and a rocprofv3 kernel-trace summary.
-# Usage (through gpurun): bash tools/gpu_round.sh <tag> [bench args...]
+# One full GPU round (through gpurun): parity tests, PMC traffic passes for k_match, the bench line
+# (with CPU baseline), a rocprofv3 kernel-trace/stats profile of the same command, extra bench
+# lines.  Usage: bash tools/gpu_round.sh <tag> [bench args...]
 set -o pipefail
-TAG=${1:-r}
+TAG=${1:-round}
 shift || true
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-rc=$?; echo "tests_rc=$rc"; tail -3 $OUT/gpu_tests.log
+rc=$?; echo "tests_rc=$rc"; tail -2 $OUT/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
+bash tools/pmc_kmatch.sh $TAG/pmc k_match "$@" || exit $?
+cp $OUT/pmc/pmc_summary.json profiles/pmc_k_match_c3.json
+timeout -k 10 500 python3 -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench_rc=$rc"; cat $OUT/bench.json; tail -2 $OUT/bench.err
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/prof.log 2>&1
 rc=$?; echo "prof_rc=$rc"
-f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -20 "$f"
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+for extra in "--workload c3 --symbols 8192" "--workload c2" "--workload c2 --epoch 1048576"; do
+  timeout -k 10 300 python3 -u bench.py --no-cpu-baseline $extra >> $OUT/bench_extra.jsonl 2>> $OUT/bench_extra.err
+  rc=$?; echo "extra [$extra] rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
