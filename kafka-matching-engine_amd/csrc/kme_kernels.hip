@@ -432,48 +432,55 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
 }
 
 // ------------------------------------------------------------------ (1) stable radix partition
-// LSD radix sort of (group, input index) pairs, 8-bit digits.  Records without a group sort into
-// bucket G, which nobody processes.  Stability = arrival order inside each group.
+// LSD radix sort of (group, input index) pairs, RADIX_BITS-bit digits (65,536 symbol groups: two
+// passes).  Records without a group sort into bucket G, which nobody processes.  Stability =
+// arrival order inside each group.
+constexpr int RADIX_DIGITS = 1 << RADIX_BITS;
+constexpr int RADIX_PER_T = RADIX_DIGITS / 256;   // digits per thread of a 256-thread block
+
+KDEV uint32_t radix_key(const DevState& S, int pass, int src, uint32_t k) {
+    if (pass == 0) { const int32_t g = S.route_grp[k]; return g < 0 ? (uint32_t)S.G : (uint32_t)g; }
+    return (src ? S.rkeys[1] : S.rkeys[0])[k];
+}
+
 __global__ void __launch_bounds__(256) k_radix_hist(DevState S, EpochIO io, int pass, int src) {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t h[RADIX_DIGITS];
     const int t = threadIdx.x;
-    h[t] = 0;
+    for (int q = 0; q < RADIX_PER_T; ++q) h[t + 256 * q] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * RADIX_TILE;
     for (int j = 0; j < RADIX_TILE / 256; ++j) {
         const uint32_t k = base + j * 256 + t;
-        if (k < io.n) {
-            uint32_t key;
-            if (pass == 0) { int32_t g = S.route_grp[k]; key = g < 0 ? (uint32_t)S.G : (uint32_t)g; }
-            else key = (src ? S.rkeys[1] : S.rkeys[0])[k];
-            atomicAdd(&h[(key >> (8 * pass)) & 255], 1u);
-        }
+        if (k < io.n) atomicAdd(&h[(radix_key(S, pass, src, k) >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1)], 1u);
     }
     __syncthreads();
-    S.ghist[t * gridDim.x + blockIdx.x] = h[t];
+    for (int q = 0; q < RADIX_PER_T; ++q) S.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
 }
 
 __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, int pass, int src) {
-    __shared__ uint32_t running[256];
-    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t running[RADIX_DIGITS];
+    __shared__ uint32_t wcnt[4][RADIX_DIGITS];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    running[t] = S.ghist[t * gridDim.x + blockIdx.x];
+    for (int q = 0; q < RADIX_PER_T; ++q) running[t + 256 * q] = S.ghist[(t + 256 * q) * gridDim.x + blockIdx.x];
     const uint32_t base = blockIdx.x * RADIX_TILE;
     const int dst = src ^ 1;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     for (int j = 0; j < RADIX_TILE / 256; ++j) {
-        wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+        for (int q = 0; q < RADIX_PER_T; ++q) {
+            wcnt[0][t + 256 * q] = 0; wcnt[1][t + 256 * q] = 0; wcnt[2][t + 256 * q] = 0; wcnt[3][t + 256 * q] = 0;
+        }
         __syncthreads();
         const uint32_t k = base + j * 256 + t;
         const bool valid = k < io.n;
         uint32_t key = 0, val = 0;
         if (valid) {
-            if (pass == 0) { int32_t g = S.route_grp[k]; key = g < 0 ? (uint32_t)S.G : (uint32_t)g; val = k; }
-            else { key = (src ? S.rkeys[1] : S.rkeys[0])[k]; val = (src ? S.rvals[1] : S.rvals[0])[k]; }
+            key = radix_key(S, pass, src, k);
+            val = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
         }
-        const uint32_t d = (key >> (8 * pass)) & 255;
+        const uint32_t d = (key >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1);
+        // lanes of this wavefront with the same digit (match-any over the digit bits)
         unsigned long long peers = __ballot(valid);
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < RADIX_BITS; ++b) {
             const unsigned long long bb = __ballot(valid && ((d >> b) & 1));
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
@@ -487,7 +494,10 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
             (dst ? S.rvals[1] : S.rvals[0])[pos] = val;
         }
         __syncthreads();
-        running[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+        for (int q = 0; q < RADIX_PER_T; ++q) {
+            const int dd = t + 256 * q;
+            running[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
+        }
         __syncthreads();
     }
 }
@@ -1102,6 +1112,10 @@ KDEV int64_t U64(int64_t v) { return (int64_t)bcast64((uint64_t)v); }
 KDEV int64_t mk64(int32_t lo, int32_t hi) { return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo); }
 KDEV int32_t lo32(int64_t v) { return (int32_t)(uint32_t)(uint64_t)v; }
 KDEV int32_t hi32(int64_t v) { return (int32_t)(uint32_t)((uint64_t)v >> 32); }
+// Side of book key sid * (BUY ? 1 : -1) (KP:201, 292): 1 when the key is negative.  For the
+// records and nodes of a symbol group sid is +-g with g < 2^24, so this is a sign test (no 64-bit
+// multiply); sid 0 is the shared book of side 0 (H4).
+KDEV int book_side(int64_t sid, bool is_buy) { return (sid != 0 && ((hi32(sid) < 0) != !is_buy)) ? 1 : 0; }
 
 // Overflow path of GroupWave::flush_trades: marks this reservation's share of the shard region
 // as holes and reserves n records in the overflow region; ~0 when that is full too.
@@ -1436,8 +1450,7 @@ struct GroupWave {
     // ---------------- addOrder, KP:200-223 (after the book-exists and balance checks)
     KDEV void rest(const Rec& r, int32_t tsize, Out& o) {
         KST(unsigned long long ts0 = stamp();)
-        const int64_t key = jlmul(r.sid, r.action == BUY ? 1 : -1);
-        const int s = key < 0 ? 1 : 0;
+        const int s = book_side(r.sid, r.action == BUY);
         uint64_t lo = bl(s), hi = bm(s);                     // books.get(sid) again (KP:205)
         const int32_t p = r.price;                           // 0..100 (k_emap)
         const int32_t slot = alloc_slot();
@@ -1486,7 +1499,7 @@ struct GroupWave {
             const v16i v = sload_node(&pool[s]);
             const int32_t action = v[13];
             o.ok = v[14] != 0 && mk64(v[0], v[1]) == oid && mk64(v[2], v[3]) == aid;
-            o.side = jlmul(mk64(v[4], v[5]), action == BUY ? 1 : -1) < 0 ? 1 : 0;
+            o.side = book_side(mk64(v[4], v[5]), action == BUY);
             o.price = v[12];
             o.size = v[8]; o.next = v[9]; o.prev = v[10];
             o.prev_oid = mk64(v[6], v[7]);
@@ -1497,7 +1510,7 @@ struct GroupWave {
         const int64_t nsid = mk64(rl32(v.x, 1), rl32(v.y, 1));
         const int32_t action = rl32(v.y, 3);
         o.ok = rl32(v.z, 3) != 0 && noid == oid && naid == aid;
-        o.side = jlmul(nsid, action == BUY ? 1 : -1) < 0 ? 1 : 0;
+        o.side = book_side(nsid, action == BUY);
         o.price = rl32(v.x, 3);
         o.size = rl32(v.x, 2); o.next = rl32(v.y, 2); o.prev = rl32(v.z, 2);
         o.prev_oid = mk64(rl32(v.z, 1), rl32(v.w, 1));
@@ -1573,8 +1586,7 @@ struct GroupWave {
         case SELL: {
             if (!exists || !r.acct_ok) break;               // books.get(sid) == null / balances.get == null
             const bool is_buy = r.action == BUY;
-            const int64_t key = jlmul(r.sid, is_buy ? 1 : -1);
-            const int os = jlneg(key) < 0 ? 1 : 0;          // opposite book (the same book for sid 0)
+            const int os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
             int32_t tsize = r.size;
             uint32_t ntr = 0;
             KST(unsigned long long tp0 = stamp();)
@@ -1647,7 +1659,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
             const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
             B.pf_ok = c3.z != 0 && noid == B.oid && naid == B.aid;
-            B.pf_meta = c3.x | ((jlmul(nsid, c3.y == BUY ? 1 : -1) < 0 ? 1 : 0) << 8);
+            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8);
             B.pf_poid = mk64(c1.z, c1.w);
             B.pf_size = c2.x; B.pf_next = c2.y; B.pf_prev = c2.z;
         }
@@ -1791,16 +1803,17 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
 }
 
 // ------------------------------------------------------------------ (4) compaction
-// Block s < TSHARDS moves shard s's trades, block TSHARDS the overflow region's, each to
-// trades[trade_off[seq] + ord] (arrival order); the shard blocks fold their rest / cancel counts
-// into the counters block and zero their line for the next epoch.
+// Blocks (s, *) with s < TSHARDS move shard s's trades, blocks (TSHARDS, *) the overflow
+// region's, each to trades[trade_off[seq] + ord] (arrival order).
+constexpr uint32_t SCATTER_SUB = 8;   // blocks per shard region
 __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const uint32_t* total) {
     const uint32_t s = blockIdx.x;
     const bool fits = *total <= io.trades_cap;
-    if (s == 0 && threadIdx.x == 0) {
+    if (s == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (!fits) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, -1);
         else S.ctr[ci(C_TRADES)] = *total;
     }
+    if (!fits) return;
     size_t base;
     uint32_t cnt;
     if (s < TSHARDS) {
@@ -1812,19 +1825,22 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
         const unsigned long long used = S.ctr[ci(C_TTMP)];
         cnt = (uint32_t)(used < S.ttmp_cap ? used : S.ttmp_cap);
     }
-    if (fits) {
-        for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
-            const TradeTmp r = S.ttmp[base + k];
-            if (r.seq < 0) continue;
-            io.trades[io.trade_off[r.seq] + (uint32_t)r.ord] = r.t;
-        }
+    for (uint32_t k = blockIdx.y * blockDim.x + threadIdx.x; k < cnt; k += gridDim.y * blockDim.x) {
+        const TradeTmp r = S.ttmp[base + k];
+        if (r.seq < 0) continue;
+        io.trades[io.trade_off[r.seq] + (uint32_t)r.ord] = r.t;
     }
-    __syncthreads();
-    if (s < TSHARDS && threadIdx.x == 0) {
-        KG unsigned long long* line = S.tsh + (size_t)s * CTR_STRIDE;
-        if (line[TS_RESTS]) atomicAdd(&S.ctr[ci(C_RESTS)], line[TS_RESTS]);
-        if (line[TS_CANCELS]) atomicAdd(&S.ctr[ci(C_CANCEL_OK)], line[TS_CANCELS]);
-        line[TS_USED] = 0; line[TS_RESTS] = 0; line[TS_CANCELS] = 0;
+}
+// The shard lines' rest / cancel counts into the counters block; the lines zeroed for the next epoch.
+__global__ void __launch_bounds__(256) k_tsh_fold(DevState S) {
+    __shared__ uint32_t red[4];
+    KG unsigned long long* line = S.tsh + (size_t)threadIdx.x * CTR_STRIDE;   // TSHARDS == 256 threads
+    const unsigned long long rests = line[TS_RESTS], cancels = line[TS_CANCELS];
+    line[TS_USED] = 0; line[TS_RESTS] = 0; line[TS_CANCELS] = 0;
+    const uint32_t r = block_sum_256((uint32_t)rests, red), c = block_sum_256((uint32_t)cancels, red);
+    if (threadIdx.x == 0) {
+        if (r) atomicAdd(&S.ctr[ci(C_RESTS)], (unsigned long long)r);
+        if (c) atomicAdd(&S.ctr[ci(C_CANCEL_OK)], (unsigned long long)c);
     }
 }
 
@@ -1931,7 +1947,7 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     for (int pass = 0; pass < S.passes; ++pass) {
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(256), 0, st, S, io, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
-        const uint32_t L = 256 * ntiles;
+        const uint32_t L = RADIX_DIGITS * ntiles;
         uint32_t* bsum = S.ghist + L;
         uint32_t* total = bsum + cdiv(L, SCAN_BLOCK) + 1;
         launch_scan(S.ghist, S.ghist, L, bsum, total, st);
@@ -1952,7 +1968,9 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     uint32_t* total = bsum + nb + 1;
     launch_scan(io.n_trades, io.trade_off, io.n, bsum, total, st);
     (void)hipMemcpyAsync(io.trade_off + io.n, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1), dim3(256), 0, st, S, io, (const uint32_t*)total);
+    hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1, SCATTER_SUB), dim3(256), 0, st, S, io, (const uint32_t*)total);
+    static_assert(TSHARDS == 256, "k_tsh_fold: one thread per shard line");
+    hipLaunchKernelGGL(k_tsh_fold, dim3(1), dim3(256), 0, st, S);
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;

@@ -158,7 +158,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     {
         int bits = 0;
         while ((1ull << bits) <= (uint64_t)G) ++bits;   // keys 0..G
-        S.passes = (bits + 7) / 8;
+        S.passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
     }
     S.pool_cap = (uint32_t)P;
     e->otab_cap = pow2_at_least(std::max<uint64_t>(2 * P, 1024));
@@ -208,7 +208,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.tsh, (size_t)TSHARDS * CTR_STRIDE);
     }
     const uint64_t ntiles = (E + RADIX_TILE - 1) / RADIX_TILE;
-    ALLOC(S.ghist, 256 * ntiles + 2 * (E / 2048 + 16) + 4096);
+    ALLOC(S.ghist, (size_t)(1 << RADIX_BITS) * ntiles + 2 * (E / 2048 + 16) + 4096);
     ALLOC(S.seg, (size_t)G + 2);
     ALLOC(S.ctr, (size_t)C_NCTR * CTR_STRIDE);
     ALLOC(S.dbg, (size_t)G * KME_DBG_WORDS);
