@@ -1392,6 +1392,34 @@ struct GroupWave {
         KST(unsigned long long tw = stamp();)
         Maker m = ld_maker(ms);
         KST(acc[ST_MAKER_WAIT] += stamp() - tw; acc[ST_N_MAKER] += 1;)
+        // (3) Sweep scan.  When the best level cannot absorb the taker, lane l takes the l-th level
+        // after it in sweep order (ascending asks for a BUY, descending bids for a SELL) and a DPP
+        // prefix scan over their resting quantity finds every level the sweep reaches (the
+        // quantity before it is at most the taker's size).  Those levels' head makers are fetched
+        // now, one lane each, so moving to the next level costs a readlane instead of a dependent
+        // load.  Only levels the sweep itself has not touched are prefetched, and nothing writes
+        // them before the sweep gets there, so the copies are exact; the loop below still applies
+        // KP:237-253 maker by maker.
+        const int32_t pb0 = pb;
+        uint64_t pfmask = 0;
+        int32_t pf_slot = -1, pf_oid0 = 0, pf_oid1 = 0, pf_aid0 = 0, pf_aid1 = 0, pf_sid0 = 0, pf_sid1 = 0, pf_size = 0,
+                pf_next = 0;
+        if ((int64_t)tsize > lqty) {
+            const int p = is_buy ? pb + 1 + lane : pb - 1 - lane;
+            const bool occ = p >= 0 && p <= 100 && check_bit(lo, hi, p) && (is_buy ? p <= P : p >= P);
+            const int lp = os * LVP + (occ ? p : 0);
+            const int64_t q = occ ? L.qty[lp] : 0;
+            const int64_t before = lqty + wave_incl_scan_i64(q) - q;
+            const bool reach = occ && before <= (int64_t)tsize;
+            pfmask = __ballot(reach);
+            // (no branch around the loads: lanes that do not reach a level read the best level's
+            // head, a valid node; a divergent branch here would demote the loop state to VGPRs)
+            pf_slot = reach ? L.ht[lp].x : ms;
+            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[pf_slot]);
+            const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2];
+            pf_oid0 = c0.x; pf_oid1 = c0.y; pf_aid0 = c0.z; pf_aid1 = c0.w;
+            pf_sid0 = c1.x; pf_sid1 = c1.y; pf_size = c2.x; pf_next = c2.y;
+        }
         bool head_moved = false;                             // ms is a later maker of level li
         for (;;) {
             const int32_t ts = imin(tsize, m.size);
@@ -1436,7 +1464,15 @@ struct GroupWave {
                 if (nms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER); return false; }
             }
             KST(tw = stamp();)
-            const Maker nm = ld_maker(nms);                  // in flight during this trade's stores
+            Maker nm;
+            const int l = is_buy ? npb - pb0 - 1 : pb0 - 1 - npb;
+            if (!same && l >= 0 && l < 64 && ((pfmask >> l) & 1) && rl32(pf_slot, l) == nms) {   // swept level
+                nm.oid = mk64(rl32(pf_oid0, l), rl32(pf_oid1, l)); nm.aid = mk64(rl32(pf_aid0, l), rl32(pf_aid1, l));
+                nm.sid = mk64(rl32(pf_sid0, l), rl32(pf_sid1, l));
+                nm.size = rl32(pf_size, l); nm.next = rl32(pf_next, l);
+            } else {
+                nm = ld_maker(nms);                          // in flight during this trade's stores
+            }
             emit(ntr++, m, pb, ts);
             free_slot(ms);
             KST(acc[ST_MAKER_WAIT] += stamp() - tw; acc[ST_N_MAKER] += 1;)
