@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
+    ap.add_argument("--serialize", action="store_true",
+                    help="also print each epoch's MatchOut tape on the GPU (kme_tape_json_device) inside the step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,12 +145,18 @@ def main():
     def epoch_ptrs(k):
         return {name: t.data_ptr() + k * E * t.element_size() for name, t in cols.items()}
 
+    tape_buf = torch.empty(args.serialize * (512 * E + (1 << 20)), dtype=torch.uint8, device=dev)
+    tape_bytes = []
+
     def run_epoch(k):
         eng.submit_device(epoch_ptrs(k), E)
         eng.top_of_book(tob.data_ptr())
         if world > 1:
             dist.all_gather_into_tensor(tob_all, tob)  # market-data snapshot over RCCL / xGMI
-        return eng.wait()
+        st = eng.wait()
+        if args.serialize:  # MatchOut text of the epoch, printed on the GPU, left in HBM
+            tape_bytes.append(eng.tape_json_device_into(epoch_ptrs(k), E, tape_buf.data_ptr(), tape_buf.numel()))
+        return st
 
     for k in range(args.warmup):
         run_epoch(k)
@@ -245,6 +253,9 @@ def main():
                          "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",
                          "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg))},
         }
+        if args.serialize:
+            out["serialize"] = {"tape_bytes_per_epoch": float(np.mean(tape_bytes[-args.steps:])),
+                                "note": "step includes kme_tape_json_device (MatchOut text in HBM)"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(setup, stream, args.cpu_sample)
         print(json.dumps(out), flush=True)

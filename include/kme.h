@@ -189,6 +189,14 @@ kme_status kme_enable_timing(kme_engine* e, int enable);
 kme_status kme_tape_json(const kme_orders* in, uint32_t n, const kme_epoch_result* res,
                          char* buf, size_t cap, size_t* len);
 
+/* The same text produced on the GPU (SURVEY §8 row f next-1): `in_dev` = the epoch's device
+ * inputs, `res_dev` = its device results (NULL: the engine-owned results of the last
+ * kme_submit_epoch_device), `out_dev` = a device buffer of `cap` bytes.  Stream-ordered on the
+ * engine stream and synchronous; *len = the full length.  Nothing is written when *len > cap
+ * (call again with a bigger buffer); KME_E_CAPACITY when one epoch's text would exceed 4 GiB. */
+kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,
+                                void* out_dev, size_t cap, size_t* len);
+
 /* Jackson JsonDeserializer<Order> (KP:513-520) for one record: numbers or numeric strings,
  * unknown properties rejected, next/prev must be absent or null. */
 kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, int64_t* oid,

@@ -1971,7 +1971,7 @@ void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t
     if (io.n == 0) return;
     hipLaunchKernelGGL(k_route, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io, funded ? 1 : 0);
 }
-static void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, uint32_t* total, hipStream_t st) {
+void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, uint32_t* total, hipStream_t st) {
     const uint32_t nb = cdiv(L > 0 ? L : 1, SCAN_BLOCK);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, in, out, L, bsum);
     hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, bsum, nb, total);

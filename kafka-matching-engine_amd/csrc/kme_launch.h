@@ -1,6 +1,7 @@
 // kme_launch.h -- host-side launchers of the epoch kernels (kme_kernels.hip), used by the runtime.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "kme.h"
 #include "kme_device.h"
 
 namespace kme {
@@ -21,6 +22,14 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
 // EXACT pipeline (emap + route shared)
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
+// exclusive scan of L u32 values (DPP wave scans): out[k] = sum(in[0..k)); bsum needs
+// L / 2048 + 1 words of scratch, *total receives the sum
+void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, uint32_t* total, hipStream_t st);
+// device serializer (kme_serialize.hip)
+void launch_ser_len(const kme_orders& in, const kme_epoch_result& r, uint32_t n, uint32_t* len, unsigned long long* total,
+                    hipStream_t st);
+void launch_ser_write(const kme_orders& in, const kme_epoch_result& r, uint32_t n, const uint32_t* off, void* out,
+                      hipStream_t st);
 // maintenance
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st);   // pool slots [0, used) hold every node
 void launch_tob(const DevState& S, void* out, hipStream_t st);

@@ -51,6 +51,10 @@ struct kme_engine {
     uint32_t *d_ntrades = nullptr, *d_trade_off = nullptr;
     TradeRec* d_trades = nullptr;
     unsigned long long* h_ctr = nullptr;  // pinned copy of the counters block
+    // device serializer scratch: per-input byte counts, offsets, scan partials, u64 total
+    uint32_t *d_ser_len = nullptr, *d_ser_off = nullptr, *d_ser_tmp = nullptr;
+    unsigned long long* d_ser_total = nullptr;
+    unsigned long long* h_ser_total = nullptr;
     std::vector<void*> allocs;
     int64_t seq_base = 0;
     uint32_t last_n = 0;
@@ -219,8 +223,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(e->d_out_action, E); ALLOC(e->d_out_size, E); ALLOC(e->d_out_prev, E);
     ALLOC(e->d_out_flags, E); ALLOC(e->d_ntrades, E); ALLOC(e->d_trade_off, (size_t)E + 1);
     ALLOC(e->d_trades, cfg->max_trades);
+    ALLOC(e->d_ser_len, E); ALLOC(e->d_ser_off, (size_t)E + 1); ALLOC(e->d_ser_tmp, (size_t)E / 2048 + 64);
+    ALLOC(e->d_ser_total, 1);
     ALLOC(e->d_S, 1);
     ALLOC(e->d_io, 1);
+    HIP_TRY(hipHostMalloc((void**)&e->h_ser_total, sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&e->h_ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipHostMallocDefault));
 
     // initial store contents: every group absent, empty tables
@@ -253,6 +260,7 @@ kme_status kme_destroy(kme_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+    if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
     for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -391,6 +399,29 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     }
     if (st) *st = s;
     return (kme_status)s.status;
+}
+
+kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,
+                                void* out_dev, size_t cap, size_t* len) {
+    if (!e || !in_dev || !len) return KME_E_INVALID;
+    if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
+    HIP_TRY(hipSetDevice(e->device));
+    kme_epoch_result r{};
+    if (res_dev) r = *res_dev; else kme_device_results(e, &r);
+    hipStream_t st = e->stream;
+    launch_ser_len(*in_dev, r, n, e->d_ser_len, e->d_ser_total, st);
+    HIP_TRY(hipMemcpyAsync(e->h_ser_total, e->d_ser_total, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t total = *e->h_ser_total;
+    *len = (size_t)total;
+    if (total >= (1ull << 32)) return KME_E_CAPACITY;
+    if (total > cap || n == 0) return KME_OK;
+    if (!out_dev) return KME_E_INVALID;
+    launch_scan(e->d_ser_len, e->d_ser_off, n, e->d_ser_tmp, e->d_ser_off + n, st);
+    launch_ser_write(*in_dev, r, n, e->d_ser_off, out_dev, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return KME_OK;
 }
 
 kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n) {

@@ -65,7 +65,7 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
+    "kme_tape_json_device", "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
 ]
@@ -107,6 +107,8 @@ def lib():
         "kme_enable_timing": (st, [vp, C.c_int]),
         "kme_tape_json": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                C.POINTER(C.c_size_t)]),
+        "kme_tape_json_device": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]),
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
         "kme_shard_of": (u32, [i64, u32]),
@@ -285,7 +287,35 @@ class Engine:
         rc = self._L.kme_debug_counters(self._h, C.c_void_p(out.ctypes.data), out.size)
         if rc:
             raise KmeError(rc, "kme_debug_counters")
-        return out.reshape(-1, 16)
+        return out.reshape(-1, 32)
+
+    def tape_json_device_into(self, ptrs: dict, n: int, out_ptr: int, cap: int) -> int:
+        """kme_tape_json_device into a caller device buffer; returns the text length (nothing is
+        written when it exceeds cap)."""
+        s = kme_orders(*[C.c_void_p(int(ptrs[k])) for k in ("action", "oid", "aid", "sid", "price", "size")])
+        got = C.c_size_t(0)
+        rc = self._L.kme_tape_json_device(self._h, C.byref(s), n, None, C.c_void_p(int(out_ptr)), cap, C.byref(got))
+        if rc:
+            raise KmeError(rc, "kme_tape_json_device")
+        return got.value
+
+    def tape_json_device(self, ptrs: dict, n: int) -> bytes:
+        """kme_tape_json_device over the last device epoch (inputs at `ptrs`, engine-owned results):
+        the MatchOut tape printed by the GPU, copied back to the host."""
+        import torch
+
+        s = kme_orders(*[C.c_void_p(int(ptrs[k])) for k in ("action", "oid", "aid", "sid", "price", "size")])
+        need = C.c_size_t(0)
+        rc = self._L.kme_tape_json_device(self._h, C.byref(s), n, None, None, 0, C.byref(need))
+        if rc:
+            raise KmeError(rc, "kme_tape_json_device")
+        buf = torch.empty(max(1, need.value), dtype=torch.uint8, device=f"cuda:{int(self.cfg.device)}")
+        got = C.c_size_t(0)
+        rc = self._L.kme_tape_json_device(self._h, C.byref(s), n, None, C.c_void_p(buf.data_ptr()), buf.numel(),
+                                          C.byref(got))
+        if rc:
+            raise KmeError(rc, "kme_tape_json_device")
+        return buf[: got.value].cpu().numpy().tobytes()
 
     def snapshot_books(self) -> str:
         return self._text(self._L.kme_snapshot_books)

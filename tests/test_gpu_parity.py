@@ -179,3 +179,41 @@ def test_top_of_book(kme_mod, oracle_mod):
         msb, lsb = books[-g]
         bits = [p for p in range(127) if ((lsb >> p) & 1 if p < 63 else (msb >> (p - 63)) & 1)]
         assert tob[g, 1] == (min(bits) if bits else -1)
+
+
+def _device_cols(orders):
+    import torch
+
+    cols = {k: torch.from_numpy(np.ascontiguousarray(getattr(orders, k))).cuda()
+            for k in ("action", "oid", "aid", "sid", "price", "size")}
+    return cols, {k: t.data_ptr() for k, t in cols.items()}
+
+
+@pytest.mark.parametrize("mode", ["funded", "exact"])
+def test_device_serializer_matches_oracle_tape(kme_mod, oracle_mod, mode):
+    """kme_tape_json_device (SURVEY §8 f next-1): the GPU prints each epoch's MatchOut records
+    byte-identically to the reference's Jackson + consumer.js format."""
+    if mode == "funded":
+        n_sym = 48
+        setup = W.funded_setup(256, range(1, n_sym + 1))
+        stream = W.uniform(30_000, n_symbols=n_sym, n_accounts=256, seed=21)
+        eng = _funded_engine(kme_mod, n_sym + 1, accounts=256)
+    else:
+        orders = W.exchange_test(12_000, seed=5)
+        setup, stream = orders.slice(0, 40), orders.slice(40, len(orders))
+        eng = _exact_engine(kme_mod, E=1 << 14, P=1 << 16)
+    o = oracle_mod.Oracle()
+    o.process(setup)
+    eng.process(setup)
+    o.clear_tape()
+    epoch = 7_001
+    for a in range(0, len(stream), epoch):
+        part = stream.slice(a, min(len(stream), a + epoch))
+        cols, ptrs = _device_cols(part)
+        eng.submit_device(ptrs, len(part))
+        eng.wait()
+        got = eng.tape_json_device(ptrs, len(part)).decode()
+        o.process(part)
+        want = o.tape_text()
+        o.clear_tape()
+        assert got == want, _first_diff(got, want)
