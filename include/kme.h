@@ -159,6 +159,17 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st);
 /* Engine-owned device result buffers of the last device epoch. */
 kme_status kme_device_results(kme_engine* e, kme_epoch_result* out_dev);
 
+/* Persistence (SURVEY §8 row f next-3; the reference keeps its state in RocksDB stores with
+ * changelogs, KP:30-49, and commits after every record, KP:125).  kme_checkpoint writes the
+ * engine's whole device state -- books, buckets, resting orders, oid table, the FUNDED reservation
+ * ledger or the EXACT Balances/Positions, and the input sequence number -- to a file, between
+ * epochs (call it after the epoch whose input offsets are being committed).  kme_restore loads
+ * such a file into a freshly created engine of the same configuration; processing then resumes with
+ * the records after the committed offset and produces exactly the tape an uninterrupted engine
+ * would.  KME_E_INVALID on a config / format mismatch, KME_E_FAILED if the engine has failed. */
+kme_status kme_checkpoint(kme_engine* e, const char* path);
+kme_status kme_restore(kme_engine* e, const char* path);
+
 /* Canonical text snapshots (sorted), identical in format to the reference stores' contents:
  *   books : "B <key> <msb> <lsb>" (Books), "K <bucketPtr> <firstOid> <lastOid>" (Buckets),
  *           "O <oid> <action> <aid> <sid> <price> <size> <next|null> <prev|null>" (Orders)

@@ -401,6 +401,108 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     return (kme_status)s.status;
 }
 
+// ------------------------------------------------------------------ persistence
+namespace {
+constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '1'};
+struct CkptHeader {
+    char magic[8];
+    kme_config cfg;
+    int64_t seq_base;
+    uint64_t pool_used, otab_used, bal_used, pos_used;
+};
+struct Blob { void* dev; size_t bytes; };
+
+std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
+    const DevState& S = e->S;
+    const size_t G = e->cfg.max_symbols;
+    std::vector<Blob> b = {
+        {S.grp, G * sizeof(GroupState)},
+        {S.lev, G * 2 * NLEV * sizeof(Level)},
+        {S.pool, pool_used * sizeof(Node)},
+        {S.otab, e->otab_cap * sizeof(uint64_t)},
+    };
+    if (e->cfg.mode == KME_MODE_FUNDED) {
+        b.push_back({S.acct_since, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
+        b.push_back({S.acct_lb, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
+    } else {
+        const size_t lc = (size_t)S.bal_mask + 1;
+        b.push_back({S.bal_state, lc * sizeof(uint32_t)});
+        b.push_back({S.bal_key, lc * sizeof(int64_t)});
+        b.push_back({S.bal_val, lc * sizeof(int64_t)});
+        b.push_back({S.pos_state, lc * sizeof(uint32_t)});
+        b.push_back({S.pos, lc * sizeof(PosEntry)});
+    }
+    return b;
+}
+}  // namespace
+
+kme_status kme_checkpoint(kme_engine* e, const char* path) {
+    if (!e || !path) return KME_E_INVALID;
+    if (e->failed) return KME_E_FAILED;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long ctr[C_NCTR * CTR_STRIDE];
+    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    CkptHeader h{};
+    std::memcpy(h.magic, kCkptMagic, sizeof h.magic);
+    h.cfg = e->cfg;
+    h.seq_base = e->seq_base;
+    h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->cfg.max_resting);
+    h.otab_used = ctr[ci(C_OTAB_USED)];
+    h.bal_used = ctr[ci(C_BAL_USED)];
+    h.pos_used = ctr[ci(C_POS_USED)];
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return KME_E_INVALID;
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
+    std::vector<char> host;
+    for (const Blob& b : state_blobs(e, h.pool_used)) {
+        if (!ok) break;
+        host.resize(b.bytes);
+        if (b.bytes && hipMemcpy(host.data(), b.dev, b.bytes, hipMemcpyDeviceToHost) != hipSuccess) { ok = false; break; }
+        const uint64_t n = b.bytes;
+        ok = std::fwrite(&n, sizeof n, 1, f) == 1 && (n == 0 || std::fwrite(host.data(), 1, n, f) == n);
+    }
+    ok = std::fclose(f) == 0 && ok;
+    return ok ? KME_OK : KME_E_INVALID;
+}
+
+kme_status kme_restore(kme_engine* e, const char* path) {
+    if (!e || !path) return KME_E_INVALID;
+    if (e->failed) return KME_E_FAILED;
+    HIP_TRY(hipSetDevice(e->device));
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return KME_E_INVALID;
+    CkptHeader h{};
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, sizeof h.magic) == 0;
+    // the same store geometry (device, stream and timing choices may differ)
+    ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
+         h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
+         h.cfg.max_resting == e->cfg.max_resting && h.cfg.ledger_capacity == e->cfg.ledger_capacity &&
+         h.cfg.credit_shards == e->cfg.credit_shards && h.pool_used <= e->cfg.max_resting;
+    std::vector<char> host;
+    for (const Blob& b : ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{}) {
+        uint64_t n = 0;
+        ok = std::fread(&n, sizeof n, 1, f) == 1 && n == b.bytes;
+        if (!ok) break;
+        host.resize(n);
+        ok = n == 0 || std::fread(host.data(), 1, n, f) == n;
+        if (!ok) break;
+        HIP_TRY(hipMemcpyAsync(b.dev, host.data(), n, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));   // host buffer is reused
+    }
+    std::fclose(f);
+    if (!ok) return KME_E_INVALID;
+    unsigned long long ctr[C_NCTR * CTR_STRIDE];
+    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    ctr[ci(C_POOL_BUMP)] = h.pool_used;
+    ctr[ci(C_OTAB_USED)] = h.otab_used;
+    ctr[ci(C_BAL_USED)] = h.bal_used;
+    ctr[ci(C_POS_USED)] = h.pos_used;
+    HIP_TRY(hipMemcpy(e->S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
+    e->seq_base = h.seq_base;
+    return KME_OK;
+}
+
 kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,
                                 void* out_dev, size_t cap, size_t* len) {
     if (!e || !in_dev || !len) return KME_E_INVALID;

@@ -65,7 +65,7 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_tape_json_device", "kme_order_from_json", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
+    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
 ]
@@ -109,6 +109,8 @@ def lib():
                                C.POINTER(C.c_size_t)]),
         "kme_tape_json_device": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                       C.POINTER(C.c_size_t)]),
+        "kme_checkpoint": (st, [vp, C.c_char_p]),
+        "kme_restore": (st, [vp, C.c_char_p]),
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
         "kme_shard_of": (u32, [i64, u32]),
@@ -288,6 +290,16 @@ class Engine:
         if rc:
             raise KmeError(rc, "kme_debug_counters")
         return out.reshape(-1, 32)
+
+    def checkpoint(self, path: str):
+        rc = self._L.kme_checkpoint(self._h, str(path).encode())
+        if rc:
+            raise KmeError(rc, "kme_checkpoint")
+
+    def restore(self, path: str):
+        rc = self._L.kme_restore(self._h, str(path).encode())
+        if rc:
+            raise KmeError(rc, "kme_restore")
 
     def tape_json_device_into(self, ptrs: dict, n: int, out_ptr: int, cap: int) -> int:
         """kme_tape_json_device into a caller device buffer; returns the text length (nothing is

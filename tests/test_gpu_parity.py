@@ -217,3 +217,37 @@ def test_device_serializer_matches_oracle_tape(kme_mod, oracle_mod, mode):
         want = o.tape_text()
         o.clear_tape()
         assert got == want, _first_diff(got, want)
+
+
+@pytest.mark.parametrize("mode", ["funded", "exact"])
+def test_checkpoint_restore_resumes_exactly(kme_mod, oracle_mod, mode, tmp_path):
+    """Row f next-3: a checkpoint taken after an epoch, restored into a fresh engine, continues the
+    stream with the tape, books (and EXACT ledger) of an uninterrupted run."""
+    if mode == "funded":
+        n_sym = 40
+        setup = W.funded_setup(300, range(1, n_sym + 1))
+        stream = W.uniform(24_000, n_symbols=n_sym, n_accounts=300, seed=31)
+        allin = W.Orders.concat([setup, stream])
+        make = lambda: _funded_engine(kme_mod, n_sym + 1, accounts=300)
+    else:
+        allin = W.exchange_test(16_000, seed=9)
+        make = lambda: _exact_engine(kme_mod, E=1 << 14, P=1 << 16)
+    cut = len(allin) // 2
+    first, second = allin.slice(0, cut), allin.slice(cut, len(allin))
+    a = make()
+    _run_epochs(a, first, 4096)
+    ck = tmp_path / "engine.ckpt"
+    a.checkpoint(ck)
+    want_rest = _run_epochs(a, second, 4096)
+    b = make()
+    b.restore(ck)
+    got_rest = _run_epochs(b, second, 4096)
+    assert got_rest == want_rest, _first_diff(got_rest, want_rest)
+    o = oracle_mod.Oracle()
+    o.process(first)
+    o.clear_tape()
+    o.process(second)
+    assert got_rest == o.tape_text(), _first_diff(got_rest, o.tape_text())
+    assert b.snapshot_books() == o.dump_books()
+    if mode == "exact":
+        assert b.snapshot_ledger() == o.dump_ledger()
