@@ -116,3 +116,68 @@ def _sort_dump(lines):
         p = l.split()
         return (order.get(p[0], 3), int(p[1]) if len(p) > 1 and p[1].lstrip("-").isdigit() else 0, l)
     return sorted(lines, key=key)
+
+
+# ----------------------------------------------------------------------------- partitioned topics
+class PartitionRouter:
+    """MatchIn / MatchOut partitioned by symbol group (SURVEY.md §8 row f "next-4").
+
+    The reference produces every record to partition 0 of MatchIn (exchange_test.js:14-16,
+    topic.js:17-18).  Here each input record is answered by exactly ONE engine, so engine k's output
+    is MatchOut partition k as it stands -- no host merge of the N streams:
+
+    * BUY/SELL/ADD_SYMBOL/REMOVE_SYMBOL/PAYOUT -> ``shard_of(|sid|, n)`` (Kafka's keyed partitioner);
+    * CANCEL -> the partition that received the last BUY/SELL carrying that oid (a host
+      oid -> partition directory); an oid never seen goes to partition 0, which rejects
+      it exactly as the reference does (``orders.get(oid) == null``, KP:290);
+    * CREATE_BALANCE/TRANSFER -> every partition (each engine proves its orders against 1/n of the
+      credit, ``kme_config.credit_shards``), echoed by partition 0 only;
+    * any other action -> partition 0.
+
+    Within a partition records keep arrival order; across partitions only per-symbol order is
+    defined, as with any keyed Kafka topic.  FUNDED mode only (the EXACT ledger couples symbols).
+    """
+
+    def __init__(self, n: int):
+        self.n = n
+        self.directory: dict[int, int] = {}
+        self.seq = 0
+
+    def route(self, orders: Orders):
+        """-> (parts, echo, seqs): per partition the Orders it processes, a bool mask of the records
+        whose MatchOut chunk belongs in that partition, and their input sequence numbers."""
+        sym_route = route(orders, self.n)
+        dest = np.zeros(len(orders), np.int64)
+        a = orders.action
+        for i in range(len(orders)):
+            ai = int(a[i])
+            if ai in (BUY, SELL):
+                dest[i] = sym_route[i]
+                self.directory[int(orders.oid[i])] = int(dest[i])
+            elif ai == CANCEL:
+                dest[i] = self.directory.get(int(orders.oid[i]), 0)
+            elif ai in (CREATE_BALANCE, TRANSFER):
+                dest[i] = BROADCAST
+            elif ai in (ADD_SYMBOL, REMOVE_SYMBOL, PAYOUT):
+                dest[i] = sym_route[i]
+            else:
+                dest[i] = 0
+        seq = np.arange(len(orders), dtype=np.int64) + self.seq
+        self.seq += len(orders)
+        parts, echo, seqs = [], [], []
+        for k in range(self.n):
+            idx = np.flatnonzero((dest == k) | (dest == BROADCAST))
+            parts.append(Orders(orders.action[idx], orders.oid[idx], orders.aid[idx], orders.sid[idx],
+                                orders.price[idx], orders.size[idx],
+                                None if orders.oid_is_string is None else orders.oid_is_string[idx]))
+            echo.append((dest[idx] == k) | ((dest[idx] == BROADCAST) & (k == 0)))
+            seqs.append(seq[idx])
+        return parts, echo, seqs
+
+
+def partition_tape(tape: str, echo: np.ndarray) -> str:
+    """MatchOut partition text: the engine's tape without the chunks of records it processed only
+    for their side effects (account records echoed by partition 0)."""
+    chunks = _chunks(tape)
+    assert len(chunks) == len(echo), (len(chunks), len(echo))
+    return "".join(c for c, e in zip(chunks, echo.tolist()) if e)
