@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 1
+#define KME_ABI_VERSION 2
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -72,6 +72,16 @@ enum kme_domain {
  *         the reservation bound only (exact balances/positions: EXACT mode). */
 enum kme_mode { KME_MODE_EXACT = 0, KME_MODE_FUNDED = 1 };
 
+/* kme_config.flags
+ * KME_FLAG_EXACT_LEDGER (FUNDED, SURVEY §8 row f next-2): after the parallel matching of each
+ *   epoch, one wavefront replays the epoch's ledger effects in arrival order -- createBalance /
+ *   transfer (KP:131-146), checkBalance's reservation and position adjustment (KP:167-182), both
+ *   fillOrder calls per trade (KP:276-287) and postRemoveAdjustments (KP:325-333), with the
+ *   value-keyed position writes of KP:434-436 -- into device Balances / Positions tables, so the
+ *   final ledger stores are bit-exact too (kme_snapshot_ledger).  The replay is a serial chain:
+ *   it costs far more than the matching it follows. */
+#define KME_FLAG_EXACT_LEDGER 1u
+
 typedef struct kme_config {
     uint32_t abi_version;      /* KME_ABI_VERSION */
     uint32_t mode;             /* kme_mode */
@@ -86,6 +96,8 @@ typedef struct kme_config {
                                   (0 or 1 = one engine).  Each shard proves its own orders against
                                   floor(credit / n) and ceil(debit / n), so the shards' reservations
                                   together never exceed the account's cash. */
+    uint32_t flags;            /* KME_FLAG_* */
+    uint32_t _reserved;
 } kme_config;
 
 /* One epoch of input records, structure-of-arrays (Order fields KP:451-456).  The reference's
@@ -174,7 +186,7 @@ kme_status kme_restore(kme_engine* e, const char* path);
  *   books : "B <key> <msb> <lsb>" (Books), "K <bucketPtr> <firstOid> <lastOid>" (Buckets),
  *           "O <oid> <action> <aid> <sid> <price> <size> <next|null> <prev|null>" (Orders)
  *   ledger: "A <aid> <balance>" (Balances), "P <keyMsb> <keyLsb> <amount> <available>" (Positions);
- *           EXACT mode only (FUNDED: KME_E_UNSUPPORTED).
+ *           EXACT mode, or FUNDED with KME_FLAG_EXACT_LEDGER (otherwise KME_E_UNSUPPORTED).
  * *text is malloc'd; free with kme_free. */
 kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len);
 kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len);

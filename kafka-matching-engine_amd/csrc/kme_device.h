@@ -97,6 +97,7 @@ enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2 };
 
 struct DevState {
     int32_t G, mode, A, passes;
+    int32_t ledger_replay, _pad0[3];  // FUNDED + KME_FLAG_EXACT_LEDGER
     uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
     uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
     KG GroupState* grp;
@@ -120,6 +121,8 @@ struct DevState {
     KG int32_t* route_grp;
     KG int64_t* cancel_tgt;           // EXACT: cancel target (FUNDED: in the packed record)
     KG int32_t* rest_slot;
+    KG int4* vic;                     // FUNDED + exact ledger: per accepted cancel, the removed order
+                                      // (price | action << 8, size, sid) for postRemoveAdjustments
     KG int4* prec;                    // FUNDED: packed records, 32 B each (k_route -> k_match):
                                       // w0 = action | price << 8 | acct_ok << 16 | (sid < 0) << 17,
                                       // size, oid, aid, cancel target (slot | -(j + 2) | -1), 0

@@ -1140,6 +1140,7 @@ struct Maker {
 struct Victim {
     int32_t ok;                   // live, same oid and same aid (KP:290-291)
     int32_t side, price, size, next, prev;
+    int32_t sell, sid_neg;        // the order's action (BUY / SELL) and sid sign (sid = +-g)
     int64_t prev_oid;
 };
 
@@ -1150,7 +1151,7 @@ struct Lanes {
     uint32_t i;
     int32_t w0, size, tgt;        // PRec word 0 (action | price << 8 | acct_ok << 16 | sid < 0 << 17)
     int64_t oid, aid;
-    int32_t pf_slot, pf_ok, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8
+    int32_t pf_slot, pf_ok, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10
     int64_t pf_poid;
 };
 
@@ -1170,6 +1171,8 @@ struct GroupWave {
     KG unsigned long long* ctr;
     KG unsigned long long* tsh;       // this group's trade shard line
     KG int32_t* rest_slot;
+    KG int4* vic;
+    int32_t ledger_replay;
     uint32_t pool_cap, ttmp_cap, tshard_cap, tbase;   // tbase: first record of the shard region
     GroupLds& L;
     const int lane, q;            // q = lane & 3: the node piece this lane loads / stores
@@ -1186,7 +1189,8 @@ struct GroupWave {
 
     KDEV GroupWave(const DevState& S, GroupLds& lds, int32_t gg)
         : pool(S.pool), lev(S.lev + (size_t)gg * 2 * NLEV), gst(S.grp + gg), ttmp(S.ttmp), ctr(S.ctr),
-          tsh(S.tsh + (size_t)(gg & (TSHARDS - 1)) * CTR_STRIDE), rest_slot(S.rest_slot), pool_cap(S.pool_cap),
+          tsh(S.tsh + (size_t)(gg & (TSHARDS - 1)) * CTR_STRIDE), rest_slot(S.rest_slot), vic(S.vic),
+          ledger_replay(S.ledger_replay), pool_cap(S.pool_cap),
           ttmp_cap(S.ttmp_cap), tshard_cap(S.tshard_cap), tbase((uint32_t)(gg & (TSHARDS - 1)) * S.tshard_cap), L(lds),
           lane(lane_id()),
           q(lane_id() & 3), g(gg) {
@@ -1536,6 +1540,7 @@ struct GroupWave {
             const int32_t action = v[13];
             o.ok = v[14] != 0 && mk64(v[0], v[1]) == oid && mk64(v[2], v[3]) == aid;
             o.side = book_side(mk64(v[4], v[5]), action == BUY);
+            o.sell = action == SELL; o.sid_neg = v[5] < 0;
             o.price = v[12];
             o.size = v[8]; o.next = v[9]; o.prev = v[10];
             o.prev_oid = mk64(v[6], v[7]);
@@ -1547,6 +1552,7 @@ struct GroupWave {
         const int32_t action = rl32(v.y, 3);
         o.ok = rl32(v.z, 3) != 0 && noid == oid && naid == aid;
         o.side = book_side(nsid, action == BUY);
+        o.sell = action == SELL; o.sid_neg = hi32(nsid) < 0;
         o.price = rl32(v.x, 3);
         o.size = rl32(v.x, 2); o.next = rl32(v.y, 2); o.prev = rl32(v.z, 2);
         o.prev_oid = mk64(rl32(v.z, 1), rl32(v.w, 1));
@@ -1561,7 +1567,7 @@ struct GroupWave {
         if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
             o.ok = rl32(B.pf_ok, r.lane);
             const int32_t meta = rl32(B.pf_meta, r.lane);
-            o.price = meta & 0xFF; o.side = meta >> 8;
+            o.price = meta & 0xFF; o.side = (meta >> 8) & 1; o.sell = (meta >> 9) & 1; o.sid_neg = (meta >> 10) & 1;
             o.size = rl32(B.pf_size, r.lane); o.next = rl32(B.pf_next, r.lane); o.prev = rl32(B.pf_prev, r.lane);
             o.prev_oid = rl64(B.pf_poid, r.lane);
         } else {
@@ -1594,6 +1600,8 @@ struct GroupWave {
         }
         L.qty[li] = U64(L.qty[li]) - o.size;
         free_slot(slot);
+        if (ledger_replay)   // the removed order, for postRemoveAdjustments in k_ledger_replay
+            vic[r.i] = make_int4(o.price | ((o.sell ? SELL : BUY) << 8), o.size, o.sid_neg ? -g : g, o.sid_neg ? -1 : 0);
         return !dead;
     }
 
@@ -1695,7 +1703,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
             const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
             B.pf_ok = c3.z != 0 && noid == B.oid && naid == B.aid;
-            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8);
+            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10);
             B.pf_poid = mk64(c1.z, c1.w);
             B.pf_size = c2.x; B.pf_next = c2.y; B.pf_prev = c2.z;
         }
@@ -1835,6 +1843,61 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
         S.ctr[ci(C_TRADES)] = c.tnext;
         S.ctr[ci(C_RESTS)] = n_rest;
         S.ctr[ci(C_CANCEL_OK)] = n_cancel;
+    }
+}
+
+// FUNDED + KME_FLAG_EXACT_LEDGER (row f next-2): the epoch's ledger effects replayed in arrival
+// order on one wavefront, after the parallel matching decided every outcome: createBalance /
+// transfer (KP:131-146), checkBalance (KP:167-182) for each accepted BUY/SELL, both fillOrder calls
+// per trade in executeTrade order (KP:265-287), postRemoveAdjustments (KP:325-333) for each
+// accepted cancel -- all on the exact Balances / Positions tables of EXACT mode (Core), so the
+// value-keyed position writes (KP:434-436) clobber exactly what the reference clobbers.
+__global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
+    const DevState& S = *Sp;
+    const EpochIO& io = *iop;
+    if (failed(S.ctr)) return;
+    Core c(S, io);
+    const int lane = lane_id();
+    for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool valid = k < io.n;
+        const uint32_t bi = valid ? k : 0;
+        const int32_t b_action = valid ? io.action[bi] : -1, b_out = valid ? io.out_action[bi] : -1;
+        const int32_t b_price = valid ? io.price[bi] : 0, b_size = valid ? io.size[bi] : 0;
+        const int64_t b_aid = valid ? io.aid[bi] : 0, b_sid = valid ? io.sid[bi] : 0, b_oid = valid ? io.oid[bi] : 0;
+        const uint32_t b_t0 = valid ? io.trade_off[bi] : 0, b_t1 = valid ? io.trade_off[bi + 1] : 0;
+        const int4 b_vic = (valid && b_action == CANCEL && b_out == CANCEL) ? S.vic[bi] : make_int4(0, 0, 0, 0);
+        const int nb = (int)(io.n - k0 < 64 ? io.n - k0 : 64);
+#pragma nounroll
+        for (int j = 0; j < nb && !c.dead; ++j) {
+            const uint32_t i = k0 + (uint32_t)j;
+            const int32_t a = rl32(b_action, j), out = rl32(b_out, j);
+            const int64_t aid = rl64(b_aid, j);
+            if (a == CREATE_BALANCE) {
+                c.create_balance(aid, i);
+            } else if (a == TRANSFER) {
+                c.transfer(aid, rl32(b_size, j));
+            } else if ((a == BUY || a == SELL) && out == a) {
+                Taker t;
+                t.action = a; t.price = rl32(b_price, j); t.size = rl32(b_size, j); t._pad = 0;
+                t.oid = rl64(b_oid, j); t.aid = aid; t.sid = rl64(b_sid, j);
+                if (!c.check_balance(t, i)) { if (!c.dead) c.die(KME_E_UNFUNDED, KME_D_NONE, i); break; }
+                const bool is_buy = a == BUY;
+                for (uint32_t q = (uint32_t)rl32((int32_t)b_t0, j); q < (uint32_t)rl32((int32_t)b_t1, j) && !c.dead; ++q) {
+                    const TradeRec tr = io.trades[q];
+                    const int64_t maid = U64(tr.maid), msid = U64(tr.msid);
+                    const int32_t mprice = U32(tr.mprice), ts = U32(tr.size);
+                    c.fill_order(is_buy ? SOLD : BOUGHT, maid, msid, 0, ts, i);                       // maker fill
+                    if (!c.dead) c.fill_order(is_buy ? BOUGHT : SOLD, aid, t.sid, jisub(t.price, mprice), ts, i);
+                }
+            } else if (a == CANCEL && out == CANCEL) {
+                Node o;
+                const int32_t meta = rl32(b_vic.x, j);
+                o.price = meta & 0xFF; o.action = meta >> 8; o.size = rl32(b_vic.y, j);
+                o.sid = mk64(rl32(b_vic.z, j), rl32(b_vic.w, j)); o.aid = aid;
+                c.post_remove_adjustments(o, i);
+            }
+        }
     }
 }
 
@@ -2011,6 +2074,9 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
     hipLaunchKernelGGL(k_table, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);
+}
+void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
+    hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);
 }
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev);

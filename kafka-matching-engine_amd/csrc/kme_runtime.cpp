@@ -23,8 +23,8 @@ using namespace kme;
 
 namespace {
 
-const char* kPhaseNames[] = {"emap", "ledger", "route", "partition", "match", "compact", "table", "serial"};
-enum Phase { PH_EMAP, PH_LEDGER, PH_ROUTE, PH_PART, PH_MATCH, PH_COMPACT, PH_TABLE, PH_SERIAL, PH_N };
+const char* kPhaseNames[] = {"emap", "ledger", "route", "partition", "match", "compact", "table", "serial", "replay"};
+enum Phase { PH_EMAP, PH_LEDGER, PH_ROUTE, PH_PART, PH_MATCH, PH_COMPACT, PH_TABLE, PH_SERIAL, PH_REPLAY, PH_N };
 
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t p = 1;
@@ -141,6 +141,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         return KME_E_INVALID;
     if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28)))
         return KME_E_INVALID;
+    if ((cfg->flags & ~KME_FLAG_EXACT_LEDGER) != 0 ||
+        ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1))   // a shard sees part of the ledger only
+        return KME_E_INVALID;
     if (cfg->credit_shards > (1u << 16) || (cfg->mode == KME_MODE_EXACT && cfg->credit_shards > 1))
         return KME_E_INVALID;
     kme_engine* e = new kme_engine();
@@ -182,13 +185,17 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.lev, (size_t)G * 2 * NLEV);
     ALLOC(S.pool, P);
     ALLOC(S.otab, e->otab_cap);
+    const bool exact_ledger = !funded || (cfg->flags & KME_FLAG_EXACT_LEDGER);
+    S.ledger_replay = funded && exact_ledger ? 1 : 0;
     if (funded) {
         ALLOC(S.acct_since, cfg->max_accounts);
         ALLOC(S.acct_lb, cfg->max_accounts);
         ALLOC(S.acct_need, cfg->max_accounts);
         ALLOC(S.acct_negx, cfg->max_accounts);
         ALLOC(S.acct_xfer, cfg->max_accounts);
-    } else {
+        if (S.ledger_replay) ALLOC(S.vic, E);
+    }
+    if (exact_ledger) {
         const uint64_t lc = pow2_at_least(std::max<uint64_t>(2 * std::max<uint64_t>(cfg->ledger_capacity, 1024), 2048));
         if (lc > (1ull << 31)) { kme_destroy(e); return KME_E_INVALID; }
         S.bal_mask = (uint32_t)(lc - 1);
@@ -241,7 +248,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         HIP_TRY(hipMemsetAsync(S.acct_need, 0, cfg->max_accounts * sizeof(int64_t), st));
         HIP_TRY(hipMemsetAsync(S.acct_negx, 0, cfg->max_accounts * sizeof(int64_t), st));
         HIP_TRY(hipMemsetAsync(S.acct_xfer, 0, cfg->max_accounts * sizeof(int64_t), st));
-    } else {
+    }
+    if (exact_ledger) {
         const size_t lc = (size_t)S.bal_mask + 1;
         HIP_TRY(hipMemsetAsync(S.bal_state, 0, lc * sizeof(uint32_t), st));
         HIP_TRY(hipMemsetAsync(S.pos_state, 0, lc * sizeof(uint32_t), st));
@@ -332,6 +340,11 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         phase_begin(e, PH_COMPACT);
         launch_compact(S, io, st);
         phase_end(e, PH_COMPACT);
+        if (S.ledger_replay) {
+            phase_begin(e, PH_REPLAY);
+            launch_ledger_replay(e->d_S, e->d_io, st);
+            phase_end(e, PH_REPLAY);
+        }
     } else {
         phase_begin(e, PH_SERIAL);
         launch_serial(e->d_S, e->d_io, st);
@@ -424,7 +437,8 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
     if (e->cfg.mode == KME_MODE_FUNDED) {
         b.push_back({S.acct_since, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
         b.push_back({S.acct_lb, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
-    } else {
+    }
+    if (e->cfg.mode == KME_MODE_EXACT || S.ledger_replay) {
         const size_t lc = (size_t)S.bal_mask + 1;
         b.push_back({S.bal_state, lc * sizeof(uint32_t)});
         b.push_back({S.bal_key, lc * sizeof(int64_t)});
@@ -478,7 +492,8 @@ kme_status kme_restore(kme_engine* e, const char* path) {
     ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
          h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
          h.cfg.max_resting == e->cfg.max_resting && h.cfg.ledger_capacity == e->cfg.ledger_capacity &&
-         h.cfg.credit_shards == e->cfg.credit_shards && h.pool_used <= e->cfg.max_resting;
+         h.cfg.credit_shards == e->cfg.credit_shards && h.cfg.flags == e->cfg.flags &&
+         h.pool_used <= e->cfg.max_resting;
     std::vector<char> host;
     for (const Blob& b : ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{}) {
         uint64_t n = 0;
@@ -735,7 +750,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
 
 kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
     if (!e || !text) return KME_E_INVALID;
-    if (e->cfg.mode != KME_MODE_EXACT) return KME_E_UNSUPPORTED;
+    if (e->cfg.mode != KME_MODE_EXACT && !e->S.ledger_replay) return KME_E_UNSUPPORTED;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     const size_t lc = (size_t)e->S.bal_mask + 1;

@@ -26,7 +26,8 @@ MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
           7: "FAILED"}
-ABI_VERSION = 1
+ABI_VERSION = 2
+FLAG_EXACT_LEDGER = 1
 
 TRADE_DTYPE = np.dtype([("maker_oid", "<i8"), ("maker_aid", "<i8"), ("maker_sid", "<i8"),
                         ("maker_price", "<i4"), ("size", "<i4")])
@@ -38,7 +39,7 @@ class kme_config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("mode", C.c_uint32), ("max_symbols", C.c_uint32),
                 ("max_accounts", C.c_uint32), ("max_epoch", C.c_uint32), ("max_trades", C.c_uint32),
                 ("max_resting", C.c_uint64), ("ledger_capacity", C.c_uint64), ("device", C.c_int32),
-                ("credit_shards", C.c_uint32)]
+                ("credit_shards", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32)]
 
 
 class kme_orders(C.Structure):
@@ -189,10 +190,11 @@ class EpochResult:
 
 
 def default_config(mode: int, max_symbols: int, max_epoch: int, max_resting: int, max_trades: int | None = None,
-                   max_accounts: int = 0, ledger_capacity: int = 1 << 16, device: int = 0) -> kme_config:
+                   max_accounts: int = 0, ledger_capacity: int = 1 << 16, device: int = 0,
+                   flags: int = 0) -> kme_config:
     return kme_config(ABI_VERSION, mode, max_symbols, max_accounts, max_epoch,
                       max_trades if max_trades is not None else max(4 * max_epoch, 1 << 16),
-                      max_resting, ledger_capacity, device, 0)
+                      max_resting, ledger_capacity, device, 0, flags, 0)
 
 
 class Engine:

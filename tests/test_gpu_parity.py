@@ -251,3 +251,31 @@ def test_checkpoint_restore_resumes_exactly(kme_mod, oracle_mod, mode, tmp_path)
     assert b.snapshot_books() == o.dump_books()
     if mode == "exact":
         assert b.snapshot_ledger() == o.dump_ledger()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "cancel_replace", "hazards"])
+def test_funded_exact_ledger_replay(kme_mod, oracle_mod, kind):
+    """Row f next-2: FUNDED matching in parallel + the serial ledger replay gives the reference's
+    final Balances / Positions stores, value-keyed position writes (KP:434-436) included."""
+    if kind == "hazards":
+        names = [n for n in sorted(hazards.FUNDED_OK)]
+        streams = [hazards.as_orders(hazards.streams()[n]) for n in names]
+        G, A = 8, 16
+    else:
+        n_sym, n_acc = 24, 48
+        body = (W.uniform(20_000, n_symbols=n_sym, n_accounts=n_acc, seed=41) if kind == "uniform"
+                else W.cancel_replace(12_000, n_symbols=n_sym, n_accounts=n_acc, seed=42))
+        k = W.funded_transfers_needed(len(body), n_acc, big=kind == "cancel_replace")
+        streams = [W.Orders.concat([W.funded_setup(n_acc, range(1, n_sym + 1), transfers_per_account=k), body])]
+        G, A = n_sym + 1, n_acc
+    for orders in streams:
+        eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=G, max_epoch=4096,
+                                                    max_resting=1 << 16, max_accounts=A,
+                                                    flags=kme_mod.FLAG_EXACT_LEDGER))
+        got = _run_epochs(eng, orders, 4096)
+        o = oracle_mod.Oracle()
+        o.process(orders)
+        assert got == o.tape_text(), _first_diff(got, o.tape_text())
+        assert eng.snapshot_books() == o.dump_books()
+        assert eng.snapshot_ledger() == o.dump_ledger()
+        eng.close()
