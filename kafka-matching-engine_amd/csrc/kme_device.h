@@ -45,10 +45,11 @@ struct alignas(32) Level {         // one bucket (KP:379-389)
 static_assert(sizeof(Level) == 32, "Level");
 
 struct alignas(64) Node {          // one resting Order (KP:449-458)
-    int64_t oid, aid, sid;
+    int64_t oid, aid, sid;         // bytes 0..31: what a maker contributes to a trade, one
+    int32_t size, next;            //   s_load_dwordx8 in the matching loop
     int64_t prev_oid;              // oid of the previous node in the level (valid when prev >= 0)
-    int32_t size, next, prev, group;
-    int32_t price, action, live, _pad;
+    int32_t prev, group;
+    int32_t price, action, live, _pad;   // live = word 14 (free-list blocks use words 0..13)
 };
 static_assert(sizeof(Node) == 64, "Node");
 

@@ -98,7 +98,9 @@ KDEV bool failed(const unsigned long long* ctr) {
 // Integer restatement: ctz / clz, the NaN path of a negative argument (-> 0), and the overshoot
 // of log10 rounding for h >= 47 (h + 1 once n >= 2^(h+1) - D[h]; D[] from
 // tools/gen_log10_table.py under a correctly rounded log10).  No floating point on the device.
-__constant__ int64_t kLog10D[16] = {1, 2, 3, 7, 14, 28, 90, 178, 340, 663, 1296, 2527, 4799, 9344, 18175, 35328};
+// D[h - 47] for h = 47..62, 16 bits each, four per word: register-only (a table in memory put an
+// SMEM load and its lgkmcnt wait on every bid-side scan of the matching loop).
+constexpr uint64_t kLog10D0 = 0x0007000300020001ull, kLog10D1 = 0x00b2005a001c000eull, kLog10D2 = 0x09df051002970154ull, kLog10D3 = 0x8a0046ff248012bfull;
 
 KDEV int32_t first_set_bit_pos(uint64_t n) {          // KP:371-373, n != 0
     uint64_t low = n & (0ull - n);
@@ -108,7 +110,14 @@ KDEV int32_t first_set_bit_pos(uint64_t n) {          // KP:371-373, n != 0
 KDEV int32_t last_set_bit_pos(uint64_t n) {           // KP:375-377, n != 0
     if ((int64_t)n < 0) return 0;
     int32_t h = 63 - (int32_t)__builtin_clzll(n);
-    if (h >= 47 && n >= (2ull << h) - (uint64_t)kLog10D[h - 47]) h += 1;
+    if (h >= 47) {
+        const uint64_t r = (2ull << h) - n;              // n >= 2^(h+1) - D[h]  <=>  r <= D[h]
+        if (r <= 35328) {
+            const uint32_t k = (uint32_t)(h - 47);
+            const uint64_t w = k < 8 ? (k < 4 ? kLog10D0 : kLog10D1) : (k < 12 ? kLog10D2 : kLog10D3);
+            if (r <= ((w >> (16 * (k & 3))) & 0xFFFFull)) h += 1;
+        }
+    }
     return h;
 }
 KDEV int32_t min_price_ptr(uint64_t lsb, uint64_t msb) {   // KP:359-363
@@ -1102,6 +1111,14 @@ KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 // stores; nodes written since the last vmcnt(0) (the batch dirty filter) take the vector path.
 // The wait sits in the same asm block: the compiler does not track this lgkmcnt event.
 typedef int32_t v16i __attribute__((ext_vector_type(16)));
+typedef int32_t v8i __attribute__((ext_vector_type(8)));
+// the first 32 bytes (oid, aid, sid, size, next): a maker
+KDEV v8i sload_maker(const KG Node* p) {
+    const uint64_t a = bcast64((uint64_t)(uintptr_t)p);
+    v8i r;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(a) : "memory");
+    return r;
+}
 KDEV v16i sload_node(const KG Node* p) {
     const uint64_t a = bcast64((uint64_t)(uintptr_t)p);   // an SGPR pair even where the compiler
     v16i r;                                                // would keep the address in VGPRs
@@ -1325,17 +1342,17 @@ struct GroupWave {
     KDEV Maker ld_maker(int32_t s) const {
         Maker m;
         if (!is_dirty(s)) {
-            const v16i v = sload_node(&pool[s]);
+            const v8i v = sload_maker(&pool[s]);
             m.oid = mk64(v[0], v[1]); m.aid = mk64(v[2], v[3]); m.sid = mk64(v[4], v[5]);
-            m.size = v[8]; m.next = v[9];
+            m.size = v[6]; m.next = v[7];
             return m;
         }
         const int4 v = reinterpret_cast<const KG int4*>(&pool[s])[q];
         m.oid = mk64(rl32(v.x, 0), rl32(v.y, 0));
         m.aid = mk64(rl32(v.z, 0), rl32(v.w, 0));
         m.sid = mk64(rl32(v.x, 1), rl32(v.y, 1));
-        m.size = rl32(v.x, 2);
-        m.next = rl32(v.y, 2);
+        m.size = rl32(v.z, 1);
+        m.next = rl32(v.w, 1);
         return m;
     }
 
@@ -1420,9 +1437,9 @@ struct GroupWave {
             // head, a valid node; a divergent branch here would demote the loop state to VGPRs)
             pf_slot = reach ? L.ht[lp].x : ms;
             const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[pf_slot]);
-            const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2];
+            const int4 c0 = nd[0], c1 = nd[1];
             pf_oid0 = c0.x; pf_oid1 = c0.y; pf_aid0 = c0.z; pf_aid1 = c0.w;
-            pf_sid0 = c1.x; pf_sid1 = c1.y; pf_size = c2.x; pf_next = c2.y;
+            pf_sid0 = c1.x; pf_sid1 = c1.y; pf_size = c1.z; pf_next = c1.w;
         }
         bool head_moved = false;                             // ms is a later maker of level li
         for (;;) {
@@ -1521,10 +1538,10 @@ struct GroupWave {
         // by bit: a compare chain on q becomes a switch whose default the compiler marks
         // unreachable, a divergent loop exit that demotes the whole loop's state to VGPRs.
         const bool q0 = (q & 1) != 0, q1 = (q & 2) != 0;
-        const int32_t x = q1 ? (q0 ? p : tsize) : (q0 ? lo32(r.sid) : lo32(r.oid));
-        const int32_t y = q1 ? (q0 ? r.action : -1) : (q0 ? hi32(r.sid) : hi32(r.oid));
-        const int32_t z = q1 ? (q0 ? 1 : nprev) : (q0 ? lo32(poid) : lo32(r.aid));
-        const int32_t w = q1 ? (q0 ? 0 : g) : (q0 ? hi32(poid) : hi32(r.aid));
+        const int32_t x = q1 ? (q0 ? p : lo32(poid)) : (q0 ? lo32(r.sid) : lo32(r.oid));
+        const int32_t y = q1 ? (q0 ? r.action : hi32(poid)) : (q0 ? hi32(r.sid) : hi32(r.oid));
+        const int32_t z = q1 ? (q0 ? 1 : nprev) : (q0 ? tsize : lo32(r.aid));
+        const int32_t w = q1 ? (q0 ? 0 : g) : (q0 ? -1 : hi32(r.aid));
         if (lane < 4) reinterpret_cast<KG int4*>(&pool[slot])[lane] = make_int4(x, y, z, w);
         mark_dirty(slot);
         rest_slot[r.i] = slot;
@@ -1542,8 +1559,8 @@ struct GroupWave {
             o.side = book_side(mk64(v[4], v[5]), action == BUY);
             o.sell = action == SELL; o.sid_neg = v[5] < 0;
             o.price = v[12];
-            o.size = v[8]; o.next = v[9]; o.prev = v[10];
-            o.prev_oid = mk64(v[6], v[7]);
+            o.size = v[6]; o.next = v[7]; o.prev = v[10];
+            o.prev_oid = mk64(v[8], v[9]);
             return o;
         }
         const int4 v = reinterpret_cast<const KG int4*>(&pool[s])[q];
@@ -1554,8 +1571,8 @@ struct GroupWave {
         o.side = book_side(nsid, action == BUY);
         o.sell = action == SELL; o.sid_neg = hi32(nsid) < 0;
         o.price = rl32(v.x, 3);
-        o.size = rl32(v.x, 2); o.next = rl32(v.y, 2); o.prev = rl32(v.z, 2);
-        o.prev_oid = mk64(rl32(v.z, 1), rl32(v.w, 1));
+        o.size = rl32(v.z, 1); o.next = rl32(v.w, 1); o.prev = rl32(v.z, 2);
+        o.prev_oid = mk64(rl32(v.x, 2), rl32(v.y, 2));
         return o;
     }
     KDEV bool cancel(const Rec& r, const Lanes& B) {
@@ -1704,8 +1721,8 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
             B.pf_ok = c3.z != 0 && noid == B.oid && naid == B.aid;
             B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10);
-            B.pf_poid = mk64(c1.z, c1.w);
-            B.pf_size = c2.x; B.pf_next = c2.y; B.pf_prev = c2.z;
+            B.pf_poid = mk64(c2.x, c2.y);
+            B.pf_size = c1.z; B.pf_next = c1.w; B.pf_prev = c2.z;
         }
         lds.dirty[lane] = 0;
         w.sync_lds();
@@ -1735,9 +1752,12 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
 #ifdef KME_STAMPS
             {
                 const unsigned long long dt = stamp() - tr0;
-                const int cat = (r.action == BUY || r.action == SELL) ? (o.ntr ? 0 : 1) : (r.action == CANCEL ? 2 : 3);
-                w.acc[ST_TRADE_REC + cat] += dt;
-                if (cat < 3) w.acc[ST_N_TRADE_REC + cat] += 1;
+                // constant indices only: a computed index puts acc[] in scratch memory
+                if (r.action == BUY || r.action == SELL) {
+                    if (o.ntr) { w.acc[ST_TRADE_REC] += dt; w.acc[ST_N_TRADE_REC] += 1; }
+                    else { w.acc[ST_REST_REC] += dt; w.acc[ST_N_REST_REC] += 1; }
+                } else if (r.action == CANCEL) { w.acc[ST_CANCEL_REC] += dt; w.acc[ST_N_CANCEL_REC] += 1; }
+                else w.acc[ST_OTHER_REC] += dt;
             }
 #endif
             const bool me = lane == j;
