@@ -50,15 +50,16 @@ def algorithmic_bytes(st) -> int:
             + 48 * st.n_cancel_ok)
 
 
-def make_workload(name: str, n_orders: int, rank: int, world: int, symbols: int = 0):
+def make_workload(name: str, n_orders: int, rank: int, world: int, symbols: int = 0, mix=None):
     seed = 1000 + rank
+    mix = tuple(mix) if mix else (0.34, 0.33, 0.33)
     if name == "c2":
         nsym, nacc = 1024, 4096
-        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed, mix=mix)
         desc = "C2: 1,024 symbols x 16M uniform limit/cancel orders per GPU (BASELINE configs[1])"
     elif name == "c3":
         nsym, nacc = (symbols or C3_SYMBOLS // world), C3_ACCOUNTS
-        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed, mix=mix)
         desc = (f"C3: 65,536 symbols symbol-sharded over {world} GPU(s) = {nsym:,} symbols per GPU, "
                 f"uniform limit/cancel orders (BASELINE configs[2])")
     elif name == "c4":
@@ -103,6 +104,7 @@ def main():
     ap.add_argument("--epoch", type=int, default=1 << 22)
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default 65,536 / N)")
+    ap.add_argument("--mix", default="", help="diagnostic: BUY,SELL,CANCEL fractions of the c2/c3 stream")
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,7 +123,8 @@ def main():
 
     E = args.epoch
     total = max(args.orders, (args.warmup + args.steps) * E)
-    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world, args.symbols)
+    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world, args.symbols,
+                                                   [float(x) for x in args.mix.split(",")] if args.mix else None)
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
                              max_resting=min(total, 1 << 30), max_trades=2 * E + (1 << 16),

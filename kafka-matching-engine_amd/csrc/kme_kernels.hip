@@ -31,6 +31,7 @@
 namespace kme {
 
 #define KDEV __device__ __forceinline__
+#define KC __attribute__((address_space(4)))   // constant address space: scalar loads
 
 // ------------------------------------------------------------------ Java arithmetic (wraps)
 KDEV int32_t jiadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
@@ -1089,8 +1090,9 @@ struct Core {
 //     trade against a maker or to cancel (a cancel's node is prefetched with its batch);
 //   * records arrive 64 at a time, one per lane; the OUT fields and the trades collect in lanes
 //     and leave in coalesced stores (one per field per batch, one per 64 trades).
-constexpr int LVP = 104;          // LDS level entries per book side: prices 0..100 (+ pad)
+constexpr int LVP = 101;          // LDS level entries per book side: prices 0..100
 constexpr int FSTK = 128;         // LDS free-slot stack
+constexpr int TRD = 32;           // trades staged in LDS between reservations (GroupWave::emit)
 constexpr int DIRTY_WORDS = 64;   // 2048-bit filter of node slots written since the batch prefetch
 constexpr int FBLK = 13;          // free slots per spilled free-list block (GroupWave::alloc_slot)
 
@@ -1100,9 +1102,17 @@ struct GroupLds {
     int64_t toid[2 * LVP];        // oid of the tail node = OUT.prev of an append (KP:213-217)
     int32_t fstack[FSTK];
     uint32_t dirty[DIRTY_WORDS];
+    int4 trd[2 * TRD];            // trade k: (maker oid, maker aid), (price | sid < 0 << 8, size, seq, ord)
 };
 
 KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// A constant-space view of *p that the compiler cannot hoist: every field read through it is a
+// scalar load at the point of use (GroupWave::cold).
+template <class T> KDEV const KC T& opaque_const(const T* p) {
+    uint64_t v = (uint64_t)(uintptr_t)p;
+    asm volatile("" : "+s"(v));
+    return *(const KC T*)(uintptr_t)bcast64(v);
+}
 
 // A whole 64-byte node into 16 SGPRs through the scalar memory path.  Vector loads and stores share
 // one in-order counter (vmcnt), so a vector load of a maker waits for every store the wavefront
@@ -1150,7 +1160,8 @@ __device__ __attribute__((noinline)) uint64_t trade_overflow(KG TradeTmp* ttmp, 
 // A maker as tryMatch reads it (KP:236-241, 266): oid, aid, sid, size, next.  Lane q of the
 // wavefront loads 16-byte piece q of the 64-byte node; readlane picks the fields.
 struct Maker {
-    int64_t oid, aid, sid;
+    int64_t oid, aid;
+    int32_t sneg;                 // sid < 0: a maker of group g has sid = +-g (sid 0 for group 0)
     int32_t size, next;
 };
 // A resting order as removeOrder reads it (KP:290-323), already validated against the cancel.
@@ -1168,7 +1179,7 @@ struct Lanes {
     uint32_t i;
     int32_t w0, size, tgt;        // PRec word 0 (action | price << 8 | acct_ok << 16 | sid < 0 << 17)
     int64_t oid, aid;
-    int32_t pf_slot, pf_ok, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10
+    int32_t pf_slot, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10 | ok << 11
     int64_t pf_poid;
 };
 
@@ -1182,22 +1193,14 @@ enum Stamp : int {
 
 struct GroupWave {
     KG Node* pool;
-    KG Level* lev;                // this group's [2][NLEV] HBM levels
-    KG GroupState* gst;
-    KG TradeTmp* ttmp;
-    KG unsigned long long* ctr;
-    KG unsigned long long* tsh;       // this group's trade shard line
     KG int32_t* rest_slot;
-    KG int4* vic;
-    int32_t ledger_replay;
-    uint32_t pool_cap, ttmp_cap, tshard_cap, tbase;   // tbase: first record of the shard region
+    const DevState* Sp;           // everything off the per-record path is re-read through cold()
     GroupLds& L;
     const int lane, q;            // q = lane & 3: the node piece this lane loads / stores
     int32_t g, exists;
     uint64_t b0l, b0m, b1l, b1m;  // bitmaps of book +g (side 0) and book -g (side 1)
     int32_t fsp, free_head, chunk_next, chunk_end;
-    int32_t tcnt;                 // trades collected in the lanes (lane k holds trade k)
-    int32_t t_oid0, t_oid1, t_aid0, t_aid1, t_sid0, t_sid1, t_px, t_sz, t_seq, t_ord;
+    int32_t tcnt;                 // trades staged in L.trd
     uint32_t cur;                 // input index of the record being processed
     bool dead;
 #ifdef KME_STAMPS
@@ -1205,20 +1208,27 @@ struct GroupWave {
 #endif
 
     KDEV GroupWave(const DevState& S, GroupLds& lds, int32_t gg)
-        : pool(S.pool), lev(S.lev + (size_t)gg * 2 * NLEV), gst(S.grp + gg), ttmp(S.ttmp), ctr(S.ctr),
-          tsh(S.tsh + (size_t)(gg & (TSHARDS - 1)) * CTR_STRIDE), rest_slot(S.rest_slot), vic(S.vic),
-          ledger_replay(S.ledger_replay), pool_cap(S.pool_cap),
-          ttmp_cap(S.ttmp_cap), tshard_cap(S.tshard_cap), tbase((uint32_t)(gg & (TSHARDS - 1)) * S.tshard_cap), L(lds),
+        : pool(S.pool), rest_slot(S.rest_slot), Sp(&S), L(lds),
           lane(lane_id()),
           q(lane_id() & 3), g(gg) {
         exists = 0; b0l = b0m = b1l = b1m = 0;
         fsp = 0; free_head = -1; chunk_next = chunk_end = 0;
-        tcnt = 0; t_oid0 = t_oid1 = t_aid0 = t_aid1 = t_sid0 = t_sid1 = t_px = t_sz = t_seq = t_ord = 0;
+        tcnt = 0;
         cur = 0; dead = false;
         KST(for (int k = 0; k < ST_N; ++k) acc[k] = 0;)
     }
 
-    KDEV void die(int status, int detail) { raise_wave(ctr, status, detail, (int64_t)cur); dead = true; }
+    // Fields used off the per-record path (level and group-state homes, trade scratch, counters,
+    // capacities) are not kept in registers across the matching loops: the wavefront's live
+    // uniform state already exceeds the SGPR file, and every register such a field pins is one
+    // more spill.  cold() hands out the state through an opaque constant-space pointer, so each
+    // use is a scalar load (scalar cache) at the point of use, never hoisted.
+    KDEV const KC DevState& cold() const { return opaque_const(Sp); }
+    KDEV KG Level* lev() const { return cold().lev + (size_t)g * 2 * NLEV; }
+    KDEV KG GroupState* gst() const { return cold().grp + g; }
+    KDEV KG unsigned long long* ctr() const { return cold().ctr; }
+    KDEV KG unsigned long long* tsh() const { return cold().tsh + (size_t)(g & (TSHARDS - 1)) * CTR_STRIDE; }
+    KDEV void die(int status, int detail) { raise_wave(ctr(), status, detail, (int64_t)cur); dead = true; }
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
     KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
     KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
@@ -1229,7 +1239,7 @@ struct GroupWave {
 
     // ---------------- group state in and out
     KDEV void load_group() {
-        const int4 v = reinterpret_cast<const KG int4*>(gst)[q];
+        const int4 v = reinterpret_cast<const KG int4*>(gst())[q];
         b0l = (uint64_t)mk64(rl32(v.x, 0), rl32(v.y, 0)); b0m = (uint64_t)mk64(rl32(v.z, 0), rl32(v.w, 0));
         b1l = (uint64_t)mk64(rl32(v.x, 1), rl32(v.y, 1)); b1m = (uint64_t)mk64(rl32(v.z, 1), rl32(v.w, 1));
         exists = rl32(v.x, 2); free_head = rl32(v.y, 2); chunk_next = rl32(v.z, 2); chunk_end = rl32(v.w, 2);
@@ -1243,7 +1253,7 @@ struct GroupWave {
         const int32_t y = q1 ? free_head : (q0 ? hi32((int64_t)b1l) : hi32((int64_t)b0l));
         const int32_t z = q1 ? chunk_next : (q0 ? lo32((int64_t)b1m) : lo32((int64_t)b0m));
         const int32_t w = q1 ? chunk_end : (q0 ? hi32((int64_t)b1m) : hi32((int64_t)b0m));
-        if (lane < 3) reinterpret_cast<KG int4*>(gst)[lane] = make_int4(x, y, z, w);
+        if (lane < 3) reinterpret_cast<KG int4*>(gst())[lane] = make_int4(x, y, z, w);
     }
     // Occupied levels of both books move between HBM (Level, 32 B) and LDS in one parallel pass:
     // lane l takes prices l and l + 64.  An unoccupied level's fields are dead until a rest
@@ -1257,7 +1267,7 @@ struct GroupWave {
                 const int p = lane + 64 * h;
                 if (p <= 100 && check_bit(l, m, p)) {
                     const int li = side * LVP + p;
-                    KG int4* gl = reinterpret_cast<KG int4*>(&lev[side * NLEV + p]);
+                    KG int4* gl = reinterpret_cast<KG int4*>(&lev()[side * NLEV + p]);
                     if (in) {
                         const int4 x0 = gl[0], x1 = gl[1];
                         L.ht[li] = make_int2(x0.x, x0.y);
@@ -1294,9 +1304,10 @@ struct GroupWave {
         }
         if (chunk_next >= chunk_end) {
             unsigned long long c = 0;
-            if (lane == 0) c = atomicAdd(&ctr[ci(C_POOL_BUMP)], (unsigned long long)POOL_CHUNK);
+            KG unsigned long long* bump = &ctr()[ci(C_POOL_BUMP)];   // (no asm inside a lane branch)
+            if (lane == 0) c = atomicAdd(bump, (unsigned long long)POOL_CHUNK);
             c = bcast64(c);
-            if (c + POOL_CHUNK > pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return -1; }
+            if (c + POOL_CHUNK > cold().pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return -1; }
             chunk_next = (int32_t)c;
             chunk_end = (int32_t)(c + POOL_CHUNK);
         }
@@ -1343,28 +1354,27 @@ struct GroupWave {
         Maker m;
         if (!is_dirty(s)) {
             const v8i v = sload_maker(&pool[s]);
-            m.oid = mk64(v[0], v[1]); m.aid = mk64(v[2], v[3]); m.sid = mk64(v[4], v[5]);
+            m.oid = mk64(v[0], v[1]); m.aid = mk64(v[2], v[3]); m.sneg = v[5] < 0;
             m.size = v[6]; m.next = v[7];
             return m;
         }
         const int4 v = reinterpret_cast<const KG int4*>(&pool[s])[q];
         m.oid = mk64(rl32(v.x, 0), rl32(v.y, 0));
         m.aid = mk64(rl32(v.z, 0), rl32(v.w, 0));
-        m.sid = mk64(rl32(v.x, 1), rl32(v.y, 1));
+        m.sneg = rl32(v.y, 1) < 0;
         m.size = rl32(v.z, 1);
         m.next = rl32(v.w, 1);
         return m;
     }
 
-    // ---------------- trades: lane k holds trade k until 64 are collected (or the group ends)
+    // ---------------- trades: staged in LDS (trade k in L.trd[2k..2k+1]) until TRD are collected
+    // (or the group ends), then one coalesced store per lane.  Every lane stores the same values
+    // to the same address (no bank conflict, no exec mask); in lanes they would pin 8 VGPRs for the
+    // whole kernel, one wavefront per SIMD less.
     KDEV void emit(uint32_t ord, const Maker& m, int32_t mprice, int32_t ts) {
-        const bool me = lane == tcnt;
-        t_oid0 = me ? lo32(m.oid) : t_oid0; t_oid1 = me ? hi32(m.oid) : t_oid1;
-        t_aid0 = me ? lo32(m.aid) : t_aid0; t_aid1 = me ? hi32(m.aid) : t_aid1;
-        t_sid0 = me ? lo32(m.sid) : t_sid0; t_sid1 = me ? hi32(m.sid) : t_sid1;
-        t_px = me ? mprice : t_px; t_sz = me ? ts : t_sz;
-        t_seq = me ? (int32_t)cur : t_seq; t_ord = me ? (int32_t)ord : t_ord;
-        if (++tcnt == 64) flush_trades();
+        L.trd[2 * tcnt] = make_int4(lo32(m.oid), hi32(m.oid), lo32(m.aid), hi32(m.aid));
+        L.trd[2 * tcnt + 1] = make_int4(mprice | (m.sneg << 8), ts, (int32_t)cur, (int32_t)ord);
+        if (++tcnt == TRD) flush_trades();
     }
     // Reserves tcnt records in the group's shard region through the shard's own counter line.  When
     // the shard is full, the part of the region that reservation got ([base, cap)) is marked as
@@ -1374,20 +1384,29 @@ struct GroupWave {
     KDEV void flush_trades() {
         if (tcnt == 0) return;
         unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(&tsh[TS_USED], (unsigned long long)tcnt);
+        // (plain loads here: an opaque cold() on this path makes the compiler treat the exits of
+        // the loops around emit() as divergent)
+        const uint32_t tshard_cap = Sp->tshard_cap, tbase = (uint32_t)(g & (TSHARDS - 1)) * tshard_cap;
+        KG TradeTmp* ttmp = Sp->ttmp;
+        KG unsigned long long* used = &Sp->tsh[(size_t)(g & (TSHARDS - 1)) * CTR_STRIDE + TS_USED];
+        if (lane == 0) base = atomicAdd(used, (unsigned long long)tcnt);
         base = bcast64(base);
         size_t pos = (size_t)tbase + base;
         if (base + (unsigned long long)tcnt > tshard_cap) {
-            pos = (size_t)bcast64(trade_overflow(ttmp, ctr, tbase, tshard_cap, ttmp_cap, base, (uint32_t)tcnt));
+            pos = (size_t)bcast64(trade_overflow(ttmp, Sp->ctr, tbase, tshard_cap, Sp->ttmp_cap, base, (uint32_t)tcnt));
             if (pos == ~(size_t)0) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); tcnt = 0; return; }
         }
+        sync_lds();
         if (lane < tcnt) {
+            const int4 a = L.trd[2 * lane], b = L.trd[2 * lane + 1];
             KG int4* r = reinterpret_cast<KG int4*>(&ttmp[pos + lane]);
             KG int2* r2 = reinterpret_cast<KG int2*>(&ttmp[pos + lane]);
-            r[0] = make_int4(t_oid0, t_oid1, t_aid0, t_aid1);
-            r[1] = make_int4(t_sid0, t_sid1, t_px, t_sz);
-            r2[4] = make_int2(t_seq, t_ord);
+            const int64_t sid = (b.x >> 8) & 1 ? -(int64_t)g : (int64_t)g;
+            r[0] = a;
+            r[1] = make_int4(lo32(sid), hi32(sid), b.x & 0xFF, b.y);
+            r2[4] = make_int2(b.z, b.w);
         }
+        sync_lds();
         tcnt = 0;
     }
 
@@ -1423,7 +1442,7 @@ struct GroupWave {
         // KP:237-253 maker by maker.
         const int32_t pb0 = pb;
         uint64_t pfmask = 0;
-        int32_t pf_slot = -1, pf_oid0 = 0, pf_oid1 = 0, pf_aid0 = 0, pf_aid1 = 0, pf_sid0 = 0, pf_sid1 = 0, pf_size = 0,
+        int32_t pf_slot = -1, pf_oid0 = 0, pf_oid1 = 0, pf_aid0 = 0, pf_aid1 = 0, pf_sid1 = 0, pf_size = 0,
                 pf_next = 0;
         if ((int64_t)tsize > lqty) {
             const int p = is_buy ? pb + 1 + lane : pb - 1 - lane;
@@ -1439,7 +1458,7 @@ struct GroupWave {
             const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[pf_slot]);
             const int4 c0 = nd[0], c1 = nd[1];
             pf_oid0 = c0.x; pf_oid1 = c0.y; pf_aid0 = c0.z; pf_aid1 = c0.w;
-            pf_sid0 = c1.x; pf_sid1 = c1.y; pf_size = c1.z; pf_next = c1.w;
+            pf_sid1 = c1.y; pf_size = c1.z; pf_next = c1.w;
         }
         bool head_moved = false;                             // ms is a later maker of level li
         for (;;) {
@@ -1489,7 +1508,7 @@ struct GroupWave {
             const int l = is_buy ? npb - pb0 - 1 : pb0 - 1 - npb;
             if (!same && l >= 0 && l < 64 && ((pfmask >> l) & 1) && rl32(pf_slot, l) == nms) {   // swept level
                 nm.oid = mk64(rl32(pf_oid0, l), rl32(pf_oid1, l)); nm.aid = mk64(rl32(pf_aid0, l), rl32(pf_aid1, l));
-                nm.sid = mk64(rl32(pf_sid0, l), rl32(pf_sid1, l));
+                nm.sneg = rl32(pf_sid1, l) < 0;
                 nm.size = rl32(pf_size, l); nm.next = rl32(pf_next, l);
             } else {
                 nm = ld_maker(nms);                          // in flight during this trade's stores
@@ -1582,8 +1601,8 @@ struct GroupWave {
         if (slot < 0) return false;                          // orders.get(oid) == null
         Victim o;
         if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
-            o.ok = rl32(B.pf_ok, r.lane);
             const int32_t meta = rl32(B.pf_meta, r.lane);
+            o.ok = (meta >> 11) & 1;
             o.price = meta & 0xFF; o.side = (meta >> 8) & 1; o.sell = (meta >> 9) & 1; o.sid_neg = (meta >> 10) & 1;
             o.size = rl32(B.pf_size, r.lane); o.next = rl32(B.pf_next, r.lane); o.prev = rl32(B.pf_prev, r.lane);
             o.prev_oid = rl64(B.pf_poid, r.lane);
@@ -1617,8 +1636,8 @@ struct GroupWave {
         }
         L.qty[li] = U64(L.qty[li]) - o.size;
         free_slot(slot);
-        if (ledger_replay)   // the removed order, for postRemoveAdjustments in k_ledger_replay
-            vic[r.i] = make_int4(o.price | ((o.sell ? SELL : BUY) << 8), o.size, o.sid_neg ? -g : g, o.sid_neg ? -1 : 0);
+        if (cold().ledger_replay)   // the removed order, for postRemoveAdjustments in k_ledger_replay
+            cold().vic[r.i] = make_int4(o.price | ((o.sell ? SELL : BUY) << 8), o.size, o.sid_neg ? -g : g, o.sid_neg ? -1 : 0);
         return !dead;
     }
 
@@ -1676,7 +1695,6 @@ struct GroupWave {
 __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
-    const EpochIO& io = *iop;
     const int32_t g = blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
@@ -1686,16 +1704,17 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     GroupWave w(S, lds, g);
     w.load_group();
     KST(w.acc[ST_GROUP_IN] += stamp() - tk0;)
-    const KG uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
-    const KG int4* prec = S.prec;
-    const KG int32_t* rest_slot = S.rest_slot;
-    const KG Node* pool = S.pool;
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
     for (uint32_t k0 = b; k0 < e && !w.dead; k0 += 64) {
         KST(const unsigned long long tb0 = stamp();)
         const uint32_t k = k0 + lane;
         const bool valid = k < e;
+        const KC DevState& C = opaque_const(Sp);
+        const KG uint32_t* perm = buf ? C.rvals[1] : C.rvals[0];
+        const KG int4* prec = C.prec;
+        const KG int32_t* rest_slot = C.rest_slot;
+        const KG Node* pool = C.pool;
         Lanes B;
         B.i = valid ? perm[k] : 0;
         if (valid) {   // one 32-byte gather per record (PRec, written by k_route)
@@ -1714,13 +1733,14 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             if (B.tgt >= 0) B.pf_slot = B.tgt;
             else if (B.tgt <= -2 && (uint32_t)(-(B.tgt + 2)) < i_first) B.pf_slot = rest_slot[-(B.tgt + 2)];
         }
-        B.pf_ok = 0; B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
+        B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
         if (B.pf_slot >= 0) {
             const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[B.pf_slot]);
             const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
             const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
-            B.pf_ok = c3.z != 0 && noid == B.oid && naid == B.aid;
-            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10);
+            const bool ok = c3.z != 0 && noid == B.oid && naid == B.aid;
+            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10) |
+                        ((ok ? 1 : 0) << 11);
             B.pf_poid = mk64(c2.x, c2.y);
             B.pf_size = c1.z; B.pf_next = c1.w; B.pf_prev = c2.z;
         }
@@ -1732,7 +1752,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         __builtin_amdgcn_s_waitcnt(VMCNT0);
         const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
         // per-record OUT fields collect in lane j of these registers; one store per field per batch
-        int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_flag = 0, o_ntr = 0;
+        int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_ntr = 0;   // o_act: action | flags << 16
         KST(w.acc[ST_BATCH] += stamp() - tb0;)
 #pragma nounroll
         for (int j = 0; j < nb && !w.dead; ++j) {
@@ -1761,22 +1781,23 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             }
 #endif
             const bool me = lane == j;
-            o_act = me ? o.action : o_act;
+            o_act = me ? ((o.action & 0xFFFF) | (o.has_prev ? (int32_t)KME_OUT_HAS_PREV << 16 : 0) | (o.rested ? 2 << 16 : 0))
+                       : o_act;
             o_size = me ? o.size : o_size;
             o_plo = me ? lo32(o.prev) : o_plo;
             o_phi = me ? hi32(o.prev) : o_phi;
-            o_flag = me ? ((o.has_prev ? (int32_t)KME_OUT_HAS_PREV : 0) | (o.rested ? 2 : 0)) : o_flag;
             o_ntr = me ? (int32_t)o.ntr : o_ntr;
             KST(w.acc[ST_REC_OUT] += stamp() - tr0;)
         }
-        n_rest += (uint32_t)__popcll(__ballot(lane < nb && (o_flag & 2)));
-        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && b_action == CANCEL && o_act == CANCEL));
+        n_rest += (uint32_t)__popcll(__ballot(lane < nb && ((o_act >> 16) & 2)));
+        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
         if (lane < nb && !w.dead) {
+            const KC EpochIO& io = opaque_const(iop);
             const uint32_t i = B.i;
-            io.out_action[i] = o_act;
+            io.out_action[i] = o_act & 0xFFFF;
             io.out_size[i] = o_size;
             io.out_prev[i] = mk64(o_plo, o_phi);
-            io.out_flags[i] = (uint8_t)(o_flag & KME_OUT_HAS_PREV);
+            io.out_flags[i] = (uint8_t)((o_act >> 16) & KME_OUT_HAS_PREV);
             io.n_trades[i] = (uint32_t)o_ntr;
         }
     }
@@ -1784,9 +1805,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     w.flush_trades();
     KST(w.acc[ST_FLUSH] += stamp() - to0;)
     w.store_group();
+    KG unsigned long long* tsh = w.tsh();
     if (lane == 0) {
-        if (n_rest) atomicAdd(&w.tsh[TS_RESTS], (unsigned long long)n_rest);
-        if (n_cancel) atomicAdd(&w.tsh[TS_CANCELS], (unsigned long long)n_cancel);
+        if (n_rest) atomicAdd(&tsh[TS_RESTS], (unsigned long long)n_rest);
+        if (n_cancel) atomicAdd(&tsh[TS_CANCELS], (unsigned long long)n_cancel);
     }
 #ifdef KME_STAMPS
     const unsigned long long tk1 = stamp();

@@ -139,7 +139,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         cfg->max_epoch > (1u << 30) || cfg->max_resting == 0 || cfg->max_resting >= (1ull << 31) ||
         cfg->max_trades == 0)
         return KME_E_INVALID;
-    if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28)))
+    if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28) ||
+                                         cfg->max_resting + (uint64_t)(cfg->max_symbols + 1) * POOL_CHUNK >= (1ull << 31)))
         return KME_E_INVALID;
     if ((cfg->flags & ~KME_FLAG_EXACT_LEDGER) != 0 ||
         ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1))   // a shard sees part of the ledger only
@@ -157,7 +158,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     const bool funded = cfg->mode == KME_MODE_FUNDED;
     const uint32_t G = cfg->max_symbols;
     const uint32_t E = cfg->max_epoch;
-    const uint64_t P = cfg->max_resting;
+    // node pool: max_resting plus the slots a symbol group can hold back in its bump chunk
+    // (k_match takes POOL_CHUNK slots at a time), so that max_resting resting orders always fit
+    const uint64_t P = cfg->max_resting + (funded ? (uint64_t)(G + 1) * POOL_CHUNK : 0);
     DevState& S = e->S;
     S.G = (int32_t)G;
     S.mode = (int32_t)cfg->mode;
@@ -461,7 +464,7 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
     std::memcpy(h.magic, kCkptMagic, sizeof h.magic);
     h.cfg = e->cfg;
     h.seq_base = e->seq_base;
-    h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->cfg.max_resting);
+    h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
     h.otab_used = ctr[ci(C_OTAB_USED)];
     h.bal_used = ctr[ci(C_BAL_USED)];
     h.pos_used = ctr[ci(C_POS_USED)];
@@ -493,7 +496,7 @@ kme_status kme_restore(kme_engine* e, const char* path) {
          h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
          h.cfg.max_resting == e->cfg.max_resting && h.cfg.ledger_capacity == e->cfg.ledger_capacity &&
          h.cfg.credit_shards == e->cfg.credit_shards && h.cfg.flags == e->cfg.flags &&
-         h.pool_used <= e->cfg.max_resting;
+         h.pool_used <= e->S.pool_cap;
     std::vector<char> host;
     for (const Blob& b : ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{}) {
         uint64_t n = 0;
@@ -669,7 +672,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     std::vector<Level> lev((size_t)G * 2 * NLEV);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->cfg.max_resting);
+    const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
     std::vector<Node> pool(nslots);
     HIP_TRY(hipMemcpy(grp.data(), e->S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(lev.data(), e->S.lev, lev.size() * sizeof(Level), hipMemcpyDeviceToHost));

@@ -279,3 +279,18 @@ def test_funded_exact_ledger_replay(kme_mod, oracle_mod, kind):
         assert eng.snapshot_books() == o.dump_books()
         assert eng.snapshot_ledger() == o.dump_ledger()
         eng.close()
+
+
+def test_funded_max_resting_is_a_guarantee(kme_mod, oracle_mod):
+    """max_resting resting orders fit however they spread over symbols: the pool adds the slots
+    each group can hold back in its allocation chunk (POOL_CHUNK per group)."""
+    n_sym, P = 256, 1000
+    setup = W.funded_setup(64, range(1, n_sym + 1))
+    stream = W.uniform(P, n_symbols=n_sym, n_accounts=64, seed=11, mix=(1.0, 0.0, 0.0))  # every BUY rests
+    allin = W.Orders.concat([setup, stream])
+    eng = _funded_engine(kme_mod, n_sym + 1, accounts=64, E=1 << 12, P=P)
+    got = _run_epochs(eng, allin, 1 << 12)
+    o = oracle_mod.Oracle()
+    o.process(allin)
+    assert got == o.tape_text()
+    assert eng.snapshot_books() == o.dump_books()
