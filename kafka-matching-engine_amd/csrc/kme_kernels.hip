@@ -1102,6 +1102,8 @@ struct GroupLds {
     int64_t toid[2 * LVP];        // oid of the tail node = OUT.prev of an append (KP:213-217)
     int32_t fstack[FSTK];
     uint32_t dirty[DIRTY_WORDS];
+    uint64_t bmap[4];             // level bitmaps: book +g (lsb, msb), book -g (lsb, msb)
+    int32_t gs[8];                // exists, free-list head block, bump chunk next / end, free-stack top, staged trades
     int4 trd[2 * TRD];            // trade k: (maker oid, maker aid), (price | sid < 0 << 8, size, seq, ord)
 };
 
@@ -1197,10 +1199,7 @@ struct GroupWave {
     const DevState* Sp;           // everything off the per-record path is re-read through cold()
     GroupLds& L;
     const int lane, q;            // q = lane & 3: the node piece this lane loads / stores
-    int32_t g, exists;
-    uint64_t b0l, b0m, b1l, b1m;  // bitmaps of book +g (side 0) and book -g (side 1)
-    int32_t fsp, free_head, chunk_next, chunk_end;
-    int32_t tcnt;                 // trades staged in L.trd
+    int32_t g;
     uint32_t cur;                 // input index of the record being processed
     bool dead;
 #ifdef KME_STAMPS
@@ -1211,9 +1210,6 @@ struct GroupWave {
         : pool(S.pool), rest_slot(S.rest_slot), Sp(&S), L(lds),
           lane(lane_id()),
           q(lane_id() & 3), g(gg) {
-        exists = 0; b0l = b0m = b1l = b1m = 0;
-        fsp = 0; free_head = -1; chunk_next = chunk_end = 0;
-        tcnt = 0;
         cur = 0; dead = false;
         KST(for (int k = 0; k < ST_N; ++k) acc[k] = 0;)
     }
@@ -1229,9 +1225,15 @@ struct GroupWave {
     KDEV KG unsigned long long* ctr() const { return cold().ctr; }
     KDEV KG unsigned long long* tsh() const { return cold().tsh + (size_t)(g & (TSHARDS - 1)) * CTR_STRIDE; }
     KDEV void die(int status, int detail) { raise_wave(ctr(), status, detail, (int64_t)cur); dead = true; }
-    KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
-    KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
-    KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
+    // The level bitmaps live in LDS, not in SGPRs: as loop-carried SSA values they cost a copy per
+    // bitmap at every join of the record loop, and 8 SGPRs of a file that already spills.
+    KDEV uint64_t bl(int side) const { return U64((int64_t)L.bmap[2 * side]); }
+    KDEV uint64_t bm(int side) const { return U64((int64_t)L.bmap[2 * side + 1]); }
+    KDEV void set_bm(int side, uint64_t l, uint64_t m) { L.bmap[2 * side] = l; L.bmap[2 * side + 1] = m; }
+    // so do the group's rarely changing scalars (GroupState words 8..11)
+    enum { GS_EXISTS = 0, GS_FREE_HEAD, GS_CHUNK_NEXT, GS_CHUNK_END, GS_FSP, GS_TCNT };
+    KDEV int32_t gsv(int k) const { return U32(L.gs[k]); }
+    KDEV void set_gs(int k, int32_t v) { L.gs[k] = v; }
     KDEV void sync_lds() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1240,19 +1242,23 @@ struct GroupWave {
     // ---------------- group state in and out
     KDEV void load_group() {
         const int4 v = reinterpret_cast<const KG int4*>(gst())[q];
-        b0l = (uint64_t)mk64(rl32(v.x, 0), rl32(v.y, 0)); b0m = (uint64_t)mk64(rl32(v.z, 0), rl32(v.w, 0));
-        b1l = (uint64_t)mk64(rl32(v.x, 1), rl32(v.y, 1)); b1m = (uint64_t)mk64(rl32(v.z, 1), rl32(v.w, 1));
-        exists = rl32(v.x, 2); free_head = rl32(v.y, 2); chunk_next = rl32(v.z, 2); chunk_end = rl32(v.w, 2);
+        set_bm(0, (uint64_t)mk64(rl32(v.x, 0), rl32(v.y, 0)), (uint64_t)mk64(rl32(v.z, 0), rl32(v.w, 0)));
+        set_bm(1, (uint64_t)mk64(rl32(v.x, 1), rl32(v.y, 1)), (uint64_t)mk64(rl32(v.z, 1), rl32(v.w, 1)));
+        set_gs(GS_EXISTS, rl32(v.x, 2)); set_gs(GS_FREE_HEAD, rl32(v.y, 2));
+        set_gs(GS_CHUNK_NEXT, rl32(v.z, 2)); set_gs(GS_CHUNK_END, rl32(v.w, 2));
+        set_gs(GS_FSP, 0); set_gs(GS_TCNT, 0);
         stage_levels(true);
     }
     KDEV void store_group() {
         stage_levels(false);
+        const int fsp = gsv(GS_FSP);
         if (fsp > 0) spill_blocks(0, fsp);
         const bool q0 = (q & 1) != 0, q1 = (q & 2) != 0;
-        const int32_t x = q1 ? exists : (q0 ? lo32((int64_t)b1l) : lo32((int64_t)b0l));
-        const int32_t y = q1 ? free_head : (q0 ? hi32((int64_t)b1l) : hi32((int64_t)b0l));
-        const int32_t z = q1 ? chunk_next : (q0 ? lo32((int64_t)b1m) : lo32((int64_t)b0m));
-        const int32_t w = q1 ? chunk_end : (q0 ? hi32((int64_t)b1m) : hi32((int64_t)b0m));
+        const uint64_t b0l = bl(0), b0m = bm(0), b1l = bl(1), b1m = bm(1);
+        const int32_t x = q1 ? gsv(GS_EXISTS) : (q0 ? lo32((int64_t)b1l) : lo32((int64_t)b0l));
+        const int32_t y = q1 ? gsv(GS_FREE_HEAD) : (q0 ? hi32((int64_t)b1l) : hi32((int64_t)b0l));
+        const int32_t z = q1 ? gsv(GS_CHUNK_NEXT) : (q0 ? lo32((int64_t)b1m) : lo32((int64_t)b0m));
+        const int32_t w = q1 ? gsv(GS_CHUNK_END) : (q0 ? hi32((int64_t)b1m) : hi32((int64_t)b0m));
         if (lane < 3) reinterpret_cast<KG int4*>(gst())[lane] = make_int4(x, y, z, w);
     }
     // Occupied levels of both books move between HBM (Level, 32 B) and LDS in one parallel pass:
@@ -1291,34 +1297,38 @@ struct GroupWave {
     // word 1 = count, words 2.. = ids; word 14 = Node::live stays 0).  One load refills the stack
     // with a whole block.  Last resort: a chunk of the pool's bump counter.
     KDEV int32_t alloc_slot() {
-        if (fsp > 0) { --fsp; return U32(L.fstack[fsp]); }
-        if (free_head >= 0) {
-            const int32_t blk = free_head;
+        const int fsp = gsv(GS_FSP);
+        if (fsp > 0) { set_gs(GS_FSP, fsp - 1); return U32(L.fstack[fsp - 1]); }
+        const int32_t blk = gsv(GS_FREE_HEAD);
+        if (blk >= 0) {
             const int32_t w = lane < 2 + FBLK - 1 ? reinterpret_cast<const KG int32_t*>(&pool[blk])[lane] : 0;
             const int32_t nxt = rl32(w, 0), cnt = rl32(w, 1);
             if (lane >= 2 && lane < 2 + cnt) L.fstack[lane - 2] = w;
             sync_lds();
-            fsp = cnt;
-            free_head = nxt;
+            set_gs(GS_FSP, cnt);
+            set_gs(GS_FREE_HEAD, nxt);
             return blk;
         }
-        if (chunk_next >= chunk_end) {
+        int32_t cn = gsv(GS_CHUNK_NEXT);
+        if (cn >= gsv(GS_CHUNK_END)) {
             unsigned long long c = 0;
             KG unsigned long long* bump = &ctr()[ci(C_POOL_BUMP)];   // (no asm inside a lane branch)
             if (lane == 0) c = atomicAdd(bump, (unsigned long long)POOL_CHUNK);
             c = bcast64(c);
             if (c + POOL_CHUNK > cold().pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return -1; }
-            chunk_next = (int32_t)c;
-            chunk_end = (int32_t)(c + POOL_CHUNK);
+            cn = (int32_t)c;
+            set_gs(GS_CHUNK_END, (int32_t)(c + POOL_CHUNK));
         }
-        return chunk_next++;
+        set_gs(GS_CHUNK_NEXT, cn + 1);
+        return cn;
     }
     KDEV void free_slot(int32_t s) {
         pool[s].live = 0;
         mark_dirty(s);
-        if (fsp == FSTK) spill_blocks(FSTK - FBLK, FSTK);
+        if (gsv(GS_FSP) == FSTK) spill_blocks(FSTK - FBLK, FSTK);
+        const int fsp = gsv(GS_FSP);
         L.fstack[fsp] = s;
-        ++fsp;
+        set_gs(GS_FSP, fsp + 1);
     }
     // Writes stack entries [b, e) as blocks of FBLK slots (the last slot of each block holds the
     // others' ids), chained onto the group's block list; all lanes in parallel, stores only.
@@ -1326,20 +1336,21 @@ struct GroupWave {
         sync_lds();
         const int n = e - b;
         const int nblk = (n + FBLK - 1) / FBLK;
+        const int32_t fh = gsv(GS_FREE_HEAD);
         for (int k = lane; k < nblk * 14; k += 64) {
             const int blk = k / 14, word = k - blk * 14;
             const int base = b + blk * FBLK;
             const int cnt = imin(FBLK, e - base);                // slots in this block incl. itself
             const int32_t host = L.fstack[base + cnt - 1];
             int32_t v;
-            if (word == 0) v = blk == 0 ? free_head : L.fstack[base - 1];   // previous block's host
+            if (word == 0) v = blk == 0 ? fh : L.fstack[base - 1];   // previous block's host
             else if (word == 1) v = cnt - 1;
             else v = word - 2 < cnt - 1 ? L.fstack[base + word - 2] : -1;
             reinterpret_cast<KG int32_t*>(&pool[host])[word] = v;
         }
         const int lb = b + (nblk - 1) * FBLK;
-        free_head = U32(L.fstack[lb + imin(FBLK, e - lb) - 1]);
-        fsp = b;
+        set_gs(GS_FREE_HEAD, U32(L.fstack[lb + imin(FBLK, e - lb) - 1]));
+        set_gs(GS_FSP, b);
     }
     // Per-batch filter of node slots written since the batch's cancel-target prefetch (this wave
     // is the only writer of its LDS, so a plain read-modify-write by all lanes is exact).
@@ -1372,9 +1383,11 @@ struct GroupWave {
     // to the same address (no bank conflict, no exec mask); in lanes they would pin 8 VGPRs for the
     // whole kernel, one wavefront per SIMD less.
     KDEV void emit(uint32_t ord, const Maker& m, int32_t mprice, int32_t ts) {
+        const int tcnt = gsv(GS_TCNT);
         L.trd[2 * tcnt] = make_int4(lo32(m.oid), hi32(m.oid), lo32(m.aid), hi32(m.aid));
         L.trd[2 * tcnt + 1] = make_int4(mprice | (m.sneg << 8), ts, (int32_t)cur, (int32_t)ord);
-        if (++tcnt == TRD) flush_trades();
+        set_gs(GS_TCNT, tcnt + 1);
+        if (tcnt + 1 == TRD) flush_trades();
     }
     // Reserves tcnt records in the group's shard region through the shard's own counter line.  When
     // the shard is full, the part of the region that reservation got ([base, cap)) is marked as
@@ -1382,6 +1395,7 @@ struct GroupWave {
     // second reservation site inline makes the compiler treat the enclosing loops' exits as
     // divergent and demote their wave-uniform state to VGPRs).
     KDEV void flush_trades() {
+        const int tcnt = gsv(GS_TCNT);
         if (tcnt == 0) return;
         unsigned long long base = 0;
         // (plain loads here: an opaque cold() on this path makes the compiler treat the exits of
@@ -1394,7 +1408,7 @@ struct GroupWave {
         size_t pos = (size_t)tbase + base;
         if (base + (unsigned long long)tcnt > tshard_cap) {
             pos = (size_t)bcast64(trade_overflow(ttmp, Sp->ctr, tbase, tshard_cap, Sp->ttmp_cap, base, (uint32_t)tcnt));
-            if (pos == ~(size_t)0) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); tcnt = 0; return; }
+            if (pos == ~(size_t)0) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); set_gs(GS_TCNT, 0); return; }
         }
         sync_lds();
         if (lane < tcnt) {
@@ -1407,7 +1421,7 @@ struct GroupWave {
             r2[4] = make_int2(b.z, b.w);
         }
         sync_lds();
-        tcnt = 0;
+        set_gs(GS_TCNT, 0);
     }
 
     // ---------------- tryMatch, KP:225-263 (FUNDED: sizes >= 0, prices 0..100)
@@ -1612,7 +1626,7 @@ struct GroupWave {
             KST(acc[ST_VICTIM_WAIT] += stamp() - tw; acc[ST_N_VICTIM] += 1;)
         }
         if (!o.ok) return false;                             // missing, or order.aid != aid (KP:291)
-        if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK); return false; }
+        if (!gsv(GS_EXISTS)) { die(KME_E_DOMAIN, KME_D_NPE_BOOK); return false; }
         const int li = o.side * LVP + o.price;
         if (o.prev < 0 && o.next < 0) {
             uint64_t lo = bl(o.side), hi = bm(o.side);
@@ -1649,11 +1663,11 @@ struct GroupWave {
         bool ok = false;
         switch (r.action) {
         case ADD_SYMBOL:                                    // addSymbol, KP:184-191
-            if (!exists) { exists = 1; b0l = b0m = b1l = b1m = 0; ok = true; }
+            if (!gsv(GS_EXISTS)) { set_gs(GS_EXISTS, 1); set_bm(0, 0, 0); set_bm(1, 0, 0); ok = true; }
             break;
         case REMOVE_SYMBOL:
         case PAYOUT:
-            if (exists) {                                   // removeSymbol, KP:193-198 / removeAllOrders KP:341-353
+            if (gsv(GS_EXISTS)) {                           // removeSymbol, KP:193-198 / removeAllOrders KP:341-353
                 const int s = r.sid < 0 ? 1 : 0;
                 if (bl(s) != 0 || bm(s) != 0) { die(KME_E_DOMAIN, KME_D_HANG); return o; }
             } else {
@@ -1664,7 +1678,7 @@ struct GroupWave {
             break;
         case BUY:
         case SELL: {
-            if (!exists || !r.acct_ok) break;               // books.get(sid) == null / balances.get == null
+            if (!gsv(GS_EXISTS) || !r.acct_ok) break;               // books.get(sid) == null / balances.get == null
             const bool is_buy = r.action == BUY;
             const int os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
             int32_t tsize = r.size;
