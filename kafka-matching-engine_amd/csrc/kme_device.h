@@ -98,7 +98,10 @@ enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2 };
 
 struct DevState {
     int32_t G, mode, A, passes;
-    int32_t ledger_replay, _pad0[3];  // FUNDED + KME_FLAG_EXACT_LEDGER
+    int32_t ledger_replay;            // FUNDED + KME_FLAG_EXACT_LEDGER
+    int32_t light_max;                // FUNDED: groups with at most this many records in the epoch
+                                      // run in k_match_lanes (one lane each); 0 = none
+    int32_t _pad0[2];
     uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
     uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
     KG GroupState* grp;
@@ -126,7 +129,12 @@ struct DevState {
                                       // (price | action << 8, size, sid) for postRemoveAdjustments
     KG int4* prec;                    // FUNDED: packed records, 32 B each (k_route -> k_match):
                                       // w0 = action | price << 8 | acct_ok << 16 | (sid < 0) << 17,
-                                      // size, oid, aid, cancel target (slot | -(j + 2) | -1), 0
+                                      // size, oid, aid, cancel target (slot | -(j + 2) | -1), the
+                                      // target's level (price | side << 8 | 1 << 9; 0 = unknown)
+    KG int4* osort;                   // FUNDED: the OUT echo of the matched records in group-sorted
+                                      // order, 32 B each: (action | has_prev << 16, size, prev),
+                                      // (n_trades, 0, 0, 0); k_unsort puts it in input order
+    KG int32_t* rank;                 // FUNDED: sorted position of input i (last partition pass)
     KG uint32_t* rkeys[2];
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;

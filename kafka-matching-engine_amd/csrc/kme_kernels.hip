@@ -378,7 +378,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= io.n) return;
     const int32_t a = io.action[i];
-    int32_t grp = -1;
+    int32_t grp = -1, vlev = 0;
     int64_t tgt = -1;
     S.rest_slot[i] = -1;
     io.n_trades[i] = 0;
@@ -407,14 +407,26 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         break;
     }
     case CANCEL: {
+        // the target's level (price | side << 8 | 1 << 9) rides along for k_match_lanes, which then
+        // fetches the node and its level in one step (checked against the node there)
         const int64_t oid = io.oid[i];
         const int32_t j = emap_lookup(S, io, oid);
         if (j >= 0 && (uint32_t)j < i) {
-            const int32_t gj = group_of(io.sid[j], S.G);
-            if (gj >= 0) { grp = gj; tgt = -((int64_t)j + 2); }
+            const int64_t sj = io.sid[j];
+            const int32_t gj = group_of(sj, S.G);
+            if (gj >= 0) {
+                grp = gj; tgt = -((int64_t)j + 2);
+                const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
+                vlev = (io.price[j] & 0xFF) | (side << 8) | (1 << 9);
+            }
         } else {
             const int32_t s = otab_lookup(S, oid);
-            if (s >= 0) { grp = S.pool[s].group; tgt = s; }
+            if (s >= 0) {
+                const Node nd = S.pool[s];
+                grp = nd.group; tgt = s;
+                const int side = (nd.sid != 0 && ((nd.sid < 0) != (nd.action != BUY))) ? 1 : 0;
+                vlev = (nd.price & 0xFF) | (side << 8) | (1 << 9);
+            }
         }
         if (grp < 0) { direct = true; ok = false; }                         // orders.get == null (KP:290-291)
         break;
@@ -437,7 +449,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
-        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), (int32_t)tgt, 0);
+        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), (int32_t)tgt, vlev);
     }
 }
 
@@ -502,6 +514,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
             for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][d];
             (dst ? S.rkeys[1] : S.rkeys[0])[pos] = key;
             (dst ? S.rvals[1] : S.rvals[0])[pos] = val;
+            if (pass == S.passes - 1 && S.rank) S.rank[val] = (int32_t)pos;
         }
         __syncthreads();
         for (int q = 0; q < RADIX_PER_T; ++q) {
@@ -1712,7 +1725,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     const int32_t g = blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
-    if (b >= e) return;
+    if (b >= e || e - b <= (uint32_t)S.light_max) return;   // empty, or a light group (k_match_lanes)
     if (failed(S.ctr)) return;
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
@@ -1805,14 +1818,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         }
         n_rest += (uint32_t)__popcll(__ballot(lane < nb && ((o_act >> 16) & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < nb && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
-        if (lane < nb && !w.dead) {
-            const KC EpochIO& io = opaque_const(iop);
-            const uint32_t i = B.i;
-            io.out_action[i] = o_act & 0xFFFF;
-            io.out_size[i] = o_size;
-            io.out_prev[i] = mk64(o_plo, o_phi);
-            io.out_flags[i] = (uint8_t)((o_act >> 16) & KME_OUT_HAS_PREV);
-            io.n_trades[i] = (uint32_t)o_ntr;
+        if (lane < nb && !w.dead) {   // one coalesced 32-B record per lane (k_unsort scatters them)
+            KG int4* os = opaque_const(Sp).osort + 2 * (size_t)k;
+            os[0] = make_int4((o_act & 0xFFFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 16), o_size, o_plo, o_phi);
+            os[1] = make_int4(o_ntr, 0, 0, 0);
         }
     }
     KST(const unsigned long long to0 = stamp();)
@@ -1831,6 +1840,410 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     if (lane == 0)
         for (int q = 0; q < ST_N; ++q) S.dbg[(size_t)g * KME_DBG_WORDS + q] += w.acc[q];
 #endif
+}
+
+// ------------------------------------------------------------------ (2') FUNDED, light groups
+// One LANE per symbol group.  With tens of thousands of groups and a few dozen records each
+// (C3), the wavefront-per-group program is bound by the CU's single scalar issue port: ~150
+// scalar instructions per record, one record at a time per wavefront.  Here 64 groups share one
+// wavefront, each lane running its group's records in arrival order with per-lane (vector)
+// control flow, the book levels read and written in HBM (no LDS staging), the level bitmaps and
+// group scalars in VGPRs.  One vector instruction advances up to 64 groups; the cost is
+// divergence (a step runs every path some lane takes) and one dependent HBM round trip per
+// level / maker access instead of an LDS access.  Groups with more than DevState::light_max
+// records in the epoch stay with k_match (which skips the light ones); both kernels keep the
+// same persistent group format (GroupState, Level, Node, free-slot blocks).
+constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBLK-slot blocks)
+constexpr int LANE_GROUPS = 32;   // groups per wavefront (the other lanes idle): two wavefronts
+                                  // per SIMD at 65,536 groups, so one issues while the other waits
+
+struct GroupLane {
+    const DevState& S;
+    const EpochIO& io;
+    int32_t (*fs)[64];            // fs[k][lane]: free-slot stack entry k of this lane
+    KG unsigned long long* tsh;   // this wavefront's trade shard line
+    uint32_t tbase;
+    int lane;
+    int32_t g;
+    uint64_t b0l, b0m, b1l, b1m;  // level bitmaps of book +g / book -g
+    int32_t exists, free_head, chunk_next, chunk_end, fsp;
+    uint32_t cur;
+    bool dead;
+
+    KDEV GroupLane(const DevState& s, const EpochIO& e, int32_t (*f)[64], int32_t gg)
+        : S(s), io(e), fs(f), tsh(s.tsh + (size_t)(blockIdx.x & (TSHARDS - 1)) * CTR_STRIDE),
+          tbase((blockIdx.x & (TSHARDS - 1)) * s.tshard_cap), lane(lane_id()), g(gg) {
+        b0l = b0m = b1l = b1m = 0;
+        exists = 0; free_head = -1; chunk_next = chunk_end = 0; fsp = 0;
+        cur = 0; dead = false;
+    }
+    KDEV void die(int status, int detail) { raise_thread(S.ctr, status, detail, (int64_t)cur); dead = true; }
+    KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
+    KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
+    KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
+    KDEV KG Level* level(int side, int p) const { return &S.lev[((size_t)g * 2 + side) * NLEV + p]; }
+
+    KDEV void load_group() {
+        const KG int4* gs = reinterpret_cast<const KG int4*>(&S.grp[g]);
+        const int4 a = gs[0], b = gs[1], c = gs[2];
+        b0l = (uint64_t)mk64(a.x, a.y); b0m = (uint64_t)mk64(a.z, a.w);
+        b1l = (uint64_t)mk64(b.x, b.y); b1m = (uint64_t)mk64(b.z, b.w);
+        exists = c.x; free_head = c.y; chunk_next = c.z; chunk_end = c.w;
+    }
+    KDEV void store_group() {
+        while (fsp > 0) spill_block(fsp > FBLK ? fsp - FBLK : 0);
+        KG int4* gs = reinterpret_cast<KG int4*>(&S.grp[g]);
+        gs[0] = make_int4(lo32((int64_t)b0l), hi32((int64_t)b0l), lo32((int64_t)b0m), hi32((int64_t)b0m));
+        gs[1] = make_int4(lo32((int64_t)b1l), hi32((int64_t)b1l), lo32((int64_t)b1m), hi32((int64_t)b1m));
+        gs[2] = make_int4(exists, free_head, chunk_next, chunk_end);
+    }
+
+    // ---------------- node slots (the block format of GroupWave::spill_blocks)
+    // Stack entries [b, fsp) become one block: the last entry hosts the others' ids.
+    KDEV void spill_block(int b) {
+        const int host = fs[fsp - 1][lane];
+        const int cnt = fsp - 1 - b;                        // ids besides the host, <= FBLK - 1
+        int32_t w[16];
+        w[0] = free_head; w[1] = cnt;
+#pragma unroll
+        for (int k = 0; k < FBLK - 1; ++k) w[2 + k] = k < cnt ? fs[b + k][lane] : -1;
+        w[14] = 0; w[15] = 0;                               // Node::live = 0
+        KG int4* d = reinterpret_cast<KG int4*>(&S.pool[host]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = make_int4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        free_head = host;
+        fsp = b;
+    }
+    KDEV int32_t alloc_slot() {
+        if (fsp > 0) return fs[--fsp][lane];
+        if (free_head >= 0) {
+            const int32_t blk = free_head;
+            const KG int4* d = reinterpret_cast<const KG int4*>(&S.pool[blk]);
+            int4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = d[k];
+            const int32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                   v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+            const int32_t cnt = w[1];
+#pragma unroll
+            for (int k = 0; k < FBLK - 1; ++k) if (k < cnt) fs[k][lane] = w[2 + k];
+            fsp = cnt;
+            free_head = w[0];
+            return blk;
+        }
+        if (chunk_next >= chunk_end) {
+            // one bump reservation for every lane of the wavefront that needs a chunk now
+            const unsigned long long need = __ballot(1);
+            const int leader = __ffsll((long long)need) - 1;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1));
+            unsigned long long c = 0;
+            if (lane == leader) c = atomicAdd(&S.ctr[ci(C_POOL_BUMP)], (unsigned long long)POOL_CHUNK * __popcll(need));
+            c = (unsigned long long)__shfl((long long)c, leader) + (unsigned long long)rank * POOL_CHUNK;
+            if (c + POOL_CHUNK > S.pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return -1; }
+            chunk_next = (int32_t)c;
+            chunk_end = (int32_t)(c + POOL_CHUNK);
+        }
+        return chunk_next++;
+    }
+    KDEV void free_slot(int32_t s) {
+        S.pool[s].live = 0;
+        if (fsp == LFS) spill_block(LFS - FBLK);
+        fs[fsp++][lane] = s;
+    }
+
+    // ---------------- trades: one TradeTmp per trade, reserved per wavefront step
+    KDEV void emit(uint32_t ord, int64_t moid, int64_t maid, int32_t msneg, int32_t mprice, int32_t ts) {
+        const unsigned long long act = __ballot(1);
+        const int leader = __ffsll((long long)act) - 1;
+        const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1));
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(&tsh[TS_USED], (unsigned long long)__popcll(act));
+        base = (unsigned long long)__shfl((long long)base, leader) + rank;
+        size_t pos;
+        if (base < S.tshard_cap) {
+            pos = (size_t)tbase + base;
+        } else {
+            const unsigned long long ob = atomicAdd(&S.ctr[ci(C_TTMP)], 1ull);
+            if (ob >= S.ttmp_cap) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); return; }
+            pos = (size_t)TSHARDS * S.tshard_cap + ob;
+        }
+        const int64_t msid = msneg ? -(int64_t)g : (int64_t)g;
+        KG int4* r = reinterpret_cast<KG int4*>(&S.ttmp[pos]);
+        KG int2* r2 = reinterpret_cast<KG int2*>(&S.ttmp[pos]);
+        r[0] = make_int4(lo32(moid), hi32(moid), lo32(maid), hi32(maid));
+        r[1] = make_int4(lo32(msid), hi32(msid), mprice, ts);
+        r2[4] = make_int2((int32_t)cur, (int32_t)ord);
+    }
+
+    // ---------------- tryMatch, KP:225-263: the loop of GroupWave::try_match (no sweep scan), from
+    // the first maker on (its level and node were fetched by the record's first two gathers)
+    KDEV bool try_match(int32_t P, int32_t& tsize, bool is_buy, int os, uint32_t& ntr, int32_t pb, int32_t ms,
+                        int64_t lqty, int4 m0, int4 m1) {
+        KG Level* lv = level(os, pb);
+        bool head_moved = false;
+        for (;;) {
+            const int32_t msz = m1.z, mnext = m1.w;
+            const int32_t ts = imin(tsize, msz);
+            const int32_t msize = jisub(msz, ts);
+            tsize = jisub(tsize, ts);
+            lqty -= ts;
+            emit(ntr++, mk64(m0.x, m0.y), mk64(m0.z, m0.w), m1.y < 0, pb, ts);
+            if (dead) return false;
+            if (msize != 0) {                                // maker stays, partially filled (KP:255-261)
+                S.pool[ms].size = msize;
+                if (head_moved) { lv->head = ms; S.pool[ms].prev = -1; }
+                lv->qty = lqty;
+                return tsize == 0;
+            }
+            free_slot(ms);                                   // maker consumed: orders.delete (KP:243)
+            if (mnext >= 0) {
+                ms = mnext;
+                if (!GroupWave::crosses(is_buy, tsize, pb, P)) {   // stops before the next maker
+                    lv->head = ms;
+                    S.pool[ms].prev = -1;
+                    lv->qty = lqty;
+                    return tsize == 0;
+                }
+                head_moved = true;
+            } else {                                         // level exhausted (KP:244-253)
+                uint64_t lo = bl(os), hi = bm(os);
+                unset_bit(lo, hi, pb);
+                set_bm(os, lo, hi);
+                const int32_t npb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+                const bool go = npb != -1 && check_bit(lo, hi, npb) && GroupWave::crosses(is_buy, tsize, npb, P);
+                if (!go) {
+                    if (npb != -1 && !check_bit(lo, hi, npb)) die(KME_E_DOMAIN, KME_D_NPE_BUCKET);
+                    return tsize == 0;
+                }
+                pb = npb;
+                lv = level(os, pb);
+                ms = lv->head;
+                lqty = lv->qty;
+                if (ms < 0) { die(KME_E_DOMAIN, KME_D_NPE_ORDER); return false; }
+                head_moved = false;
+            }
+            m0 = reinterpret_cast<const KG int4*>(&S.pool[ms])[0];
+            m1 = reinterpret_cast<const KG int4*>(&S.pool[ms])[1];
+        }
+    }
+
+    // ---------------- addOrder, KP:200-223 (own: the level at the order's price, when prefetched)
+    KDEV void rest(const Rec& r, int32_t tsize, Out& o, bool own_pre, int4 l0, int4 l1) {
+        const int s = book_side(r.sid, r.action == BUY);
+        uint64_t lo = bl(s), hi = bm(s);
+        const int32_t p = r.price;
+        const int32_t slot = alloc_slot();
+        if (dead) return;
+        KG Level* lv = level(s, p);
+        int32_t nprev = -1;
+        int64_t poid = 0;
+        if (!check_bit(lo, hi, p)) {                         // new bucket (KP:209-211)
+            reinterpret_cast<KG int4*>(lv)[0] = make_int4(slot, slot, 0, 0);
+            reinterpret_cast<KG int4*>(lv)[1] = make_int4((int32_t)tsize, tsize < 0 ? -1 : 0, lo32(r.oid), hi32(r.oid));
+            set_bit(lo, hi, p);
+            set_bm(s, lo, hi);
+        } else {                                             // append at the tail (KP:213-219)
+            if (!own_pre) { l0 = reinterpret_cast<const KG int4*>(lv)[0]; l1 = reinterpret_cast<const KG int4*>(lv)[1]; }
+            nprev = l0.y;
+            poid = mk64(l1.z, l1.w);
+            const int64_t q = mk64(l1.x, l1.y) + tsize;
+            S.pool[nprev].next = slot;
+            lv->tail = slot;
+            reinterpret_cast<KG int4*>(lv)[1] = make_int4(lo32(q), hi32(q), lo32(r.oid), hi32(r.oid));
+            o.has_prev = true;
+            o.prev = poid;
+        }
+        KG int4* nd = reinterpret_cast<KG int4*>(&S.pool[slot]);
+        nd[0] = make_int4(lo32(r.oid), hi32(r.oid), lo32(r.aid), hi32(r.aid));
+        nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
+        nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
+        nd[3] = make_int4(p, r.action, 1, 0);
+        S.rest_slot[r.i] = slot;
+        o.rested = true;
+    }
+
+    // ---------------- removeOrder, KP:289-323 (victim node c0..c3; vl1: its level's qty words when
+    // k_route knew the level, vlev = price | side << 8 | 1 << 9)
+    KDEV bool cancel(const Rec& r, int32_t slot, int4 c0, int4 c1, int4 c2, int4 c3, int32_t vlev, int4 vl1) {
+        if (slot < 0) return false;                          // orders.get(oid) == null
+        if (!(c3.z != 0 && mk64(c0.x, c0.y) == r.oid && mk64(c0.z, c0.w) == r.aid)) return false;   // KP:291
+        if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK); return false; }
+        const int32_t action = c3.y, price = c3.x, size = c1.z, next = c1.w, prev = c2.z;
+        const int64_t prev_oid = mk64(c2.x, c2.y);
+        const int side = book_side(mk64(c1.x, c1.y), action == BUY);
+        KG Level* lv = level(side, price);
+        if (prev < 0 && next < 0) {
+            uint64_t lo = bl(side), hi = bm(side);
+            unset_bit(lo, hi, price);
+            set_bm(side, lo, hi);
+        } else {
+            if (prev < 0) {
+                lv->head = next;
+                S.pool[next].prev = -1;
+            } else if (next < 0) {
+                lv->tail = prev;
+                lv->tail_oid = prev_oid;
+                S.pool[prev].next = -1;
+            } else {
+                S.pool[prev].next = next;
+                S.pool[next].prev = prev;
+                S.pool[next].prev_oid = prev_oid;
+            }
+            const int64_t q = vlev == (price | (side << 8) | (1 << 9)) ? mk64(vl1.x, vl1.y) : lv->qty;
+            lv->qty = q - size;
+        }
+        free_slot(slot);
+        if (S.ledger_replay)   // the removed order, for postRemoveAdjustments in k_ledger_replay
+            S.vic[r.i] = make_int4(price | ((action == SELL ? SELL : BUY) << 8), size, c1.y < 0 ? -g : g, c1.y < 0 ? -1 : 0);
+        return !dead;
+    }
+};
+
+// The records of the 64 groups run in lock step, one record per lane per step.  A step's loads
+// are issued in two gathers shared by every record type (first: the taker's best opposite level,
+// a resting order's own level, a cancel's target node or rest slot and its level; second: the
+// taker's first maker, a same-epoch cancel's node), so the round trips of a step are ~2 plus the
+// makers beyond the first, not the sum of every path's chain.
+__global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
+    __shared__ int32_t fs[LFS][64];
+    const DevState& S = *Sp;
+    const EpochIO& io = *iop;
+    if (failed(S.ctr)) return;
+    const int32_t g = (int32_t)(blockIdx.x * LANE_GROUPS + lane_id());
+    uint32_t b = 0, e = 0;
+    if (lane_id() < LANE_GROUPS && g < S.G) { b = S.seg[g]; e = S.seg[g + 1]; }
+    if (e - b > (uint32_t)S.light_max) e = b;                // a heavy group: k_match's
+    uint32_t n_rest = 0, n_cancel = 0;
+    if (b < e) {
+        GroupLane w(S, io, fs, g);
+        w.load_group();
+        const KG uint32_t* perm = buf ? S.rvals[1] : S.rvals[0];
+        // records are fetched one step ahead (their input indices two ahead), before the step's
+        // stores: a load waits for every older vector memory operation (vmcnt is in order on gfx9)
+        uint32_t i_next = perm[b];
+        uint32_t i_after = b + 1 < e ? perm[b + 1] : 0;
+        int4 n0 = S.prec[2 * (size_t)i_next], n1 = S.prec[2 * (size_t)i_next + 1];
+        const int4 z = make_int4(0, 0, 0, 0);
+        for (uint32_t k = b; k < e && !w.dead; ++k) {
+            Rec r;
+            r.i = i_next;
+            const int4 p0 = n0, p1 = n1;
+            if (k + 1 < e) {
+                i_next = i_after;
+                n0 = S.prec[2 * (size_t)i_next]; n1 = S.prec[2 * (size_t)i_next + 1];
+                i_after = k + 2 < e ? perm[k + 2] : 0;
+            }
+            r.action = p0.x & 0xFF;
+            r.price = (p0.x >> 8) & 0xFF;
+            r.acct_ok = (p0.x >> 16) & 1;
+            r.sid = (p0.x >> 17) & 1 ? -(int64_t)g : (int64_t)g;
+            r.size = p0.y;
+            r.oid = mk64(p0.z, p0.w); r.aid = mk64(p1.x, p1.y); r.tgt = (int64_t)p1.z;
+            r.lane = 0;
+            const int32_t vlev = p1.w;
+            w.cur = r.i;
+            Out o;
+            o.action = r.action; o.size = r.size; o.prev = 0; o.has_prev = false; o.rested = false; o.ntr = 0;
+            bool ok = false;
+            const bool order = (r.action == BUY || r.action == SELL) && w.exists && r.acct_ok;
+            const bool cxl = r.action == CANCEL;
+            // ---- what the record reads first (MatchingEngine.process, KP:96-126)
+            bool is_buy = r.action == BUY, tm = false, filled = false, own_pre = false;
+            int os = 0;
+            int32_t pb = -1, tsize = r.size;
+            if (order) {
+                os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
+                const uint64_t lo = w.bl(os), hi = w.bm(os);
+                pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+                if (pb != -1) {
+                    if (!check_bit(lo, hi, pb)) w.die(KME_E_DOMAIN, KME_D_NPE_BUCKET);
+                    else if (GroupWave::crosses(is_buy, tsize, pb, r.price)) tm = true;
+                    else filled = tsize == 0;
+                }
+                const int s = book_side(r.sid, is_buy);      // the order's own level, unless sid 0 (one
+                own_pre = g != 0 && check_bit(w.bl(s), w.bm(s), r.price);   // book: the sweep may change it)
+            }
+            const KG int4* la = nullptr;                     // a level: the taker's, or the cancel target's
+            if (tm) la = reinterpret_cast<const KG int4*>(w.level(os, pb));
+            else if (cxl && ((vlev >> 9) & 1)) la = reinterpret_cast<const KG int4*>(w.level((vlev >> 8) & 1, vlev & 0xFF));
+            int4 la0 = z, la1 = z, lo0 = z, lo1 = z, c0 = z, c1 = z, c2 = z, c3 = z;
+            int32_t vslot = -1;
+            // ---- first gather
+            if (la) { la0 = la[0]; la1 = la[1]; }
+            if (own_pre) {
+                const KG int4* lp = reinterpret_cast<const KG int4*>(w.level(book_side(r.sid, is_buy), r.price));
+                lo0 = lp[0]; lo1 = lp[1];
+            }
+            if (cxl) {
+                if (r.tgt >= 0) {
+                    vslot = (int32_t)r.tgt;
+                    const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
+                    c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
+                } else if (r.tgt <= -2) {
+                    vslot = S.rest_slot[-(r.tgt + 2)];
+                }
+            }
+            // ---- second gather
+            int32_t ms = -1;
+            int64_t lqty = 0;
+            int4 m0 = z, m1 = z;
+            if (tm) {
+                ms = la0.x;
+                lqty = mk64(la1.x, la1.y);
+                if (ms < 0) { w.die(KME_E_DOMAIN, KME_D_NPE_ORDER); tm = false; }
+                else { const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[ms]); m0 = nd[0]; m1 = nd[1]; }
+            }
+            if (cxl && r.tgt <= -2 && vslot >= 0) {
+                const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
+                c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
+            }
+            if (w.dead) break;
+            // ---- the record
+            if (order) {
+                uint32_t ntr = 0;
+                if (tm) filled = w.try_match(r.price, tsize, is_buy, os, ntr, pb, ms, lqty, m0, m1);
+                o.ntr = ntr;
+                if (w.dead) break;
+                if (!filled) { w.rest(r, tsize, o, own_pre, lo0, lo1); if (w.dead) break; }
+                ok = true;
+                o.size = tsize;
+            } else if (cxl) {
+                ok = w.cancel(r, vslot, c0, c1, c2, c3, vlev, la1);
+                if (w.dead) break;
+            } else if (r.action == ADD_SYMBOL) {             // addSymbol, KP:184-191
+                if (!w.exists) { w.exists = 1; w.b0l = w.b0m = w.b1l = w.b1m = 0; ok = true; }
+            } else if (r.action == REMOVE_SYMBOL || r.action == PAYOUT) {   // KP:193-198 / 341-353
+                if (w.exists) {
+                    const int s = r.sid < 0 ? 1 : 0;
+                    if (w.bl(s) != 0 || w.bm(s) != 0) { w.die(KME_E_DOMAIN, KME_D_HANG); break; }
+                } else {
+                    ok = r.action == REMOVE_SYMBOL;
+                    if (r.action == PAYOUT) { w.die(KME_E_UNSUPPORTED, KME_D_NONE); break; }
+                }
+                if (r.action == PAYOUT) ok = false;
+            }                                                // BUY / SELL without book or balance: REJECT
+            o.action = ok ? r.action : (int32_t)REJECT;
+            {   // the OUT echo in sorted order: this lane's writes walk consecutive lines
+                const int64_t pv = o.has_prev ? o.prev : 0;
+                KG int4* os = S.osort + 2 * (size_t)k;
+                os[0] = make_int4((o.action & 0xFFFF) | ((o.has_prev ? KME_OUT_HAS_PREV : 0) << 16), o.size, lo32(pv), hi32(pv));
+                os[1] = make_int4((int32_t)o.ntr, 0, 0, 0);
+            }
+            n_rest += o.rested ? 1u : 0u;
+            n_cancel += (cxl && ok) ? 1u : 0u;
+        }
+        w.store_group();
+    }
+    // per-wavefront sums onto the shard line (k_tsh_fold adds the lines up)
+    for (int off = 32; off > 0; off >>= 1) {
+        n_rest += (uint32_t)__shfl_xor((int)n_rest, off);
+        n_cancel += (uint32_t)__shfl_xor((int)n_cancel, off);
+    }
+    if (lane_id() == 0) {
+        KG unsigned long long* tsh = S.tsh + (size_t)(blockIdx.x & (TSHARDS - 1)) * CTR_STRIDE;
+        if (n_rest) atomicAdd(&tsh[TS_RESTS], (unsigned long long)n_rest);
+        if (n_cancel) atomicAdd(&tsh[TS_CANCELS], (unsigned long long)n_cancel);
+    }
 }
 
 // EXACT: one wavefront, the whole epoch in arrival order, every store exact.
@@ -1957,12 +2370,33 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
     }
 }
 
+// ------------------------------------------------------------------ (3') OUT echo to input order
+// The matching kernels leave each record's OUT echo in group-sorted order (coalesced / sequential
+// lines); here every input takes its own from position rank[i]: one random 32-B read per matched
+// record instead of five random partial-line writes (the C ABI's SoA arrays) in the matching loop.
+// Records without a symbol group were answered by k_route / k_ledger_funded already.
+__global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
+    if (failed(S.ctr)) return;   // a failed epoch: route's zero trade counts stay (k_scatter stays in bounds)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
+        if (S.route_grp[i] < 0) continue;
+        const KG int4* os = S.osort + 2 * (size_t)S.rank[i];
+        const int4 a = os[0];
+        const int32_t ntr = os[1].x;
+        io.out_action[i] = a.x & 0xFFFF;
+        io.out_flags[i] = (uint8_t)((a.x >> 16) & KME_OUT_HAS_PREV);
+        io.out_size[i] = a.y;
+        io.out_prev[i] = mk64(a.z, a.w);
+        io.n_trades[i] = (uint32_t)ntr;
+    }
+}
+
 // ------------------------------------------------------------------ (4) compaction
 // Blocks (s, *) with s < TSHARDS move shard s's trades, blocks (TSHARDS, *) the overflow
 // region's, each to trades[trade_off[seq] + ord] (arrival order).
 constexpr uint32_t SCATTER_SUB = 8;   // blocks per shard region
 __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const uint32_t* total) {
     const uint32_t s = blockIdx.x;
+    if (failed(S.ctr)) return;
     const bool fits = *total <= io.trades_cap;
     if (s == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (!fits) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, -1);
@@ -2115,8 +2549,11 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf);
+    if (S.light_max > 0)
+        hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);
 }
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
+    if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);
     // trade_off[0..n] = exclusive scan of n_trades; bsum/total scratch in ghist
     uint32_t* bsum = S.ghist;
     const uint32_t nb = cdiv(io.n > 0 ? io.n : 1, SCAN_BLOCK);

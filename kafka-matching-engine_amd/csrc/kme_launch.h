@@ -9,6 +9,7 @@ namespace kme {
 constexpr int RADIX_TILE = 4096;     // inputs per partition tile (256 threads x 16)
 constexpr int RADIX_BITS = 9;        // digit width of the partition passes
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
+constexpr int kDefaultLightMax = 0;  // DevState::light_max default (KME_LIGHT_MAX overrides)
 
 // FUNDED pipeline
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);

@@ -190,6 +190,10 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.otab, e->otab_cap);
     const bool exact_ledger = !funded || (cfg->flags & KME_FLAG_EXACT_LEDGER);
     S.ledger_replay = funded && exact_ledger ? 1 : 0;
+    // FUNDED groups with at most light_max records in an epoch are matched one lane per group
+    // (k_match_lanes), the others one wavefront per group (k_match); KME_LIGHT_MAX overrides.
+    S.light_max = funded ? kDefaultLightMax : 0;
+    if (const char* v = std::getenv("KME_LIGHT_MAX")) S.light_max = funded ? std::max(0, std::atoi(v)) : 0;
     if (funded) {
         ALLOC(S.acct_since, cfg->max_accounts);
         ALLOC(S.acct_lb, cfg->max_accounts);
@@ -215,6 +219,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
     if (funded) ALLOC(S.prec, 2 * (size_t)E);
+    if (funded) ALLOC(S.osort, 2 * (size_t)E);
+    if (funded) ALLOC(S.rank, E);
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
         ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);

@@ -10,5 +10,5 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -I../../include -I. --offload-device
   | grep -A11 "Name: _ZN3kme7k_match" | grep -E "SGPRs:|VGPRs:|Occupancy|Spill|LDS Size" | sed 's/.*remark: *//'
 /opt/rocm/bin/hipcc $FLAGS -emit-llvm -S $F -o /tmp/kme_chk.ll 2>/dev/null
 /opt/rocm/lib/llvm/bin/opt -passes='print<uniformity>' -disable-output /tmp/kme_chk.ll 2>&1 \
-  | awk '/UniformityInfo for function .*k_match/{f=1;next} /UniformityInfo for function/{f=0} f' \
+  | awk '/UniformityInfo for function .*_ZN3kme7k_matchE/{f=1;next} /UniformityInfo for function/{f=0} f' \
   | awk '/CYCLES WITH DIVERGENT EXIT/{f=1;print;next} /^$/{f=0} f' | cut -c1-100
