@@ -2549,8 +2549,9 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf);
-    if (S.light_max > 0)
-        hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);
+}
+void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
+    hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);
 }
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);

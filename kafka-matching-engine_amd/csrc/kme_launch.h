@@ -9,7 +9,7 @@ namespace kme {
 constexpr int RADIX_TILE = 4096;     // inputs per partition tile (256 threads x 16)
 constexpr int RADIX_BITS = 9;        // digit width of the partition passes
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
-constexpr int kDefaultLightMax = 0;  // DevState::light_max default (KME_LIGHT_MAX overrides)
+constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT_MAX overrides)
 
 // FUNDED pipeline
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);
@@ -19,6 +19,8 @@ void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t
 // returns the buffer index (0/1) holding the sorted input permutation
 int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st);
+// light groups (at most S.light_max records in the epoch), one lane each; independent of k_match
+void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st);
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
 // EXACT pipeline (emap + route shared)

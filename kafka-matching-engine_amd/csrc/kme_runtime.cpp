@@ -38,6 +38,8 @@ struct kme_engine {
     kme_config cfg{};
     int device = 0;
     hipStream_t own_stream = nullptr;
+    hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t stream = nullptr;
     DevState S{};
     DevState* d_S = nullptr;
@@ -152,6 +154,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     e->device = cfg->device;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->lane_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
     e->stream = e->own_stream;
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
 
@@ -280,6 +285,9 @@ kme_status kme_destroy(kme_engine* e) {
     if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
     for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    if (e->lane_stream) (void)hipStreamDestroy(e->lane_stream);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
     return KME_OK;
 }
@@ -344,7 +352,14 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         const int buf = launch_partition(S, io, st);
         phase_end(e, PH_PART);
         phase_begin(e, PH_MATCH);
+        if (S.light_max > 0) {   // light groups one lane each, concurrently with k_match's heavy ones
+            HIP_TRY(hipEventRecord(e->ev_fork, st));
+            HIP_TRY(hipStreamWaitEvent(e->lane_stream, e->ev_fork, 0));
+            launch_match_lanes(S, e->d_S, e->d_io, buf, e->lane_stream);
+            HIP_TRY(hipEventRecord(e->ev_join, e->lane_stream));
+        }
         launch_match(S, e->d_S, e->d_io, buf, st);
+        if (S.light_max > 0) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);
         launch_compact(S, io, st);

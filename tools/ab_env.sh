@@ -9,7 +9,7 @@ env $ENVSET timeout -k 10 300 python3 -u -m pytest tests -m gpu -q -x --timeout 
 rc=$?; echo "tests [$ENVSET] rc=$rc"; tail -3 gpurun_out/ab/tests.log
 [ $rc -eq 0 ] || exit $rc
 for args in "$@"; do
-  for E in "" "$ENVSET" "" "$ENVSET"; do
+  for E in ${AB_ORDER:-"" "$ENVSET" "" "$ENVSET"}; do
     env $E timeout -k 10 200 python3 bench.py --no-cpu-baseline $args > gpurun_out/ab/one.json 2>gpurun_out/ab/err.log || { tail -3 gpurun_out/ab/err.log; exit 1; }
     python3 -c "import json;d=json.load(open('gpurun_out/ab/one.json'));print('[$E]', '$args', round(d['value']/1e6,1), d['phase_ms_last_epoch']['match'])"
   done
