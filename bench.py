@@ -251,7 +251,8 @@ def main():
             "trades_per_s": n_trades_all / elapsed,
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
-            "roofline": {"kernel": "k_match", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "
+                                   "one wavefront each, concurrent)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",
                          "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg))},

@@ -98,7 +98,11 @@ typedef struct kme_config {
                                   floor(credit / n) and ceil(debit / n), so the shards' reservations
                                   together never exceed the account's cash. */
     uint32_t flags;            /* KME_FLAG_* */
-    uint32_t _reserved;
+    int32_t light_max;         /* FUNDED: a symbol group with at most this many records in an epoch is
+                                  matched by one lane of a wavefront shared with 31 other groups
+                                  (k_match_lanes), a busier one by a whole wavefront (k_match); both
+                                  run concurrently.  0 = engine default (128), < 0 = wavefronts only.
+                                  Results are identical either way. */
 } kme_config;
 
 /* One epoch of input records, structure-of-arrays (Order fields KP:451-456).  The reference's

@@ -197,8 +197,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.ledger_replay = funded && exact_ledger ? 1 : 0;
     // FUNDED groups with at most light_max records in an epoch are matched one lane per group
     // (k_match_lanes), the others one wavefront per group (k_match); KME_LIGHT_MAX overrides.
-    S.light_max = funded ? kDefaultLightMax : 0;
-    if (const char* v = std::getenv("KME_LIGHT_MAX")) S.light_max = funded ? std::max(0, std::atoi(v)) : 0;
+    int32_t lm = cfg->light_max == 0 ? kDefaultLightMax : std::max(0, (int32_t)cfg->light_max);
+    if (const char* v = std::getenv("KME_LIGHT_MAX")) lm = std::max(0, std::atoi(v));   // diagnostics
+    S.light_max = funded ? lm : 0;
     if (funded) {
         ALLOC(S.acct_since, cfg->max_accounts);
         ALLOC(S.acct_lb, cfg->max_accounts);

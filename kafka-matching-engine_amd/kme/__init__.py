@@ -39,7 +39,7 @@ class kme_config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("mode", C.c_uint32), ("max_symbols", C.c_uint32),
                 ("max_accounts", C.c_uint32), ("max_epoch", C.c_uint32), ("max_trades", C.c_uint32),
                 ("max_resting", C.c_uint64), ("ledger_capacity", C.c_uint64), ("device", C.c_int32),
-                ("credit_shards", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32)]
+                ("credit_shards", C.c_uint32), ("flags", C.c_uint32), ("light_max", C.c_int32)]
 
 
 class kme_orders(C.Structure):
@@ -191,10 +191,10 @@ class EpochResult:
 
 def default_config(mode: int, max_symbols: int, max_epoch: int, max_resting: int, max_trades: int | None = None,
                    max_accounts: int = 0, ledger_capacity: int = 1 << 16, device: int = 0,
-                   flags: int = 0) -> kme_config:
+                   flags: int = 0, light_max: int = 0) -> kme_config:
     return kme_config(ABI_VERSION, mode, max_symbols, max_accounts, max_epoch,
                       max_trades if max_trades is not None else max(4 * max_epoch, 1 << 16),
-                      max_resting, ledger_capacity, device, 0, flags, 0)
+                      max_resting, ledger_capacity, device, 0, flags, light_max)
 
 
 class Engine:

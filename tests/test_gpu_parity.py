@@ -12,9 +12,9 @@ from kme import workloads as W
 pytestmark = pytest.mark.gpu
 
 
-def _funded_engine(kme, G, accounts=4096, E=1 << 16, P=1 << 18):
+def _funded_engine(kme, G, accounts=4096, E=1 << 16, P=1 << 18, light_max=0):
     return kme.Engine(kme.default_config(kme.MODE_FUNDED, max_symbols=G, max_epoch=E, max_resting=P,
-                                         max_accounts=accounts))
+                                         max_accounts=accounts, light_max=light_max))
 
 
 def _exact_engine(kme, G=16, E=1 << 16, P=1 << 16):
@@ -294,3 +294,57 @@ def test_funded_max_resting_is_a_guarantee(kme_mod, oracle_mod):
     o.process(allin)
     assert got == o.tape_text()
     assert eng.snapshot_books() == o.dump_books()
+
+
+# light_max: -1 = one wavefront per group only (k_match), 1 << 30 = one lane per group only
+# (k_match_lanes), 40 = both kernels in the same epoch (concurrently, on disjoint groups)
+LIGHT = [-1, 1 << 30, 40]
+
+
+@pytest.mark.parametrize("light_max", LIGHT)
+@pytest.mark.parametrize("kind", ["uniform", "zipf", "cancel_replace"])
+def test_funded_matching_paths_agree(kme_mod, oracle_mod, kind, light_max):
+    """Both matching kernels, alone and together, give the reference's tape and books."""
+    n_sym, n_acc = 256, 512
+    if kind == "uniform":
+        stream = W.uniform(30_000, n_symbols=n_sym, n_accounts=n_acc, seed=21)
+    elif kind == "zipf":
+        stream = W.zipf(30_000, n_symbols=n_sym, n_accounts=n_acc, seed=22)
+    else:
+        stream = W.cancel_replace(12_000, n_symbols=n_sym, n_accounts=n_acc, seed=23)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1),
+                           transfers_per_account=W.funded_transfers_needed(len(stream), n_acc, big=kind == "cancel_replace"))
+    allin = W.Orders.concat([setup, stream])
+    eng = _funded_engine(kme_mod, n_sym + 1, accounts=n_acc, light_max=light_max)
+    got = _run_epochs(eng, allin, 8192)
+    o = oracle_mod.Oracle()
+    o.process(allin)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+
+
+@pytest.mark.parametrize("light_max", LIGHT)
+@pytest.mark.parametrize("name", sorted(hazards.FUNDED_OK))
+def test_funded_hazards_both_paths(kme_mod, oracle_mod, name, light_max):
+    orders = hazards.as_orders(hazards.streams()[name])
+    eng = _funded_engine(kme_mod, 8, accounts=16, E=1024, P=4096, light_max=light_max)
+    got = _run_epochs(eng, orders, 1024)
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+
+
+@pytest.mark.parametrize("light_max", [-1, 1 << 30])
+@pytest.mark.parametrize("name", sorted(n for n in hazards.domain_streams() if n != "price_126"))
+def test_funded_domain_errors_both_paths(kme_mod, oracle_mod, name, light_max):
+    rows, detail = hazards.domain_streams()[name]
+    orders = hazards.as_orders(rows)
+    o = oracle_mod.Oracle()
+    with pytest.raises(oracle_mod.OracleError) as oe:
+        o.process(orders)
+    eng = _funded_engine(kme_mod, 8, 16, 1024, 4096, light_max=light_max)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        _run_epochs(eng, orders, 1024)
+    assert ke.value.status == 3 and ke.value.detail == detail
+    assert ke.value.index == oe.value.index

@@ -23,9 +23,10 @@ def counters(d, kernel_re):
                 if not re.search(kernel_re, row.get("Kernel_Name", "")):
                     continue
                 name = row["Counter_Name"]
+                kern = row.get("Kernel_Name", "").split("(")[0]
                 disp = int(row.get("Dispatch_Id", 0))
-                vals.setdefault(name, {}).setdefault(disp, 0.0)
-                vals[name][disp] += float(row["Counter_Value"])
+                vals.setdefault(name, {}).setdefault(kern, {}).setdefault(disp, 0.0)
+                vals[name][kern][disp] += float(row["Counter_Value"])
     return vals
 
 
@@ -38,10 +39,17 @@ def main():
             for k, v in counters(sub, kre).items():
                 allv[k] = v
     res = {"kernel_regex": kre, "source": os.path.relpath(d)}
-    for k, per in sorted(allv.items()):
-        xs = [per[i] for i in sorted(per)][skip:]
-        if xs:
-            res[k] = {"mean_per_dispatch": sum(xs) / len(xs), "dispatches": len(xs)}
+    # several kernels may match (k_match and k_match_lanes both run once per epoch): the figure per
+    # epoch ("per launch" of the match phase) is the sum of each kernel's mean per dispatch
+    for k, kerns in sorted(allv.items()):
+        tot, per_kernel = 0.0, {}
+        for kern, per in sorted(kerns.items()):
+            xs = [per[i] for i in sorted(per)][skip:]
+            if xs:
+                per_kernel[kern] = sum(xs) / len(xs)
+                tot += per_kernel[kern]
+        if per_kernel:
+            res[k] = {"mean_per_dispatch": tot, "per_kernel": per_kernel}
     f = res.get("FETCH_SIZE", {}).get("mean_per_dispatch")
     w = res.get("WRITE_SIZE", {}).get("mean_per_dispatch")
     if f is not None and w is not None:
