@@ -11,6 +11,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -2 $OUT/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; echo "smoke_rc=$rc"; tail -1 $OUT/smoke.log
+[ $rc -eq 0 ] || exit $rc
 bash tools/pmc_kmatch.sh $TAG/pmc k_match "$@" || exit $?
 cp $OUT/pmc/pmc_summary.json profiles/pmc_k_match_c3.json
 timeout -k 10 500 python3 -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
@@ -19,7 +22,7 @@ rc=$?; echo "bench_rc=$rc"; cat $OUT/bench.json; tail -2 $OUT/bench.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/prof.log 2>&1
 rc=$?; echo "prof_rc=$rc"
 [ $rc -eq 0 ] || exit $rc
-for extra in "--workload c3 --symbols 8192" "--workload c2" "--workload c2 --epoch 1048576"; do
+for extra in "--workload c3 --symbols 32768" "--workload c3 --symbols 8192" "--workload c2" "--workload c4 --steps 4 --warmup 1"; do
   timeout -k 10 300 python3 -u bench.py --no-cpu-baseline $extra >> $OUT/bench_extra.jsonl 2>> $OUT/bench_extra.err
   rc=$?; echo "extra [$extra] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
