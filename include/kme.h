@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 2
+#define KME_ABI_VERSION 3
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -81,6 +81,13 @@ enum kme_mode { KME_MODE_EXACT = 0, KME_MODE_FUNDED = 1 };
  *   final ledger stores are bit-exact too (kme_snapshot_ledger).  The replay is a serial chain:
  *   it costs far more than the matching it follows. */
 #define KME_FLAG_EXACT_LEDGER 1u
+/* KME_FLAG_SERIAL_FALLBACK (FUNDED, requires KME_FLAG_EXACT_LEDGER; SURVEY §8 row f next-2, the
+ *   validate-and-replay relaxation): an epoch whose funded proof fails -- some checkBalance
+ *   (KP:177) or transfer debit (KP:142) might reject -- is not refused with KME_E_UNFUNDED but
+ *   matched by the serial EXACT engine on the exact ledger (every reject as in the reference), after
+ *   which the funded bounds restart from the exact balances.  kme_epoch_status.serial_fallback
+ *   tells which epochs took that path. */
+#define KME_FLAG_SERIAL_FALLBACK 2u
 
 typedef struct kme_config {
     uint32_t abi_version;      /* KME_ABI_VERSION */
@@ -148,6 +155,9 @@ typedef struct kme_epoch_status {
     uint32_t n_trades;
     uint64_t n_orders;     /* BUY/SELL/CANCEL records (headline metric unit) */
     uint64_t n_rests, n_maker_visits, n_cancel_ok;
+    uint32_t serial_fallback;   /* epochs (device sub-epochs of kme_submit_epoch) that ran serially
+                                   under KME_FLAG_SERIAL_FALLBACK */
+    uint32_t _pad;
 } kme_epoch_status;
 
 typedef struct kme_engine kme_engine;

@@ -85,6 +85,7 @@ enum Ctr : int {
     C_OTAB_USED,       // non-empty oid-table slots
     C_ACCT_OPS,        // FUNDED: account records in the epoch
     C_BAL_USED, C_POS_USED,
+    C_FALLBACK,        // FUNDED + KME_FLAG_SERIAL_FALLBACK: nonzero = this epoch runs serially
     C_NCTR = 16
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
@@ -101,7 +102,8 @@ struct DevState {
     int32_t ledger_replay;            // FUNDED + KME_FLAG_EXACT_LEDGER
     int32_t light_max;                // FUNDED: groups with at most this many records in the epoch
                                       // run in k_match_lanes (one lane each); 0 = none
-    int32_t _pad0[2];
+    int32_t fallback;                 // KME_FLAG_SERIAL_FALLBACK
+    int32_t _pad0;
     uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
     uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
     KG GroupState* grp;

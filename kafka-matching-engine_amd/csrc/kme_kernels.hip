@@ -345,7 +345,8 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
                         S.acct_xfer[aid] += share;
                         if (share < 0) S.acct_negx[aid] -= share;
                     } else {
-                        raise_wave(S.ctr, KME_E_UNFUNDED, KME_D_NONE, j);
+                        if (S.fallback) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull);   // the epoch runs serially
+                        else raise_wave(S.ctr, KME_E_UNFUNDED, KME_D_NONE, j);
                         return;
                     }
                 }
@@ -366,7 +367,10 @@ __global__ void k_check_funded(DevState S, EpochIO io) {
     if (need == 0 && negx == 0 && xfer == 0) return;
     const int64_t since = S.acct_since[a];
     const int64_t lbs = since < io.seq_base ? S.acct_lb[a] : 0;
-    if (need > 0 && lbs - need - negx < 0) raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_NONE, -1);
+    if (need > 0 && lbs - need - negx < 0) {
+        if (S.fallback) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull);   // k_serial takes the epoch
+        else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_NONE, -1);
+    }
     if (since < io.seq_base + (int64_t)io.n) S.acct_lb[a] = lbs - need + xfer;
     S.acct_need[a] = 0; S.acct_negx[a] = 0; S.acct_xfer[a] = 0;
 }
@@ -439,10 +443,8 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         break;
     }
     S.route_grp[i] = grp;
-    if (!funded) {
-        S.cancel_tgt[i] = tgt;
-        return;
-    }
+    if (!funded || S.fallback) S.cancel_tgt[i] = tgt;   // k_serial's cancel target
+    if (!funded) return;
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
     if (grp >= 0) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
@@ -627,6 +629,8 @@ struct Taker {
 // EXACT mode (k_serial): the whole epoch in arrival order on one wavefront, every store -- the
 // book stores and the Balances / Positions ledger -- exact.  The current symbol group's bitmaps
 // and free list are held in registers; levels and nodes are read and written in HBM.
+constexpr int FBLK = 13;          // free slots per spilled free-list block (GroupWave::alloc_slot)
+
 struct Core {
     static constexpr bool EXACT = true;
     const DevState& S;
@@ -681,13 +685,18 @@ struct Core {
         return n;
     }
 
-    // Node slots: the group's free list linked through Node::next, else a chunk of the pool's
-    // bump counter.
+    // Node slots: the group's free list in the block format of the FUNDED matchers (a free slot
+    // hosting up to FBLK - 1 more free ids: word 0 = next block, word 1 = count, words 2.. = ids;
+    // GroupWave::spill_blocks), so a group's state is valid for every kernel; else a chunk of the
+    // pool's bump counter.
     KDEV int32_t alloc_slot(int64_t idx) {
         if (free_head >= 0) {
-            const int32_t s = free_head;
-            free_head = S.pool[s].next;
-            return s;
+            const int32_t blk = free_head;
+            int32_t* w = reinterpret_cast<int32_t*>(&S.pool[blk]);
+            const int32_t cnt = w[1];
+            if (cnt > 0) { const int32_t s = w[1 + cnt]; w[1] = cnt - 1; return s; }
+            free_head = w[0];
+            return blk;
         }
         if (chunk_next >= chunk_end) {
             unsigned long long c = 0;
@@ -701,7 +710,13 @@ struct Core {
     }
     KDEV void free_slot(int32_t s) {
         S.pool[s].live = 0;
-        S.pool[s].next = free_head;
+        if (free_head >= 0) {                               // room in the head block
+            int32_t* w = reinterpret_cast<int32_t*>(&S.pool[free_head]);
+            const int32_t cnt = w[1];
+            if (cnt < FBLK - 1) { w[2 + cnt] = s; w[1] = cnt + 1; return; }
+        }
+        int32_t* w = reinterpret_cast<int32_t*>(&S.pool[s]);   // s becomes the head block
+        w[0] = free_head; w[1] = 0;
         free_head = s;
     }
 
@@ -1107,7 +1122,6 @@ constexpr int LVP = 101;          // LDS level entries per book side: prices 0..
 constexpr int FSTK = 128;         // LDS free-slot stack
 constexpr int TRD = 32;           // trades staged in LDS between reservations (GroupWave::emit)
 constexpr int DIRTY_WORDS = 64;   // 2048-bit filter of node slots written since the batch prefetch
-constexpr int FBLK = 13;          // free slots per spilled free-list block (GroupWave::alloc_slot)
 
 struct GroupLds {
     int2 ht[2 * LVP];             // head / tail node slot of level (side, price)
@@ -1726,7 +1740,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e || e - b <= (uint32_t)S.light_max) return;   // empty, or a light group (k_match_lanes)
-    if (failed(S.ctr)) return;
+    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
     w.load_group();
@@ -2108,7 +2122,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
     __shared__ int32_t fs[LFS][64];
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
-    if (failed(S.ctr)) return;
+    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;
     const int32_t g = (int32_t)(blockIdx.x * LANE_GROUPS + lane_id());
     uint32_t b = 0, e = 0;
     if (lane_id() < LANE_GROUPS && g < S.G) { b = S.seg[g]; e = S.seg[g + 1]; }
@@ -2247,10 +2261,11 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
 }
 
 // EXACT: one wavefront, the whole epoch in arrival order, every store exact.
-__global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
+__global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int only_fallback) {
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     if (failed(S.ctr)) return;
+    if (only_fallback && !S.ctr[ci(C_FALLBACK)]) return;   // FUNDED epoch whose proof held
     Core c(S, io);
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
@@ -2315,6 +2330,31 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     }
 }
 
+// FUNDED + KME_FLAG_SERIAL_FALLBACK, after an epoch k_serial took: the funded bounds restart from
+// the exact ledger (balance = the tightest lower bound; an account exists from the epoch's end).
+__global__ void __launch_bounds__(256) k_resync_funded(DevState S, EpochIO io) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= S.A || !S.ctr[ci(C_FALLBACK)] || failed(S.ctr)) return;
+    uint32_t h = (uint32_t)mix64((uint64_t)a) & S.bal_mask;   // Core::bal_find
+    int64_t bal = 0;
+    bool found = false;
+    for (uint32_t p = 0; p <= S.bal_mask; ++p) {
+        const uint32_t st = S.bal_state[h];
+        if (st == 0) break;
+        if (st == 1 && S.bal_key[h] == a) { found = true; bal = S.bal_val[h]; break; }
+        h = (h + 1) & S.bal_mask;
+    }
+    const int64_t end = io.seq_base + (int64_t)io.n;
+    if (found) {
+        if (!(S.acct_since[a] < end)) S.acct_since[a] = end - 1;
+        S.acct_lb[a] = bal;
+    } else {
+        S.acct_since[a] = INT64_MAX;
+        S.acct_lb[a] = 0;
+    }
+    S.acct_need[a] = 0; S.acct_negx[a] = 0; S.acct_xfer[a] = 0;
+}
+
 // FUNDED + KME_FLAG_EXACT_LEDGER (row f next-2): the epoch's ledger effects replayed in arrival
 // order on one wavefront, after the parallel matching decided every outcome: createBalance /
 // transfer (KP:131-146), checkBalance (KP:167-182) for each accepted BUY/SELL, both fillOrder calls
@@ -2324,7 +2364,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
 __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
-    if (failed(S.ctr)) return;
+    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;   // a serial epoch kept the exact ledger itself
     Core c(S, io);
     const int lane = lane_id();
     for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
@@ -2376,7 +2416,7 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
 // record instead of five random partial-line writes (the C ABI's SoA arrays) in the matching loop.
 // Records without a symbol group were answered by k_route / k_ledger_funded already.
 __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
-    if (failed(S.ctr)) return;   // a failed epoch: route's zero trade counts stay (k_scatter stays in bounds)
+    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;   // a failed epoch: route's zero trade counts stay (k_scatter stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         if (S.route_grp[i] < 0) continue;
         const KG int4* os = S.osort + 2 * (size_t)S.rank[i];
@@ -2572,8 +2612,11 @@ void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);
 }
-void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
-    hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev);
+void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, int only_fallback) {
+    hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev, only_fallback);
+}
+void launch_resync_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
+    hipLaunchKernelGGL(k_resync_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
     (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);

@@ -24,7 +24,9 @@ void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO*
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
 // EXACT pipeline (emap + route shared)
-void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
+void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, int only_fallback = 0);
+// FUNDED + KME_FLAG_SERIAL_FALLBACK: funded bounds from the exact ledger after a serial epoch
+void launch_resync_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 // FUNDED + KME_FLAG_EXACT_LEDGER: the epoch's ledger effects in arrival order (after compaction)
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
 // exclusive scan of L u32 values (DPP wave scans): out[k] = sum(in[0..k)); bsum needs

@@ -144,8 +144,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28) ||
                                          cfg->max_resting + (uint64_t)(cfg->max_symbols + 1) * POOL_CHUNK >= (1ull << 31)))
         return KME_E_INVALID;
-    if ((cfg->flags & ~KME_FLAG_EXACT_LEDGER) != 0 ||
-        ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1))   // a shard sees part of the ledger only
+    if ((cfg->flags & ~(KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK)) != 0 ||
+        ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1) ||   // a shard sees part of the ledger only
+        ((cfg->flags & KME_FLAG_SERIAL_FALLBACK) && !(cfg->flags & KME_FLAG_EXACT_LEDGER)))   // needs the exact ledger
         return KME_E_INVALID;
     if (cfg->credit_shards > (1u << 16) || (cfg->mode == KME_MODE_EXACT && cfg->credit_shards > 1))
         return KME_E_INVALID;
@@ -195,6 +196,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.otab, e->otab_cap);
     const bool exact_ledger = !funded || (cfg->flags & KME_FLAG_EXACT_LEDGER);
     S.ledger_replay = funded && exact_ledger ? 1 : 0;
+    S.fallback = funded && (cfg->flags & KME_FLAG_SERIAL_FALLBACK) ? 1 : 0;
     // FUNDED groups with at most light_max records in an epoch are matched one lane per group
     // (k_match_lanes), the others one wavefront per group (k_match); KME_LIGHT_MAX overrides.
     int32_t lm = cfg->light_max == 0 ? kDefaultLightMax : std::max(0, (int32_t)cfg->light_max);
@@ -334,6 +336,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ERR)], 0xFF, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_TRADES)], 0, (size_t)(ci(C_TTMP) - ci(C_TRADES) + 1) * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ACCT_OPS)], 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_FALLBACK)], 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(S.emap, 0, emap_cap * sizeof(uint64_t), st));
 
     phase_begin(e, PH_EMAP);
@@ -365,6 +368,12 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         phase_begin(e, PH_COMPACT);
         launch_compact(S, io, st);
         phase_end(e, PH_COMPACT);
+        if (S.fallback) {   // an epoch whose funded proof failed: the serial engine takes it
+            phase_begin(e, PH_SERIAL);
+            launch_serial(e->d_S, e->d_io, st, 1);
+            launch_resync_funded(S, io, st);
+            phase_end(e, PH_SERIAL);
+        }
         if (S.ledger_replay) {
             phase_begin(e, PH_REPLAY);
             launch_ledger_replay(e->d_S, e->d_io, st);
@@ -410,6 +419,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_rests = c[ci(C_RESTS)];
     s.n_maker_visits = c[ci(C_TRADES)];               // every maker visit is one trade (KP:238-242)
     s.n_cancel_ok = c[ci(C_CANCEL_OK)];
+    s.serial_fallback = c[ci(C_FALLBACK)] ? 1u : 0u;
     if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
@@ -635,6 +645,7 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme
         total.n_rests += es.n_rests;
         total.n_maker_visits += es.n_maker_visits;
         total.n_cancel_ok += es.n_cancel_ok;
+        total.serial_fallback += es.serial_fallback;   // sub-epochs that ran serially
         if (rc != KME_OK) {
             total.status = es.status;
             total.detail = es.detail;

@@ -348,3 +348,45 @@ def test_funded_domain_errors_both_paths(kme_mod, oracle_mod, name, light_max):
         _run_epochs(eng, orders, 1024)
     assert ke.value.status == 3 and ke.value.detail == detail
     assert ke.value.index == oe.value.index
+
+
+@pytest.mark.parametrize("light_max", [0, -1])
+def test_funded_serial_fallback_is_exact(kme_mod, oracle_mod, light_max):
+    """Row f next-2, validate-and-replay: epochs whose funded proof fails (accounts running out of
+    cash, checkBalance rejects) are matched serially on the exact ledger; the others in parallel.
+    Tape, books and ledger stay bit-exact, and both paths are taken."""
+    n_sym, n_acc = 32, 64
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
+    rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
+    setup = W.Orders.from_rows(rows)
+    stream = W.uniform(18_000, n_symbols=n_sym, n_accounts=n_acc, seed=31)
+    topup = W.Orders.from_rows([(W.TRANSFER, 0, a, 0, 0, 160_000) for a in range(n_acc)])
+    chunks = [setup]
+    for c in range(0, len(stream), 6000):   # top up, then three epochs of 2,000 orders
+        chunks.append(topup)
+        chunks += [stream.slice(c + k, min(len(stream), c + k + 2000)) for k in range(0, 6000, 2000)]
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=1 << 12, max_resting=1 << 16,
+                                 max_accounts=n_acc, ledger_capacity=1 << 14, light_max=light_max,
+                                 flags=kme_mod.FLAG_EXACT_LEDGER | kme_mod.FLAG_SERIAL_FALLBACK)
+    eng = kme_mod.Engine(cfg)
+    got, serial = [], []
+    for ch in chunks:
+        r = eng.process(ch)
+        got.append(r.tape_json(ch))
+        if ch is not topup and ch is not setup:
+            serial.append(int(r.status.serial_fallback))
+    o = oracle_mod.Oracle()
+    o.process(W.Orders.concat(chunks))
+    got = "".join(got)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+    assert 0 < sum(serial) < len(serial), serial
+    assert '"action":7' in got   # balance rejects happened (serial epochs)
+
+
+def test_serial_fallback_needs_exact_ledger(kme_mod):
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=4, max_epoch=64, max_resting=256, max_accounts=8,
+                                 flags=kme_mod.FLAG_SERIAL_FALLBACK)
+    with pytest.raises(kme_mod.KmeError):
+        kme_mod.Engine(cfg)
