@@ -1178,7 +1178,7 @@ KDEV int book_side(int64_t sid, bool is_buy) { return (sid != 0 && ((hi32(sid) <
 __device__ __attribute__((noinline)) uint64_t trade_overflow(KG TradeTmp* ttmp, KG unsigned long long* ctr, uint32_t tbase,
                                                              uint32_t tshard_cap, uint32_t ttmp_cap, uint64_t base, uint32_t n) {
     const int lane = lane_id();
-    if (base < tshard_cap && (uint64_t)lane < tshard_cap - base) ttmp[tbase + base + lane].seq = -1;
+    if (base < tshard_cap && (uint64_t)lane < tshard_cap - base && (uint32_t)lane < n) ttmp[tbase + base + lane].seq = -1;
     unsigned long long ob = 0;
     if (lane == 0) ob = atomicAdd(&ctr[ci(C_TTMP)], (unsigned long long)n);
     ob = bcast64(ob);
@@ -1780,7 +1780,9 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
             const int64_t noid = mk64(c0.x, c0.y), naid = mk64(c0.z, c0.w), nsid = mk64(c1.x, c1.y);
             const bool ok = c3.z != 0 && noid == B.oid && naid == B.aid;
-            B.pf_meta = c3.x | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10) |
+            // (price masked: a slot freed since it was indexed may host a free-list block, whose
+            // word 12 is a slot id -- unmasked, its high bits would fake the ok bit)
+            B.pf_meta = (c3.x & 0xFF) | (book_side(nsid, c3.y == BUY) << 8) | ((c3.y == SELL ? 1 : 0) << 9) | ((c1.y < 0 ? 1 : 0) << 10) |
                         ((ok ? 1 : 0) << 11);
             B.pf_poid = mk64(c2.x, c2.y);
             B.pf_size = c1.z; B.pf_next = c1.w; B.pf_prev = c2.z;

@@ -61,6 +61,11 @@ class Orders:
         return Orders(self.action[a:b], self.oid[a:b], self.aid[a:b], self.sid[a:b],
                       self.price[a:b], self.size[a:b], s)
 
+    def take(self, idx) -> "Orders":
+        s = None if self.oid_is_string is None else self.oid_is_string[idx]
+        return Orders(self.action[idx], self.oid[idx], self.aid[idx], self.sid[idx],
+                      self.price[idx], self.size[idx], s)
+
     @staticmethod
     def concat(parts) -> "Orders":
         parts = list(parts)
