@@ -191,7 +191,9 @@ def main():
     assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
 
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
-        d = eng.debug_counters().astype(np.float64).reshape(-1, 32).sum(axis=0)
+        rows = eng.debug_counters().astype(np.float64).reshape(-1, 32)
+        hot = int(np.argmax(rows[:, 7]))   # the group with the most k_match cycles (C4: the hot symbol)
+        d = rows[hot] if os.environ.get("KME_STAMPS_HOT") else rows.sum(axis=0)
         names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",
                  "n_trade_rec", "n_rest_rec", "n_cancel_rec", "maker_wait", "n_maker", "victim_wait", "n_victim",
                  "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre"]
@@ -209,6 +211,7 @@ def main():
                "rec_pick_per_rec": v["rec_pick"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
                "rec_total_per_rec": v["rec_out"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
                "counts": {n: v[n] for n in ("n_trade_rec", "n_rest_rec", "n_cancel_rec", "n_maker", "n_victim")}}
+        per["group"] = hot if os.environ.get("KME_STAMPS_HOT") else "all"
         print(json.dumps({"stamps": per}), flush=True)
         return
     stats = torch.tensor([elapsed, float(n_orders), float(n_trades)], dtype=torch.float64, device=dev)

@@ -17,13 +17,13 @@ pytestmark = pytest.mark.gpu
 E = 1 << 18
 
 
-def _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, light_max):
+def _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, light_max, epoch=E):
     eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1,
-                                                max_epoch=max(E, len(setup)), max_resting=1 << 22,
-                                                max_trades=2 * E + (1 << 16), max_accounts=n_acc,
+                                                max_epoch=max(epoch, len(setup)), max_resting=1 << 22,
+                                                max_trades=2 * epoch + (1 << 16), max_accounts=n_acc,
                                                 light_max=light_max))
     o = oracle_mod.Oracle()
-    parts = [setup] + [stream.slice(a, min(len(stream), a + E)) for a in range(0, len(stream), E)]
+    parts = [setup] + [stream.slice(a, min(len(stream), a + epoch)) for a in range(0, len(stream), epoch)]
     for k, part in enumerate(parts):
         got = eng.process(part).tape_json(part)
         o.process(part)
@@ -71,3 +71,12 @@ def test_c4_zipf_at_scale(kme_mod, oracle_mod):
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
     _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
 
+
+
+def test_n8_shard_shape_at_scale(kme_mod, oracle_mod):
+    """The per-GPU shard of C3 at N = 8 (8,192 symbols), 2^21-record epochs: 256 records per group
+    per epoch, every group busy (one wavefront each), several record batches per group."""
+    n_sym, n_acc, n = 8192, 65536, 1 << 22
+    stream = W.uniform(n, n_symbols=n_sym, n_accounts=n_acc, seed=1003)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0, epoch=1 << 21)
