@@ -229,7 +229,8 @@ def main():
         achieved = float(np.mean(bytes_alg)) / avg_match_s / 1e9 if avg_match_s > 0 else 0.0
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
-        if os.path.exists(pmc):
+        # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round.sh)
+        if os.path.exists(pmc) and world == 1 and not args.symbols and not args.mix and E == (1 << 22):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         out = {

@@ -22,7 +22,7 @@ rc=$?; echo "bench_rc=$rc"; cat $OUT/bench.json; tail -2 $OUT/bench.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/prof.log 2>&1
 rc=$?; echo "prof_rc=$rc"
 [ $rc -eq 0 ] || exit $rc
-for extra in "--workload c3 --symbols 32768" "--workload c3 --symbols 8192" "--workload c2" "--workload c4 --steps 4 --warmup 1"; do
+for extra in "--workload c3 --symbols 32768" "--workload c3 --symbols 8192" "--workload c2" "--workload c4 --steps 2 --warmup 1" "--workload c5"; do
   timeout -k 10 300 python3 -u bench.py --no-cpu-baseline $extra >> $OUT/bench_extra.jsonl 2>> $OUT/bench_extra.err
   rc=$?; echo "extra [$extra] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
