@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default 65,536 / N)")
     ap.add_argument("--mix", default="", help="diagnostic: BUY,SELL,CANCEL fractions of the c2/c3 stream")
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
+    ap.add_argument("--max-resting", type=int, default=0,
+                    help="diagnostic: resting-order capacity (default: the whole stream, every order could rest)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
@@ -127,7 +129,7 @@ def main():
                                                    [float(x) for x in args.mix.split(",")] if args.mix else None)
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
-                             max_resting=min(total, 1 << 30), max_trades=2 * E + (1 << 16),
+                             max_resting=args.max_resting or min(total, 1 << 30), max_trades=2 * E + (1 << 16),
                              max_accounts=nacc, device=local_rank)
     eng = kme.Engine(cfg)
     stream_handle = torch.cuda.current_stream(dev).cuda_stream
