@@ -123,7 +123,7 @@ struct DevState {
     KG uint32_t* pos_state;
     KG PosEntry* pos;
     // per-epoch scratch
-    KG uint64_t* emap;                // oid -> input index of this epoch's BUY/SELL, packed entries
+    KG uint32_t* epos;                // oid-table position of this epoch's BUY/SELL i (k_emap -> k_table)
     KG int32_t* route_grp;
     KG int64_t* cancel_tgt;           // EXACT: cancel target (FUNDED: in the packed record)
     KG int32_t* rest_slot;
@@ -164,8 +164,7 @@ struct EpochIO {
     uint32_t n;
     uint32_t trades_cap;
     int64_t seq_base;
-    uint32_t emap_mask;
-    uint32_t _pad;
+    uint32_t _pad0, _pad;
 };
 
 }  // namespace kme

@@ -196,15 +196,43 @@ KDEV int64_t wave_incl_scan_i64(int64_t v) {
 KDEV uint32_t oid_fp(int64_t oid) { return (uint32_t)(mix64((uint64_t)oid ^ 0x9e3779b97f4a7c15ull) >> 32) | 1u; }
 KDEV uint64_t hentry(uint32_t fp, uint32_t v) { return ((uint64_t)fp << 32) | v; }
 
+// Entry values: a node slot (< 2^31); OT_PENDING | i for BUY/SELL i of the epoch in flight (k_emap
+// inserts every BUY/SELL; k_table turns the entry into the order's rest slot, or OT_DEAD when it
+// did not rest), so one table answers both "an earlier order of this epoch" and "a resting order".
+constexpr uint32_t OT_PENDING = 0x80000000u;
+constexpr uint32_t OT_DEAD = 0xFFFFFFFFu;
+
+// A resting order's slot (a live node with this oid), or -1.
 KDEV int32_t otab_lookup(const DevState& S, int64_t oid) {
     const uint32_t fp = oid_fp(oid);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
     for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
         const uint64_t e = S.otab[h];
         if (e == 0) return -1;
-        if ((uint32_t)(e >> 32) == fp) {
-            const int32_t s = (int32_t)(uint32_t)e;
-            if (S.pool[s].live && S.pool[s].oid == oid) return s;
+        const uint32_t v = (uint32_t)e;
+        if ((uint32_t)(e >> 32) == fp && !(v & OT_PENDING)) {
+            if (S.pool[v].live && S.pool[v].oid == oid) return (int32_t)v;
+        }
+        h = (h + 1) & S.otab_mask;
+    }
+    return -1;
+}
+// removeOrder's orders.get(oid) at input i (KP:290): an order of this epoch submitted before i
+// (returns -(j + 2)), else a resting order's slot, else -1.
+KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oid, uint32_t i) {
+    const uint32_t fp = oid_fp(oid);
+    uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
+    for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
+        const uint64_t e = S.otab[h];
+        if (e == 0) return -1;
+        const uint32_t v = (uint32_t)e;
+        if ((uint32_t)(e >> 32) == fp && v != OT_DEAD) {
+            if (v & OT_PENDING) {
+                const uint32_t j = v & ~OT_PENDING;
+                if (j < i && io.oid[j] == oid) return -((int64_t)j + 2);
+            } else if (S.pool[v].live && S.pool[v].oid == oid) {
+                return (int64_t)v;
+            }
         }
         h = (h + 1) & S.otab_mask;
     }
@@ -218,17 +246,6 @@ KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
         h = (h + 1) & S.otab_mask;
     }
     return false;
-}
-KDEV int32_t emap_lookup(const DevState& S, const EpochIO& io, int64_t oid) {
-    const uint32_t fp = oid_fp(oid);
-    uint32_t h = (uint32_t)mix64((uint64_t)oid) & io.emap_mask;
-    for (uint32_t probes = 0; probes <= io.emap_mask; ++probes) {
-        const uint64_t e = S.emap[h];
-        if (e == 0) return -1;
-        if ((uint32_t)(e >> 32) == fp && io.oid[(uint32_t)e] == oid) return (int32_t)(uint32_t)e;
-        h = (h + 1) & io.emap_mask;
-    }
-    return -1;
 }
 
 // ------------------------------------------------------------------ epoch kernels: emap / ledger / route
@@ -252,24 +269,36 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     __shared__ uint32_t red[4];
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (t0 == 0) *io_dev = io;   // the group / serial kernels read the epoch descriptor from HBM
-    uint32_t n_orders = 0, n_acct = 0;
+    uint32_t n_orders = 0, n_acct = 0, n_ins = 0;
     for (uint32_t i = t0; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
         n_orders += (a == BUY || a == SELL || a == CANCEL) ? 1u : 0u;
         if (a == BUY || a == SELL) {
+            // the order's oid-table entry (pending until k_table); on the way, the duplicate-oid
+            // guard: another BUY/SELL of this epoch, or a live resting order, with this oid
+            // (KP:221 would overwrite it and corrupt its level's list)
             const int64_t oid = io.oid[i];
             const uint32_t fp = oid_fp(oid);
-            const unsigned long long ent = hentry(fp, i);
-            uint32_t h = (uint32_t)mix64((uint64_t)oid) & io.emap_mask;
-            for (uint32_t probes = 0; probes <= io.emap_mask; ++probes) {
-                const unsigned long long prev = atomicCAS((unsigned long long*)&S.emap[h], 0ull, ent);
-                if (prev == 0) break;
-                if ((uint32_t)(prev >> 32) == fp && io.oid[(uint32_t)prev] == oid) {
-                    raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i > (uint32_t)prev ? i : (uint32_t)prev);
-                    break;
+            const unsigned long long ent = hentry(fp, OT_PENDING | i);
+            uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
+            bool placed = false;
+            for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
+                const unsigned long long prev = atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent);
+                if (prev == 0) { S.epos[i] = h; placed = true; break; }
+                const uint32_t v = (uint32_t)prev;
+                if ((uint32_t)(prev >> 32) == fp && v != OT_DEAD) {
+                    if (v & OT_PENDING) {
+                        const uint32_t j = v & ~OT_PENDING;
+                        if (io.oid[j] == oid) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i > j ? i : j); break; }
+                    } else if (S.pool[v].live && S.pool[v].oid == oid) {
+                        raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i);
+                        break;
+                    }
                 }
-                h = (h + 1) & io.emap_mask;
+                h = (h + 1) & S.otab_mask;
             }
+            if (placed) ++n_ins;
+            else S.epos[i] = OT_DEAD;
             if (funded) {
                 const int32_t price = io.price[i], size = io.size[i];
                 if (price < 0 || price > 100 || size < 0) {
@@ -288,9 +317,11 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     }
     const uint32_t no = block_sum_256(n_orders, red);
     const uint32_t na = block_sum_256(n_acct, red);
+    const uint32_t ni = block_sum_256(n_ins, red);
     if (threadIdx.x == 0) {
         if (no) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)no);
         if (na) atomicAdd(&S.ctr[ci(C_ACCT_OPS)], (unsigned long long)na);
+        if (ni) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)ni);
     }
 }
 
@@ -403,7 +434,6 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     case SELL: {
         grp = group_of(io.sid[i], S.G);
         if (grp < 0) { direct = true; ok = false; }                         // books.get == null (KP:202-203)
-        if (otab_lookup(S, io.oid[i]) >= 0) raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i);
         if (funded && grp >= 0) {
             const int64_t aid = io.aid[i];
             acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
@@ -414,23 +444,21 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         // the target's level (price | side << 8 | 1 << 9) rides along for k_match_lanes, which then
         // fetches the node and its level in one step (checked against the node there)
         const int64_t oid = io.oid[i];
-        const int32_t j = emap_lookup(S, io, oid);
-        if (j >= 0 && (uint32_t)j < i) {
+        const int64_t t = otab_cancel_target(S, io, oid, i);
+        if (t <= -2) {
+            const uint32_t j = (uint32_t)(-(t + 2));
             const int64_t sj = io.sid[j];
             const int32_t gj = group_of(sj, S.G);
             if (gj >= 0) {
-                grp = gj; tgt = -((int64_t)j + 2);
+                grp = gj; tgt = t;
                 const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
                 vlev = (io.price[j] & 0xFF) | (side << 8) | (1 << 9);
             }
-        } else {
-            const int32_t s = otab_lookup(S, oid);
-            if (s >= 0) {
-                const Node nd = S.pool[s];
-                grp = nd.group; tgt = s;
-                const int side = (nd.sid != 0 && ((nd.sid < 0) != (nd.action != BUY))) ? 1 : 0;
-                vlev = (nd.price & 0xFF) | (side << 8) | (1 << 9);
-            }
+        } else if (t >= 0) {
+            const Node nd = S.pool[t];
+            grp = nd.group; tgt = t;
+            const int side = (nd.sid != 0 && ((nd.sid < 0) != (nd.action != BUY))) ? 1 : 0;
+            vlev = (nd.price & 0xFF) | (side << 8) | (1 << 9);
         }
         if (grp < 0) { direct = true; ok = false; }                         // orders.get == null (KP:290-291)
         break;
@@ -2476,24 +2504,18 @@ __global__ void __launch_bounds__(256) k_tsh_fold(DevState S) {
 }
 
 // ------------------------------------------------------------------ oid-table maintenance
-// Orders that came to rest this epoch and are still live get an oid-table entry.  The used-slot
-// counter is bumped once per wavefront (a single hot counter would serialise every insert).
-// Oid-table entries for the orders of this epoch that are still resting.
+// Each BUY/SELL's pending entry (k_emap) becomes its rest slot, or OT_DEAD if it did not rest: one
+// plain store at the recorded position, no probe.  An order that rested and left the book later in
+// the epoch keeps a stale slot entry, dropped by validation like every lazily deleted one.
 __global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io) {
-    __shared__ uint32_t red[4];
-    uint32_t n_ins = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
+        const int32_t a = io.action[i];
+        if (a != BUY && a != SELL) continue;
+        const uint32_t h = S.epos[i];
+        if (h == OT_DEAD) continue;
         const int32_t s = S.rest_slot[i];
-        if (s >= 0) {
-            const int64_t oid = io.oid[i];
-            if (S.pool[s].live && S.pool[s].oid == oid) {
-                if (otab_insert(S, oid, s)) ++n_ins;
-                else raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, i);
-            }
-        }
+        S.otab[h] = hentry(oid_fp(io.oid[i]), s >= 0 ? (uint32_t)s : OT_DEAD);
     }
-    const uint32_t tot = block_sum_256(n_ins, red);
-    if (threadIdx.x == 0 && tot) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)tot);
 }
 // Rebuild: every live node of the pool's used prefix gets an entry.
 __global__ void __launch_bounds__(256) k_otab_refill(DevState S, uint32_t nslots) {

@@ -177,7 +177,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         S.passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
     }
     S.pool_cap = (uint32_t)P;
-    e->otab_cap = pow2_at_least(std::max<uint64_t>(2 * P, 1024));
+    // every BUY/SELL of an epoch takes an entry at k_emap (pending -> its rest slot, or dead, at
+    // k_table), so the table holds the live orders and one epoch of new ones at half load
+    e->otab_cap = pow2_at_least(std::max<uint64_t>(2 * (P + E), 1024));
     S.otab_mask = (uint32_t)(e->otab_cap - 1);
     S.credit_div = cfg->credit_shards > 1 ? cfg->credit_shards : 1;
     S.trades_cap = cfg->max_trades;
@@ -221,8 +223,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.pos_state, lc);
         ALLOC(S.pos, lc);
     }
-    const uint64_t emap_cap = pow2_at_least(std::max<uint64_t>(2ull * E, 1024));
-    ALLOC(S.emap, emap_cap);
+    ALLOC(S.epos, E);
     ALLOC(S.route_grp, E);
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
@@ -328,8 +329,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     io.n_trades = e->d_ntrades;
     io.n = n;
     io.seq_base = e->seq_base;
-    const uint64_t emap_cap = pow2_at_least(std::max<uint64_t>(2ull * n, 1024));
-    io.emap_mask = (uint32_t)(emap_cap - 1);
     for (bool& u : e->ev_used) u = false;
 
     // per-epoch counters: error = none, stats = 0 (pool bump / table usage persist)
@@ -337,7 +336,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_TRADES)], 0, (size_t)(ci(C_TTMP) - ci(C_TRADES) + 1) * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ACCT_OPS)], 0, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_FALLBACK)], 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(S.emap, 0, emap_cap * sizeof(uint64_t), st));
 
     phase_begin(e, PH_EMAP);
     launch_emap(S, io, funded, e->d_io, st);
@@ -436,7 +434,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
         }
     }
     // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild
-    if (!e->failed && c[ci(C_OTAB_USED)] * 2 > e->otab_cap) {
+    if (!e->failed && (c[ci(C_OTAB_USED)] + e->cfg.max_epoch) * 2 > e->otab_cap) {
         launch_otab_rebuild(e->S, (uint32_t)std::min<uint64_t>(c[ci(C_POOL_BUMP)], e->S.pool_cap), e->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
