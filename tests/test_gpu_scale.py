@@ -8,6 +8,7 @@ cancels hit orders that were swept earlier in the same epoch -- the combination 
 stale-node acceptance in k_match's batch cancel prefetch (a freed slot hosting a free-list block
 has a slot id in word 12, whose bit 11 was packed over the prefetch's `ok` bit).
 """
+import numpy as np
 import pytest
 
 from kme import workloads as W
@@ -80,3 +81,84 @@ def test_n8_shard_shape_at_scale(kme_mod, oracle_mod):
     stream = W.uniform(n, n_symbols=n_sym, n_accounts=n_acc, seed=1003)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
     _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0, epoch=1 << 21)
+
+
+def test_exact_exchange_test_at_scale(kme_mod, oracle_mod):
+    """C1 (exchange_test.js stream) through the EXACT engine, 300k events in 2^16-record epochs;
+    tape, books and the ledger stores (Balances, Positions) against the oracle."""
+    orders = W.exchange_test(300_000, seed=11)
+    # N(50, 10) prices leave the parity domain eventually (a BUY/SELL priced outside 0..126 may
+    # rest, where the engine refuses with KME_D_PRICE): stop before the first such order
+    out = np.nonzero(((orders.action == W.BUY) | (orders.action == W.SELL)) & ((orders.price < 0) | (orders.price > 126)))[0]
+    if len(out):
+        orders = orders.slice(0, int(out[0]))
+    assert len(orders) > 100_000
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_EXACT, max_symbols=16, max_epoch=1 << 16,
+                                                max_resting=1 << 18, ledger_capacity=1 << 16))
+    o = oracle_mod.Oracle()
+    for a in range(0, len(orders), 1 << 16):
+        part = orders.slice(a, min(len(orders), a + (1 << 16)))
+        got = eng.process(part).tape_json(part)
+        o.process(part)
+        want = o.tape_text()
+        o.clear_tape()
+        assert got == want, f"epoch at {a}"
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "cancel_replace"])
+def test_exact_ledger_replay_at_scale(kme_mod, oracle_mod, kind):
+    """FUNDED matching with KME_FLAG_EXACT_LEDGER at 512 symbols x 2,048 accounts, 2^18-record
+    epochs: the replayed Balances / Positions equal the oracle's after every epoch."""
+    n_sym, n_acc, n = 512, 2048, 3 * E
+    body = (W.uniform(n, n_symbols=n_sym, n_accounts=n_acc, seed=1004) if kind == "uniform"
+            else W.cancel_replace(n, n_symbols=n_sym, n_accounts=n_acc, seed=1005))
+    k = W.funded_transfers_needed(n, n_acc, big=kind == "cancel_replace")
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1), transfers_per_account=k)
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=E,
+                                                max_resting=1 << 21, max_trades=2 * E + (1 << 16), max_accounts=n_acc,
+                                                ledger_capacity=1 << 20, flags=kme_mod.FLAG_EXACT_LEDGER))
+    o = oracle_mod.Oracle()
+    for part in [setup] + [body.slice(a, min(n, a + E)) for a in range(0, n, E)]:
+        got = eng.process(part).tape_json(part)
+        o.process(part)
+        want = o.tape_text()
+        o.clear_tape()
+        assert got == want
+        assert eng.snapshot_ledger() == o.dump_ledger()
+    assert eng.snapshot_books() == o.dump_books()
+
+
+def test_serial_fallback_at_scale(kme_mod, oracle_mod):
+    """Validate-and-replay at 256 symbols x 1,024 accounts: accounts topped up before every third
+    2^16-record epoch, so proven epochs run in parallel and the ones that run short of cash fall
+    back to the serial exact engine; tape, books and ledger stay exact across the mix."""
+    n_sym, n_acc, ep = 256, 1024, 1 << 16
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
+    rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
+    setup = W.Orders.from_rows(rows)
+    stream = W.uniform(9 * ep, n_symbols=n_sym, n_accounts=n_acc, seed=1006)
+    topup = W.Orders.from_rows([(W.TRANSFER, 0, a, 0, 0, 300_000) for a in range(n_acc)])
+    chunks = [setup]
+    for c in range(0, len(stream), 3 * ep):
+        chunks.append(topup)
+        chunks += [stream.slice(c + k, c + k + ep) for k in range(0, 3 * ep, ep)]
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=ep,
+                                                max_resting=1 << 20, max_trades=4 * ep, max_accounts=n_acc,
+                                                ledger_capacity=1 << 18,
+                                                flags=kme_mod.FLAG_EXACT_LEDGER | kme_mod.FLAG_SERIAL_FALLBACK))
+    o = oracle_mod.Oracle()
+    serial = []
+    for ch in chunks:
+        r = eng.process(ch)
+        got = r.tape_json(ch)
+        o.process(ch)
+        want = o.tape_text()
+        o.clear_tape()
+        assert got == want
+        if ch is not topup and ch is not setup:
+            serial.append(int(r.status.serial_fallback))
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+    assert 0 < sum(serial) < len(serial), serial
