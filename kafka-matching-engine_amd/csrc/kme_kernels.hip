@@ -1898,8 +1898,12 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
 // records in the epoch stay with k_match (which skips the light ones); both kernels keep the
 // same persistent group format (GroupState, Level, Node, free-slot blocks).
 constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBLK-slot blocks)
-constexpr int LANE_GROUPS = 32;   // groups per wavefront (the other lanes idle): two wavefronts
-                                  // per SIMD at 65,536 groups, so one issues while the other waits
+#ifndef KME_LANE_GROUPS
+#define KME_LANE_GROUPS 32
+#endif
+constexpr int LANE_GROUPS = KME_LANE_GROUPS;   // groups per wavefront (the other lanes idle): two
+                                  // wavefronts per SIMD at 65,536 groups, so one issues while the other waits
+static_assert(LANE_GROUPS >= 1 && LANE_GROUPS <= 64, "k_match_lanes: one group per lane");
 
 struct GroupLane {
     const DevState& S;
@@ -2570,9 +2574,20 @@ __global__ void k_init_state(DevState S) {
     if (k < (uint32_t)S.A && S.acct_since) S.acct_since[k] = INT64_MAX;
 }
 
+// Per-epoch counters: error = none, the epoch's statistics = 0 (pool bump and table usage persist).
+// One launch instead of four fills.
+__global__ void k_epoch_reset(DevState S) {
+    const int k = threadIdx.x;
+    if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
+    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK) S.ctr[ci(k)] = 0ull;
+}
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
+void launch_epoch_reset(const DevState& S, hipStream_t st) {
+    hipLaunchKernelGGL(k_epoch_reset, dim3(1), dim3(C_NCTR), 0, st, S);
+}
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st) {
     const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
     hipLaunchKernelGGL(k_emap, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);

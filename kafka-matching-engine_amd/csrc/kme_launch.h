@@ -12,6 +12,7 @@ constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global
 constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT_MAX overrides)
 
 // FUNDED pipeline
+void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);

@@ -95,14 +95,14 @@ static kme_status dalloc(kme_engine* e, T** p, size_t count) {
         if (_s != KME_OK) { kme_destroy(e); return _s; } \
     } while (0)
 
-static void phase_begin(kme_engine* e, int ph) {
+static void phase_begin(kme_engine* e, int ph, hipStream_t s = nullptr) {
     if (!e->timing) return;
-    (void)hipEventRecord(e->ev[2 * ph], e->stream);
+    (void)hipEventRecord(e->ev[2 * ph], s ? s : e->stream);
     e->ev_used[ph] = true;
 }
-static void phase_end(kme_engine* e, int ph) {
+static void phase_end(kme_engine* e, int ph, hipStream_t s = nullptr) {
     if (!e->timing) return;
-    (void)hipEventRecord(e->ev[2 * ph + 1], e->stream);
+    (void)hipEventRecord(e->ev[2 * ph + 1], s ? s : e->stream);
 }
 
 extern "C" {
@@ -332,10 +332,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     for (bool& u : e->ev_used) u = false;
 
     // per-epoch counters: error = none, stats = 0 (pool bump / table usage persist)
-    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ERR)], 0xFF, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_TRADES)], 0, (size_t)(ci(C_TTMP) - ci(C_TRADES) + 1) * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_ACCT_OPS)], 0, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(&S.ctr[ci(C_FALLBACK)], 0, sizeof(unsigned long long), st));
+    launch_epoch_reset(S, st);
 
     phase_begin(e, PH_EMAP);
     launch_emap(S, io, funded, e->d_io, st);
@@ -382,6 +379,8 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         launch_serial(e->d_S, e->d_io, st);
         phase_end(e, PH_SERIAL);
     }
+    // k_table stays in line: beside the compaction on lane_stream both random-access phases slowed
+    // each other down to the same sum (measured: compact 0.20 -> 0.28 ms, table 0.09 -> 0.16 ms)
     phase_begin(e, PH_TABLE);
     launch_table(S, io, st);
     phase_end(e, PH_TABLE);
