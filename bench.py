@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--max-resting", type=int, default=0,
                     help="diagnostic: resting-order capacity (default: the whole stream, every order could rest)")
+    ap.add_argument("--light-max", type=int, default=0,
+                    help="diagnostic: kme_config.light_max (0 = default 128 records per group and epoch)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
@@ -130,7 +132,7 @@ def main():
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
                              max_resting=args.max_resting or min(total, 1 << 30), max_trades=2 * E + (1 << 16),
-                             max_accounts=nacc, device=local_rank)
+                             max_accounts=nacc, device=local_rank, light_max=args.light_max)
     eng = kme.Engine(cfg)
     stream_handle = torch.cuda.current_stream(dev).cuda_stream
     eng.set_stream(stream_handle)
@@ -229,12 +231,14 @@ def main():
     if rank == 0:
         avg_match_s = float(np.mean(match_ms)) / 1e3
         achieved = float(np.mean(bytes_alg)) / avg_match_s / 1e9 if avg_match_s > 0 else 0.0
-        traffic = None
+        traffic, pmc_derived = None, None
         pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
         # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round.sh)
         if os.path.exists(pmc) and world == 1 and not args.symbols and not args.mix and E == (1 << 22):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pj = json.load(f)
+            traffic = pj.get("hbm_bytes_per_launch")
+            pmc_derived = pj.get("per_kernel_derived")
         out = {
             "metric": METRIC,
             "value": n_orders_all / elapsed,
@@ -262,6 +266,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",
                          "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg))},
+            # occupancy and LDS bank conflicts of the match-phase kernels, from the committed rocprofv3
+            # PMC passes of this configuration (tools/pmc_kmatch.sh, tools/pmc_summary.py)
+            "pmc_match_phase": pmc_derived,
         }
         if args.serialize:
             out["serialize"] = {"tape_bytes_per_epoch": float(np.mean(tape_bytes[-args.steps:])),

@@ -27,3 +27,6 @@ for extra in "--workload c3 --symbols 32768" "--workload c3 --symbols 8192" "--w
   rc=$?; echo "extra [$extra] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
+# occupancy / LDS bank conflicts / traffic of the N = 8 shard shape too (every group busy: k_match)
+bash tools/pmc_kmatch.sh $TAG/pmc8k k_match --symbols 8192 || exit $?
+cp $OUT/pmc8k/pmc_summary.json profiles/pmc_k_match_c3_s8192.json

@@ -30,6 +30,30 @@ def counters(d, kernel_re):
     return vals
 
 
+N_SE, N_CU, WAVES_PER_CU = 32, 256, 32   # MI355X: 8 XCDs x 4 shader engines, 256 CUs, 32 waves/CU cap
+
+
+def derived(res):
+    """Per kernel: occupancy and LDS bank conflicts.  SQ_WAVE_CYCLES counts quad-cycles summed over
+    the waves; SQ_BUSY_CYCLES counts cycles summed over the 32 shader engines, so the kernel's own
+    duration in cycles is SQ_BUSY_CYCLES / 32 and the mean resident waves per CU is
+    4 * SQ_WAVE_CYCLES / (SQ_BUSY_CYCLES / 32) / 256.  SQ_LDS_BANK_CONFLICT = extra LDS cycles."""
+    get = lambda c, k: res.get(c, {}).get("per_kernel", {}).get(k)
+    out = {}
+    for k in res.get("SQ_WAVES", {}).get("per_kernel", {}):
+        wc, bc = get("SQ_WAVE_CYCLES", k), get("SQ_BUSY_CYCLES", k)
+        d = {"waves": get("SQ_WAVES", k)}
+        if wc and bc:
+            w = 4 * wc / (bc / N_SE) / N_CU
+            d["mean_resident_waves_per_cu"] = w
+            d["occupancy_frac"] = w / WAVES_PER_CU
+        if get("SQ_LDS_BANK_CONFLICT", k) is not None:
+            d["lds_bank_conflict_cycles"] = get("SQ_LDS_BANK_CONFLICT", k)
+            d["lds_insts"] = get("SQ_INSTS_LDS", k)
+        out[k] = d
+    return out
+
+
 def main():
     d, kre, out = sys.argv[1], sys.argv[2], sys.argv[3]
     skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
@@ -57,6 +81,7 @@ def main():
         res["write_bytes_per_launch"] = w * 1024
         res["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
         res["note"] = "FETCH_SIZE doubled per the gfx950 calibration; MALL hits included (upper bound)"
+    res["per_kernel_derived"] = derived(res)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
