@@ -517,18 +517,28 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
     const uint32_t base = blockIdx.x * RADIX_TILE;
     const int dst = src ^ 1;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    for (int j = 0; j < RADIX_TILE / 256; ++j) {
+    // the tile's keys and values are loaded up front: a load issued inside the loop would wait for
+    // the previous chunk's scattered stores too (vmcnt counts both, in order)
+    constexpr int RJ = RADIX_TILE / 256;
+    uint32_t keys[RJ], vals[RJ];
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const uint32_t k = base + j * 256 + t;
+        keys[j] = 0; vals[j] = 0;
+        if (k < io.n) {
+            keys[j] = radix_key(S, pass, src, k);
+            vals[j] = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
         for (int q = 0; q < RADIX_PER_T; ++q) {
             wcnt[0][t + 256 * q] = 0; wcnt[1][t + 256 * q] = 0; wcnt[2][t + 256 * q] = 0; wcnt[3][t + 256 * q] = 0;
         }
         __syncthreads();
         const uint32_t k = base + j * 256 + t;
         const bool valid = k < io.n;
-        uint32_t key = 0, val = 0;
-        if (valid) {
-            key = radix_key(S, pass, src, k);
-            val = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
-        }
+        const uint32_t key = keys[j], val = vals[j];
         const uint32_t d = (key >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1);
         // lanes of this wavefront with the same digit (match-any over the digit bits)
         unsigned long long peers = __ballot(valid);
@@ -2468,6 +2478,7 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
 // Blocks (s, *) with s < TSHARDS move shard s's trades, blocks (TSHARDS, *) the overflow
 // region's, each to trades[trade_off[seq] + ord] (arrival order).
 constexpr uint32_t SCATTER_SUB = 8;   // blocks per shard region
+constexpr int SCATTER_ITEMS = 4;      // trades per thread and round
 __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const uint32_t* total) {
     const uint32_t s = blockIdx.x;
     if (failed(S.ctr)) return;
@@ -2488,10 +2499,23 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
         const unsigned long long used = S.ctr[ci(C_TTMP)];
         cnt = (uint32_t)(used < S.ttmp_cap ? used : S.ttmp_cap);
     }
-    for (uint32_t k = blockIdx.y * blockDim.x + threadIdx.x; k < cnt; k += gridDim.y * blockDim.x) {
-        const TradeTmp r = S.ttmp[base + k];
-        if (r.seq < 0) continue;
-        io.trades[io.trade_off[r.seq] + (uint32_t)r.ord] = r.t;
+    // SCATTER_ITEMS trades per thread and round, every load of the round before its stores (a load
+    // after a store would wait for the store too: vmcnt counts both, in order)
+    const uint32_t stride = gridDim.y * blockDim.x;
+    for (uint32_t k0 = blockIdx.y * blockDim.x + threadIdx.x; k0 < cnt; k0 += SCATTER_ITEMS * stride) {
+        TradeTmp r[SCATTER_ITEMS];
+        uint32_t off[SCATTER_ITEMS];
+#pragma unroll
+        for (int q = 0; q < SCATTER_ITEMS; ++q) {
+            const uint32_t k = k0 + q * stride;
+            r[q].seq = -1;
+            if (k < cnt) r[q] = S.ttmp[base + k];
+        }
+#pragma unroll
+        for (int q = 0; q < SCATTER_ITEMS; ++q) off[q] = r[q].seq >= 0 ? io.trade_off[r[q].seq] : 0;
+#pragma unroll
+        for (int q = 0; q < SCATTER_ITEMS; ++q)
+            if (r[q].seq >= 0) io.trades[off[q] + (uint32_t)r[q].ord] = r[q].t;
     }
 }
 // The shard lines' rest / cancel counts into the counters block; the lines zeroed for the next epoch.
@@ -2633,7 +2657,9 @@ void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO*
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);
 }
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
-    if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);
+    // one thread per record (no counters to sum): a thread striding over several records would
+    // wait for its previous record's stores before its next loads (vmcnt counts both, in order)
+    if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);
     // trade_off[0..n] = exclusive scan of n_trades; bsum/total scratch in ghist
     uint32_t* bsum = S.ghist;
     const uint32_t nb = cdiv(io.n > 0 ? io.n : 1, SCAN_BLOCK);
@@ -2646,7 +2672,7 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
-    hipLaunchKernelGGL(k_table, dim3(std::min<uint32_t>(cdiv(io.n, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);   // one thread per record, as k_unsort
 }
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);
