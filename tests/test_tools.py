@@ -1,0 +1,53 @@
+"""Measurement tooling (CPU): the PMC summary's derived occupancy / LDS figures and the bench's
+algorithmic byte model."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import pmc_summary  # noqa: E402
+
+
+def _res(per_kernel):
+    out = {}
+    for k, counters in per_kernel.items():
+        for c, v in counters.items():
+            out.setdefault(c, {"mean_per_dispatch": 0.0, "per_kernel": {}})
+            out[c]["per_kernel"][k] = v
+            out[c]["mean_per_dispatch"] += v
+    return out
+
+
+def test_occupancy_formula():
+    # 2,048 waves resident for the whole kernel: 8 per CU; SQ_WAVE_CYCLES in quad-cycles summed over
+    # waves, SQ_BUSY_CYCLES in cycles summed over the 32 shader engines
+    cycles = 1_000_000
+    res = _res({"k": {"SQ_WAVES": 2048, "SQ_WAVE_CYCLES": 2048 * cycles / 4, "SQ_BUSY_CYCLES": 32 * cycles,
+                      "SQ_LDS_BANK_CONFLICT": 10.0, "SQ_INSTS_LDS": 1000.0}})
+    d = pmc_summary.derived(res)["k"]
+    assert abs(d["mean_resident_waves_per_cu"] - 8.0) < 1e-9
+    assert abs(d["occupancy_frac"] - 8.0 / 32) < 1e-9
+    assert d["lds_bank_conflict_cycles"] == 10.0 and d["lds_insts"] == 1000.0
+
+
+def test_committed_pmc_summaries_carry_derived_fields():
+    for name in ("pmc_k_match_c3.json", "pmc_k_match_c3_s8192.json"):
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            d = json.load(f)
+        assert d["hbm_bytes_per_launch"] > 0
+        for k, v in d["per_kernel_derived"].items():
+            assert 0.0 <= v["occupancy_frac"] <= 1.0, (name, k)
+
+
+def test_bench_byte_model():
+    import types
+    sys.path.insert(0, ROOT)
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    ns = {}
+    start = src.index("def algorithmic_bytes")
+    end = src.index("\n\n\n", start)
+    exec(src[start:end], ns)
+    st = types.SimpleNamespace(n_inputs=10, n_trades=3, n_rests=4, n_maker_visits=3, n_cancel_ok=2)
+    assert ns["algorithmic_bytes"](st) == 52 * 10 + 36 * 3 + 32 * 4 + 32 * 3 + 48 * 2
