@@ -1911,6 +1911,7 @@ constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBL
 #ifndef KME_LANE_GROUPS
 #define KME_LANE_GROUPS 32
 #endif
+constexpr int LANE_TCH = 8;       // trade scratch slots a lane reserves at a time
 constexpr int LANE_GROUPS = KME_LANE_GROUPS;   // groups per wavefront (the other lanes idle): two
                                   // wavefronts per SIMD at 65,536 groups, so one issues while the other waits
 static_assert(LANE_GROUPS >= 1 && LANE_GROUPS <= 64, "k_match_lanes: one group per lane");
@@ -1927,6 +1928,7 @@ struct GroupLane {
     int32_t exists, free_head, chunk_next, chunk_end, fsp;
     uint32_t cur;
     bool dead;
+    size_t tpos, tlim;            // this lane's reserved trade scratch [tpos, tlim) (LANE_TCH at a time)
 
     KDEV GroupLane(const DevState& s, const EpochIO& e, int32_t (*f)[64], int32_t gg)
         : S(s), io(e), fs(f), tsh(s.tsh + (size_t)(blockIdx.x & (TSHARDS - 1)) * CTR_STRIDE),
@@ -1934,6 +1936,7 @@ struct GroupLane {
         b0l = b0m = b1l = b1m = 0;
         exists = 0; free_head = -1; chunk_next = chunk_end = 0; fsp = 0;
         cur = 0; dead = false;
+        tpos = tlim = 0;
     }
     KDEV void die(int status, int detail) { raise_thread(S.ctr, status, detail, (int64_t)cur); dead = true; }
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
@@ -1949,6 +1952,7 @@ struct GroupLane {
         exists = c.x; free_head = c.y; chunk_next = c.z; chunk_end = c.w;
     }
     KDEV void store_group() {
+        while (tpos < tlim) mark_hole(tpos++);               // the reservation's unused slots
         while (fsp > 0) spill_block(fsp > FBLK ? fsp - FBLK : 0);
         KG int4* gs = reinterpret_cast<KG int4*>(&S.grp[g]);
         gs[0] = make_int4(lo32((int64_t)b0l), hi32((int64_t)b0l), lo32((int64_t)b0m), hi32((int64_t)b0m));
@@ -2009,22 +2013,40 @@ struct GroupLane {
         fs[fsp++][lane] = s;
     }
 
-    // ---------------- trades: one TradeTmp per trade, reserved per wavefront step
-    KDEV void emit(uint32_t ord, int64_t moid, int64_t maid, int32_t msneg, int32_t mprice, int32_t ts) {
-        const unsigned long long act = __ballot(1);
-        const int leader = __ffsll((long long)act) - 1;
-        const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1));
+    // ---------------- trades: one TradeTmp per trade.  Each lane reserves LANE_TCH slots at a time
+    // (one atomic per wavefront for the lanes that run out), so most trades need no returning
+    // atomic on the record's chain; unused slots are holes (seq = -1) that k_scatter skips.
+    KDEV void mark_hole(size_t pos) {
+        reinterpret_cast<KG int2*>(&S.ttmp[pos])[4] = make_int2(-1, 0);
+    }
+    KDEV void refill_trades() {
+        const unsigned long long need = __ballot(1);
+        const int leader = __ffsll((long long)need) - 1;
+        const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1));
         unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(&tsh[TS_USED], (unsigned long long)__popcll(act));
-        base = (unsigned long long)__shfl((long long)base, leader) + rank;
-        size_t pos;
-        if (base < S.tshard_cap) {
-            pos = (size_t)tbase + base;
-        } else {
-            const unsigned long long ob = atomicAdd(&S.ctr[ci(C_TTMP)], 1ull);
-            if (ob >= S.ttmp_cap) { die(KME_E_CAPACITY, KME_D_CAP_TRADES); return; }
-            pos = (size_t)TSHARDS * S.tshard_cap + ob;
+        if (lane == leader) base = atomicAdd(&tsh[TS_USED], (unsigned long long)LANE_TCH * __popcll(need));
+        base = (unsigned long long)__shfl((long long)base, leader) + (unsigned long long)rank * LANE_TCH;
+        if (base + LANE_TCH <= S.tshard_cap) {
+            tpos = (size_t)tbase + base;
+            tlim = tpos + LANE_TCH;
+            return;
         }
+        for (unsigned long long q = base; q < S.tshard_cap; ++q) mark_hole((size_t)tbase + q);   // straddles the end
+        const unsigned long long ob = atomicAdd(&S.ctr[ci(C_TTMP)], (unsigned long long)LANE_TCH);
+        if (ob + LANE_TCH > S.ttmp_cap) {
+            for (unsigned long long q = ob; q < S.ttmp_cap; ++q) mark_hole((size_t)TSHARDS * S.tshard_cap + q);
+            die(KME_E_CAPACITY, KME_D_CAP_TRADES);
+            return;
+        }
+        tpos = (size_t)TSHARDS * S.tshard_cap + ob;
+        tlim = tpos + LANE_TCH;
+    }
+    KDEV void emit(uint32_t ord, int64_t moid, int64_t maid, int32_t msneg, int32_t mprice, int32_t ts) {
+        if (tpos == tlim) {
+            refill_trades();
+            if (dead) return;
+        }
+        const size_t pos = tpos++;
         const int64_t msid = msneg ? -(int64_t)g : (int64_t)g;
         KG int4* r = reinterpret_cast<KG int4*>(&S.ttmp[pos]);
         KG int2* r2 = reinterpret_cast<KG int2*>(&S.ttmp[pos]);
