@@ -3,23 +3,30 @@
 
 One step = one epoch of E input records through the whole device pipeline (oid map, funded-ledger
 proof, cancel routing, radix partition by symbol group, per-group matching, trade compaction,
-oid-table upkeep, top-of-book snapshot; + an RCCL all-gather of top-of-book when N > 1).
+oid-table upkeep, top-of-book snapshot; + the RCCL all-gather of the snapshots when N > 1).
 Inputs are resident in HBM before the timed region; outputs stay in HBM.
 
 Default workload: the metric's own configuration, C3 (BASELINE.json configs[2]):
-65,536 symbols symbol-sharded over the N ranks (65,536 / N symbols per GPU, so every N measures the
-same 65,536-symbol universe and N = 8 is exactly C3), 65,536 accounts, uniform limit / cancel
-orders; every rank processes its own stream, E = 2^22 records per epoch and step (per-GPU work per
-step is fixed: "weak" in records).  No collective in the data path; the top-of-book snapshot is
-all-gathered over RCCL per epoch.  --workload c2 runs configs[1] (1,024 symbols per GPU).
+one universe of 65,536 symbols keyed over the N ranks by Kafka's partitioner (murmur2 of the
+decimal sid, ``kme_shard_of``), so rank r matches the records of its own ~65,536 / N
+symbols -- N = 8 is exactly C3.  65,536 accounts, each funded on every rank with 1/N of its credit
+(``credit_shards``).  Every rank processes E = 2^22 records per step (per-GPU work per step is
+fixed: "weak" scaling in records).  No collective in the data path; the ranks' top-of-book
+snapshots (16 B per symbol, their own symbols only) are all-gathered over RCCL every epoch and
+checked against each rank's own snapshot after the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--epoch E] [--workload c3|c2|c4|c5]
+
+``--gpus N`` > 1 outside a torch.distributed launcher starts the N ranks itself (torchrun as a
+child process; this parent never touches the GPU) and exits with their status.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,14 +35,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kafka-matching-engine_amd"))
 
-if "--stamps" in sys.argv:  # diagnostic build with in-kernel s_memtime stamps (never the bench line)
-    os.environ["KME_LIB"] = os.path.join(ROOT, "kafka-matching-engine_amd", "kme", "libkme_stamps.so")
-
-import torch  # noqa: E402  (first: one HIP runtime per process, see kme.lib)
-import torch.distributed as dist  # noqa: E402
-
-import kme  # noqa: E402
-from kme import workloads as W  # noqa: E402
+from kme import workloads as W  # noqa: E402  (numpy only: no HIP runtime is loaded here)
 
 METRIC = "matched orders/sec (node) at 65,536 symbols; p99 epoch latency; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
@@ -50,31 +50,48 @@ def algorithmic_bytes(st) -> int:
             + 48 * st.n_cancel_ok)
 
 
+def rank_symbols(name: str, world: int, rank: int, symbols: int = 0) -> np.ndarray:
+    """The symbol ids rank `rank` owns: for the 65,536-symbol configurations (c3, c4) its murmur2
+    partition of the universe; c2 / c5 (and the --symbols diagnostic) are per-GPU configurations
+    of their own symbols 1..n."""
+    if name in ("c3", "c4") and not symbols:
+        return W.shard_symbols(C3_SYMBOLS, world, rank)
+    n = symbols or 1024
+    return np.arange(1, n + 1, dtype=np.int64)
+
+
 def make_workload(name: str, n_orders: int, rank: int, world: int, symbols: int = 0, mix=None):
+    """(setup, stream, sids, accounts, description) of rank `rank`: its records of the configuration."""
     seed = 1000 + rank
     mix = tuple(mix) if mix else (0.34, 0.33, 0.33)
+    sids = rank_symbols(name, world, rank, symbols)
+    oid_base = 1 + rank * n_orders   # disjoint oid ranges: every oid is unique across the ranks
+    keyed = name in ("c3", "c4") and not symbols
+    shards = world if keyed else 1
     if name == "c2":
-        nsym, nacc = 1024, 4096
-        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed, mix=mix)
+        nacc = 4096
+        stream = W.uniform(n_orders, n_accounts=nacc, seed=seed, mix=mix, symbols=sids, oid_base=oid_base)
         desc = "C2: 1,024 symbols x 16M uniform limit/cancel orders per GPU (BASELINE configs[1])"
     elif name == "c3":
-        nsym, nacc = (symbols or C3_SYMBOLS // world), C3_ACCOUNTS
-        stream = W.uniform(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed, mix=mix)
-        desc = (f"C3: 65,536 symbols symbol-sharded over {world} GPU(s) = {nsym:,} symbols per GPU, "
-                f"uniform limit/cancel orders (BASELINE configs[2])")
+        nacc = C3_ACCOUNTS
+        stream = W.uniform(n_orders, n_accounts=nacc, seed=seed, mix=mix, symbols=sids, oid_base=oid_base)
+        desc = (f"C3: 65,536 symbols keyed (murmur2) over {world} GPU(s), {len(sids):,} symbols on rank {rank}, "
+                f"uniform limit/cancel orders (BASELINE configs[2])" if keyed else
+                f"C3 diagnostic: {len(sids):,} symbols per GPU, uniform limit/cancel orders")
     elif name == "c4":
-        nsym, nacc = C3_SYMBOLS // world, C3_ACCOUNTS
-        stream = W.zipf(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
-        desc = f"C4: Zipf(1.1) symbol popularity, 65,536 symbols over {world} GPU(s), 21-level band"
+        nacc = C3_ACCOUNTS
+        stream = W.zipf(n_orders, n_symbols=C3_SYMBOLS, n_accounts=nacc, seed=seed, oid_base=oid_base,
+                        shard=(rank, world))
+        desc = f"C4: Zipf(1.1) symbol popularity over 65,536 symbols keyed over {world} GPU(s), 21-level band"
     elif name == "c5":
-        nsym, nacc = 1024, 4096
-        stream = W.cancel_replace(n_orders, n_symbols=nsym, n_accounts=nacc, seed=seed)
+        nacc = 4096
+        stream = W.cancel_replace(n_orders, n_symbols=len(sids), n_accounts=nacc, seed=seed, oid_base=oid_base)
         desc = "C5: 90% cancel/replace + 10% sweeping orders of 5k-50k, 1,024 symbols per GPU"
     else:
         raise SystemExit(f"unknown workload {name}")
-    setup = W.funded_setup(nacc, range(1, nsym + 1),
-                           transfers_per_account=W.funded_transfers_needed(n_orders, nacc, big=name == "c5"))
-    return setup, stream, nsym, nacc, desc
+    need = W.funded_transfers_needed(n_orders, nacc, big=name == "c5")
+    setup = W.funded_setup(nacc, sids, transfers_per_account=need * shards)
+    return setup, stream, sids, nacc, shards, desc
 
 
 def cpu_baseline(setup, stream, max_orders: int):
@@ -96,14 +113,70 @@ def cpu_baseline(setup, stream, max_orders: int):
                       f"C restatement of KProcessor.MatchingEngine with hash-map stores, {dt:.1f} s"}
 
 
-def main():
+def _free_port() -> int:
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(gpus: int) -> int:
+    """--gpus N > 1 without a launcher: the N ranks as a torchrun child process.  Called before
+    anything initialises HIP (no torch.cuda call, libkme not loaded), so nothing here is replaced
+    by exec; the parent only waits and returns the ranks' exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def market_data_layout(world: int, name: str, symbols: int = 0):
+    """(rows per rank in the all-gathered snapshot, symbols of each rank): every rank pads its
+    snapshot to the largest partition so the all-gather is one equal-sized block per rank."""
+    per_rank = [rank_symbols(name, world, r, symbols) for r in range(world)]
+    return max(len(p) for p in per_rank), per_rank
+
+
+def exchange_market_data(dist, tob_local, tob_all):
+    """The per-epoch market-data collective: every rank's top-of-book rows -> every rank (RCCL
+    over xGMI on the GPU ranks; gloo in the CPU tests of this glue and in the one-GPU rehearsal,
+    where device tensors go through host copies)."""
+    if tob_local.is_cuda and dist.get_backend() == "gloo":
+        host = tob_all.cpu()
+        dist.all_gather_into_tensor(host, tob_local.cpu())
+        tob_all.copy_(host)
+        return
+    dist.all_gather_into_tensor(tob_all, tob_local)
+
+
+def verify_market_data(tob_all, tob_local, rank: int, rows: int) -> bool:
+    """After the all-gather, block `rank` of every rank's copy is this rank's own snapshot."""
+    return bool((tob_all[rank * rows:(rank + 1) * rows] == tob_local).all().item())
+
+
+def reduce_stats(dist, torch, elapsed: float, n_orders: int, n_trades: int, ok: bool, device):
+    """Whole-job figures: the slowest rank's time (MAX) and the records / trades of all ranks (SUM),
+    the market-data check of every rank (MIN)."""
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    sums = torch.tensor([float(n_orders), float(n_trades)], dtype=torch.float64, device=device)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.get_backend() == "gloo":
+            t, sums, flag = t.cpu(), sums.cpu(), flag.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return float(t.item()), float(sums[0].item()), float(sums[1].item()), bool(flag.item())
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epoch", type=int, default=1 << 22)
     ap.add_argument("--workload", default="c3")
-    ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default 65,536 / N)")
+    ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default: the murmur2 partition of 65,536)")
     ap.add_argument("--mix", default="", help="diagnostic: BUY,SELL,CANCEL fractions of the c2/c3 stream")
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--max-resting", type=int, default=0,
@@ -115,24 +188,50 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
     ap.add_argument("--serialize", action="store_true",
                     help="also print each epoch's MatchOut tape on the GPU (kme_tape_json_device) inside the step")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.stamps:  # diagnostic build with in-kernel s_memtime stamps (never the bench line)
+        os.environ["KME_LIB"] = os.path.join(ROOT, "kafka-matching-engine_amd", "kme", "libkme_stamps.so")
+
+    import torch
+    import torch.distributed as dist
+
+    import kme
+
+    # KME_BENCH_REHEARSAL=1 (diagnostic, never a bench line): every rank on GPU 0 with gloo
+    # collectives, to rehearse the N-rank path on a one-GPU box
+    rehearsal = os.environ.get("KME_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local_rank)
 
     E = args.epoch
     total = max(args.orders, (args.warmup + args.steps) * E)
-    setup, stream, nsym, nacc, desc = make_workload(args.workload, total, rank, world, args.symbols,
-                                                   [float(x) for x in args.mix.split(",")] if args.mix else None)
+    setup, stream, sids, nacc, shards, desc = make_workload(
+        args.workload, total, rank, world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
+    max_sid = int(sids.max())
 
-    cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=E,
+    cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=max_sid + 1, max_epoch=E,
                              max_resting=args.max_resting or min(total, 1 << 30), max_trades=2 * E + (1 << 16),
                              max_accounts=nacc, device=local_rank, light_max=args.light_max)
+    cfg.credit_shards = shards
     eng = kme.Engine(cfg)
     stream_handle = torch.cuda.current_stream(dev).cuda_stream
     eng.set_stream(stream_handle)
@@ -146,8 +245,11 @@ def main():
         "price": torch.from_numpy(stream.price).to(dev), "size": torch.from_numpy(stream.size).to(dev),
     }
     orders_per_epoch = [int(stream.slice(k * E, (k + 1) * E).n_orders()) for k in range(args.warmup + args.steps)]
-    tob = torch.zeros((nsym + 1, 4), dtype=torch.int32, device=dev)
-    tob_all = torch.zeros((world * (nsym + 1), 4), dtype=torch.int32, device=dev) if world > 1 else None
+    # market data: this rank's symbols' top of book, all-gathered (16 B per symbol)
+    rows, per_rank = market_data_layout(world, args.workload, args.symbols)
+    groups = torch.from_numpy(sids.astype(np.int32)).to(dev)
+    tob = torch.full((rows, 4), -1, dtype=torch.int32, device=dev)
+    tob_all = torch.zeros((world * rows, 4), dtype=torch.int32, device=dev)
 
     def epoch_ptrs(k):
         return {name: t.data_ptr() + k * E * t.element_size() for name, t in cols.items()}
@@ -157,9 +259,9 @@ def main():
 
     def run_epoch(k):
         eng.submit_device(epoch_ptrs(k), E)
-        eng.top_of_book(tob.data_ptr())
+        eng.top_of_book_groups(groups.data_ptr(), len(sids), tob.data_ptr())
         if world > 1:
-            dist.all_gather_into_tensor(tob_all, tob)  # market-data snapshot over RCCL / xGMI
+            exchange_market_data(dist, tob, tob_all)   # market-data snapshot over RCCL / xGMI
         st = eng.wait()
         if args.serialize:  # MatchOut text of the epoch, printed on the GPU, left in HBM
             tape_bytes.append(eng.tape_json_device_into(epoch_ptrs(k), E, tape_buf.data_ptr(), tape_buf.numel()))
@@ -194,10 +296,19 @@ def main():
     elapsed = t1 - t0
     assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
 
+    # market data check (outside the timed region): this rank's rows of the full-range snapshot,
+    # its own compact snapshot, and its block of the all-gathered one agree
+    full = torch.zeros((max_sid + 1, 4), dtype=torch.int32, device=dev)
+    eng.top_of_book(full.data_ptr())
+    torch.cuda.synchronize(dev)
+    md_ok = bool((full[groups.long()] == tob[:len(sids)]).all().item()) and bool((tob[:len(sids), 0] >= 0).any().item())
+    if world > 1:
+        md_ok = md_ok and verify_market_data(tob_all, tob, rank, rows)
+
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
-        rows = eng.debug_counters().astype(np.float64).reshape(-1, 32)
-        hot = int(np.argmax(rows[:, 7]))   # the group with the most k_match cycles (C4: the hot symbol)
-        d = rows[hot] if os.environ.get("KME_STAMPS_HOT") else rows.sum(axis=0)
+        rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 32)
+        hot = int(np.argmax(rows_[:, 7]))   # the group with the most k_match cycles (C4: the hot symbol)
+        d = rows_[hot] if os.environ.get("KME_STAMPS_HOT") else rows_.sum(axis=0)
         names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",
                  "n_trade_rec", "n_rest_rec", "n_cancel_rec", "maker_wait", "n_maker", "victim_wait", "n_victim",
                  "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre"]
@@ -218,15 +329,8 @@ def main():
         per["group"] = hot if os.environ.get("KME_STAMPS_HOT") else "all"
         print(json.dumps({"stamps": per}), flush=True)
         return
-    stats = torch.tensor([elapsed, float(n_orders), float(n_trades)], dtype=torch.float64, device=dev)
-    if world > 1:
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        sums = stats[1:].clone()
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed, n_orders_all, n_trades_all = float(t_max.item()), float(sums[0].item()), float(sums[1].item())
-    else:
-        n_orders_all, n_trades_all = float(n_orders), float(n_trades)
+    elapsed, n_orders_all, n_trades_all, md_all = reduce_stats(dist if world > 1 else None, torch, elapsed,
+                                                              n_orders, n_trades, md_ok, dev)
 
     if rank == 0:
         avg_match_s = float(np.mean(match_ms)) / 1e3
@@ -252,13 +356,17 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
-            "config": {"workload": desc, "symbols_per_gpu": nsym, "accounts": nacc, "epoch_records": E,
+            "config": {"workload": desc, "symbols_per_gpu_rank0": int(len(sids)), "accounts": nacc, "epoch_records": E,
                        "stream_records_per_gpu": total, "mode": "FUNDED (symbol groups in parallel)",
-                       "parallelism": f"symbol-sharded x{world}"},
+                       "parallelism": f"symbol-keyed x{world} (murmur2, Kafka's keyed partitioner)",
+                       "credit_shards": shards},
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
+            "market_data": {"symbols": int(sum(len(p) for p in per_rank)), "bytes_per_epoch": int(world * rows * 16),
+                            "collective": "RCCL all_gather_into_tensor per epoch" if world > 1 else "none (N = 1)",
+                            "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "
@@ -279,6 +387,8 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if not md_all:
+        raise SystemExit("bench.py: the all-gathered market data does not match the ranks' own snapshots")
 
 
 if __name__ == "__main__":

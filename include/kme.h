@@ -212,6 +212,11 @@ void kme_free(void* p);
  * Bid = highest price in book +g, ask = lowest price in book -g (book 0 is shared). */
 typedef struct kme_tob { int32_t bid_px, ask_px, bid_qty, ask_qty; } kme_tob;
 kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out);
+/* The same for a list of groups (device array of n group ids, e.g. the symbols of this engine's
+ * partition): dev_out[k] = top of book of dev_groups[k] (-1 / 0 for an id >= max_symbols).  With
+ * symbols keyed over N engines this is the engine's share of the market-data snapshot that
+ * bench.py all-gathers over RCCL. */
+kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uint32_t n, kme_tob* dev_out);
 
 /* Wall-clock (HIP event) duration in ms of each kernel phase of the last epoch; index by name
  * (kme_phase_names).  Used by bench.py for the roofline of the dominant kernel. */

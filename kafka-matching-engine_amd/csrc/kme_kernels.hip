@@ -2582,9 +2582,7 @@ __global__ void __launch_bounds__(256) k_otab_refill(DevState S, uint32_t nslots
 }
 
 // ------------------------------------------------------------------ market data: top of book
-__global__ void k_tob(DevState S, kme_tob* out) {
-    const int32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= S.G) return;
+KDEV kme_tob tob_of(const DevState& S, int32_t g) {
     const GroupState gs = S.grp[g];
     kme_tob r{-1, -1, 0, 0};
     if (gs.exists) {
@@ -2606,7 +2604,18 @@ __global__ void k_tob(DevState S, kme_tob* out) {
             r.ask_qty = (int32_t)(q > INT32_MAX ? INT32_MAX : q);
         }
     }
-    out[g] = r;
+    return r;
+}
+__global__ void k_tob(DevState S, kme_tob* out) {
+    const int32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < S.G) out[g] = tob_of(S, g);
+}
+// The snapshot of a list of groups (a shard's own symbols): out[k] = top of book of groups[k].
+__global__ void k_tob_groups(DevState S, const uint32_t* groups, uint32_t n, kme_tob* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t g = groups[k];
+    out[k] = g < (uint32_t)S.G ? tob_of(S, (int32_t)g) : kme_tob{-1, -1, 0, 0};
 }
 
 __global__ void k_init_state(DevState S) {
@@ -2713,6 +2722,10 @@ void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st)
 }
 void launch_tob(const DevState& S, void* out, hipStream_t st) {
     hipLaunchKernelGGL(k_tob, dim3(cdiv((uint32_t)S.G, 256)), dim3(256), 0, st, S, (kme_tob*)out);
+}
+void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_tob_groups, dim3(cdiv(n, 256)), dim3(256), 0, st, S, groups, n, (kme_tob*)out);
 }
 void launch_init_state(const DevState& S, hipStream_t st) {
     const uint32_t n = (uint32_t)(S.G > S.A ? S.G : S.A);

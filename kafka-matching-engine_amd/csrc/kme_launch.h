@@ -41,6 +41,7 @@ void launch_ser_write(const kme_orders& in, const kme_epoch_result& r, uint32_t 
 // maintenance
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st);   // pool slots [0, used) hold every node
 void launch_tob(const DevState& S, void* out, hipStream_t st);
+void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st);
 void launch_init_state(const DevState& S, hipStream_t st);
 
 }  // namespace kme

@@ -684,6 +684,13 @@ kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out) {
     return KME_OK;
 }
 
+kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uint32_t n, kme_tob* dev_out) {
+    if (!e || (n && (!dev_groups || !dev_out))) return KME_E_INVALID;
+    launch_tob_groups(e->S, dev_groups, n, dev_out, e->stream);
+    HIP_TRY(hipGetLastError());
+    return KME_OK;
+}
+
 // ------------------------------------------------------------------ snapshots
 static char* dup_string(const std::string& s, size_t* len) {
     char* p = (char*)std::malloc(s.size() + 1);

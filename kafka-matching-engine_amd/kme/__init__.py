@@ -67,7 +67,7 @@ COMMIT_FN = C.CFUNCTYPE(None, C.c_void_p)
 EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
-    "kme_top_of_book", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
+    "kme_top_of_book", "kme_top_of_book_groups", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
     "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
@@ -105,6 +105,7 @@ def lib():
         "kme_snapshot_ledger": (st, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
         "kme_free": (None, [vp]),
         "kme_top_of_book": (st, [vp, vp]),
+        "kme_top_of_book_groups": (st, [vp, vp, u32, vp]),
         "kme_phase_times": (st, [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
         "kme_phase_name": (C.c_char_p, [C.c_int]),
         "kme_enable_timing": (st, [vp, C.c_int]),
@@ -276,6 +277,12 @@ class Engine:
         rc = self._L.kme_top_of_book(self._h, C.c_void_p(int(dev_ptr)))
         if rc:
             raise KmeError(rc, "kme_top_of_book")
+
+    def top_of_book_groups(self, groups_ptr: int, n: int, dev_ptr: int):
+        """kme_top_of_book_groups: the snapshot of n groups (a device u32 array) into dev_ptr."""
+        rc = self._L.kme_top_of_book_groups(self._h, C.c_void_p(int(groups_ptr)), int(n), C.c_void_p(int(dev_ptr)))
+        if rc:
+            raise KmeError(rc, "kme_top_of_book_groups")
 
     def _text(self, fn) -> str:
         p = C.c_void_p()

@@ -11,6 +11,7 @@ action i32, oid i64, aid i64, sid i64, price i32, size i32.
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 from dataclasses import dataclass, field
@@ -241,17 +242,41 @@ def _cancel_targets(action, aid, oid, rng) -> np.ndarray:
     return out
 
 
+@functools.lru_cache(maxsize=16)
+def _shard_assignment(n_symbols: int, n_shards: int, sid_base: int) -> bytes:
+    return np.array([shard_of(s, n_shards) for s in range(sid_base, sid_base + n_symbols)], np.int64).tobytes()
+
+
+def shard_assignment(n_symbols: int, n_shards: int, sid_base: int = 1) -> np.ndarray:
+    """Partition of each sid sid_base .. sid_base + n_symbols - 1 under Kafka's keyed partitioner
+    (murmur2 of the decimal |sid|, ``shard_of``)."""
+    if n_shards <= 1:
+        return np.zeros(n_symbols, np.int64)
+    return np.frombuffer(_shard_assignment(n_symbols, n_shards, sid_base), np.int64).copy()
+
+
+def shard_symbols(n_symbols: int, n_shards: int, shard: int, sid_base: int = 1) -> np.ndarray:
+    """The sids of partition ``shard`` of ``n_shards`` (``shard_assignment``), ascending."""
+    sids = np.arange(sid_base, sid_base + n_symbols, dtype=np.int64)
+    return sids[shard_assignment(n_symbols, n_shards, sid_base) == shard]
+
+
 def uniform(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: int = 1,
             sid_base: int = 1, aid_base: int = 0, oid_base: int = 1, price_lo: int = 30,
-            price_hi: int = 75, mix=(0.34, 0.33, 0.33)) -> Orders:
+            price_hi: int = 75, mix=(0.34, 0.33, 0.33), symbols: np.ndarray | None = None) -> Orders:
     """C2/C3: 34/33/33 BUY/SELL/CANCEL, sid uniform, price uniform [30,75] (the
     H5-safe band), size floor(N(50,10)) clamped to [1,100], cancels of an earlier oid of the same
-    account."""
+    account.  ``symbols``: draw sids uniformly from this set instead of sid_base + [0, n_symbols)
+    (a murmur2 shard of a larger universe, ``shard_symbols``); the same draws otherwise."""
     rng = np.random.Generator(np.random.PCG64(seed))
     u = rng.random(n_orders)
     action = np.where(u < mix[0], BUY, np.where(u < mix[0] + mix[1], SELL, CANCEL)).astype(np.int32)
     aid = rng.integers(0, n_accounts, n_orders).astype(np.int64) + aid_base
-    sid = rng.integers(0, n_symbols, n_orders).astype(np.int64) + sid_base
+    if symbols is None:
+        sid = rng.integers(0, n_symbols, n_orders).astype(np.int64) + sid_base
+    else:
+        symbols = np.asarray(symbols, np.int64)
+        sid = symbols[rng.integers(0, len(symbols), n_orders)]
     price = rng.integers(price_lo, price_hi + 1, n_orders).astype(np.int32)
     size = np.clip(np.floor(rng.normal(50, 10, n_orders)), 1, 100).astype(np.int32)
     oid = _unique_oids(n_orders, oid_base)
@@ -265,9 +290,11 @@ def uniform(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: 
 
 def zipf(n_orders: int, n_symbols: int = 65536, n_accounts: int = 65536, s: float = 1.1,
          seed: int = 1, sid_base: int = 1, aid_base: int = 0, oid_base: int = 1,
-         price_lo: int = 40, price_hi: int = 60) -> Orders:
+         price_lo: int = 40, price_hi: int = 60, shard: tuple[int, int] = (0, 1)) -> Orders:
     """C4: Zipf(s) symbol popularity; a narrow price band keeps hot books deep (~1e4 resting
-    orders over <= 21 levels) -- the reference's book has at most 127 levels."""
+    orders over <= 21 levels) -- the reference's book has at most 127 levels.
+    ``shard`` = (k, n): only the symbols of murmur2 partition k of n, with their popularity in
+    the whole universe (the records of partition k of one Zipf stream over ``n_symbols``)."""
     o = uniform(n_orders, n_symbols, n_accounts, seed, sid_base, aid_base, oid_base, price_lo, price_hi,
                 mix=(0.36, 0.36, 0.28))
     rng = np.random.Generator(np.random.PCG64(seed + 7919))
@@ -275,6 +302,10 @@ def zipf(n_orders: int, n_symbols: int = 65536, n_accounts: int = 65536, s: floa
     p = ranks ** (-s)
     p /= p.sum()
     perm = rng.permutation(n_symbols)  # hot symbols spread over the id space
+    if shard[1] > 1:
+        keep = np.isin(perm + sid_base, shard_symbols(n_symbols, shard[1], shard[0], sid_base))
+        p = np.where(keep, p, 0.0)
+        p /= p.sum()
     draw = rng.choice(n_symbols, size=n_orders, p=p)
     sid = perm[draw].astype(np.int64) + sid_base
     o.sid = np.where(o.action == CANCEL, 0, sid)

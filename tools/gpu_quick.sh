@@ -18,6 +18,6 @@ python3 - $OUT/bench.jsonl <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
     d = json.loads(l)
-    print(d["config"]["symbols_per_gpu"], d["config"]["epoch_records"], round(d["value"] / 1e6, 1), "M/s p99",
+    print(d["config"]["symbols_per_gpu_rank0"], d["config"]["epoch_records"], round(d["value"] / 1e6, 1), "M/s p99",
           round(d["p99_epoch_ms"], 2), d["phase_ms_last_epoch"])
 PY
