@@ -233,8 +233,13 @@ def main():
                              max_accounts=nacc, device=local_rank, light_max=args.light_max)
     cfg.credit_shards = shards
     eng = kme.Engine(cfg)
-    stream_handle = torch.cuda.current_stream(dev).cuda_stream
-    eng.set_stream(stream_handle)
+    # one explicit stream for the engine and every torch / collective op of this rank, so they are
+    # ordered (the default stream's handle is 0, which would leave the engine on its own
+    # non-blocking stream, unordered with the all-gather's reads of the snapshot)
+    work = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(work)
+    assert work.cuda_stream != 0
+    eng.set_stream(work.cuda_stream)
     eng.enable_timing(True)
     eng.process(setup)  # CREATE_BALANCE / TRANSFER / ADD_SYMBOL records (host path)
 
@@ -301,9 +306,12 @@ def main():
     full = torch.zeros((max_sid + 1, 4), dtype=torch.int32, device=dev)
     eng.top_of_book(full.data_ptr())
     torch.cuda.synchronize(dev)
-    md_ok = bool((full[groups.long()] == tob[:len(sids)]).all().item()) and bool((tob[:len(sids), 0] >= 0).any().item())
-    if world > 1:
-        md_ok = md_ok and verify_market_data(tob_all, tob, rank, rows)
+    md_local = bool((full[groups.long()] == tob[:len(sids)]).all().item()) and bool((tob[:len(sids), 0] >= 0).any().item())
+    md_gather = verify_market_data(tob_all, tob, rank, rows) if world > 1 else True
+    md_ok = md_local and md_gather
+    if not md_ok:
+        print(f"rank {rank}: market data check failed (own snapshot vs full-range: {md_local}, "
+              f"all-gathered block: {md_gather})", file=sys.stderr, flush=True)
 
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
         rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 32)

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 3
+#define KME_ABI_VERSION 4
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -36,7 +36,11 @@ typedef enum kme_status {
     KME_E_DOMAIN = 3,       /* input where the reference throws (NPE) or never terminates, or that
                                falls outside the documented parity domain (detail: kme_domain) */
     KME_E_UNFUNDED = 4,     /* FUNDED mode: acceptance of some order is not provably
-                               independent of the ledger (see kme_mode) */
+                               independent of the ledger (see kme_mode).  NOT fatal: the records
+                               before kme_epoch_status.n_effective took effect, nothing after them
+                               did (an order epoch whose proof fails: none of it), and the engine
+                               accepts further epochs -- e.g. after TRANSFER records that top the
+                               accounts up, the refused records can be resubmitted. */
     KME_E_UNSUPPORTED = 5,  /* operation not available in this mode (PAYOUT of an absent symbol in
                                FUNDED mode needs the positions ledger) */
     KME_E_HIP = 6,          /* HIP runtime error */
@@ -147,17 +151,22 @@ typedef struct kme_epoch_result {
     uint32_t trades_cap;
 } kme_epoch_result;
 
+/* On an error the records [0, n_effective) of the submission took effect exactly as the reference
+ * would have processed them, and their results are valid (out_* [0, n_effective),
+ * trade_off[0 .. n_effective], trades[0 .. trade_off[n_effective])): the reference forwards and
+ * commits every record before the one that throws (KP:97, 124-125).  Nothing from the faulting
+ * record on is answered.  Every error except KME_E_UNFUNDED leaves the engine failed. */
 typedef struct kme_epoch_status {
     int32_t status;        /* kme_status of the epoch */
     int32_t detail;        /* kme_domain */
-    int64_t error_index;   /* input index of the first fault, or -1 */
+    int64_t error_index;   /* input index of the first fault, or -1 (a fault of the epoch as a whole) */
     uint32_t n_inputs;
     uint32_t n_trades;
     uint64_t n_orders;     /* BUY/SELL/CANCEL records (headline metric unit) */
     uint64_t n_rests, n_maker_visits, n_cancel_ok;
     uint32_t serial_fallback;   /* epochs (device sub-epochs of kme_submit_epoch) that ran serially
                                    under KME_FLAG_SERIAL_FALLBACK */
-    uint32_t _pad;
+    uint32_t n_effective;       /* records of the submission that took effect (= n_inputs when OK) */
 } kme_epoch_status;
 
 typedef struct kme_engine kme_engine;

@@ -93,6 +93,16 @@ KDEV void raise_wave(unsigned long long* ctr, int status, int detail, int64_t id
 KDEV bool failed(const unsigned long long* ctr) {
     return __hip_atomic_load(&ctr[ci(C_ERR)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ~0ull;
 }
+// The records of the epoch that still take effect: every record before the first fault raised so
+// far (the reference forwards and commits each record before the one that throws, KP:97, 124-125);
+// none after a fault of the epoch as a whole (no index: the funded proof, trade capacity).
+KDEV uint32_t err_limit(const unsigned long long* ctr, uint32_t n) {
+    const unsigned long long c = __hip_atomic_load(&ctr[ci(C_ERR)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == ~0ull) return n;
+    const unsigned long long ix = c >> 16;
+    if (ix == 0xFFFFFFFFFFFFull) return 0;
+    return ix < n ? (uint32_t)ix : n;
+}
 
 // ------------------------------------------------------------------ the book bit scans (KP:359-416)
 // getFirstSetBitPos / getLastSetBitPos compute (int)(Math.log10(x) / Math.log10(2)) in double.
@@ -336,11 +346,12 @@ KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int3
 // createBalance KP:131-138; transfer KP:140-146 with the balance replaced by the reservation
 // bound: a debit is accepted only when it provably passes, otherwise KME_E_UNFUNDED.
 __global__ void k_ledger_funded(DevState S, EpochIO io) {
-    if (S.ctr[ci(C_ACCT_OPS)] == 0 || failed(S.ctr)) return;
+    if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
+    const uint32_t lim = err_limit(S.ctr, io.n);
     const int lane = lane_id();
-    for (uint32_t base = 0; base < io.n; base += 64) {
+    for (uint32_t base = 0; base < lim; base += 64) {
         const uint32_t i = base + lane;
-        const int32_t a = i < io.n ? io.action[i] : -1;
+        const int32_t a = i < lim ? io.action[i] : -1;
         unsigned long long m = __ballot(a == CREATE_BALANCE || a == TRANSFER);
         while (m) {
             const int l = __builtin_ctzll(m);
@@ -390,19 +401,31 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
 }
 
 // FUNDED per-account proof: balance >= lb_start - need - debits >= 0 >= any single risk remaining,
-// i.e. every checkBalance (KP:177) of this epoch passes.  Then roll the bound forward.
+// i.e. every checkBalance (KP:177) of this epoch passes.  Otherwise the epoch runs serially
+// (KME_FLAG_SERIAL_FALLBACK) or is refused as a whole (KME_E_UNFUNDED, no index).
 __global__ void k_check_funded(DevState S, EpochIO io) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= S.A) return;
+    const int64_t need = S.acct_need[a];
+    if (need <= 0) return;
+    const int64_t lbs = S.acct_since[a] < io.seq_base ? S.acct_lb[a] : 0;
+    if (lbs - need - S.acct_negx[a] < 0) {
+        if (S.fallback) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull);   // k_serial takes the epoch
+        else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_NONE, -1);
+    }
+}
+// The bounds roll forward once the whole proof is in (a kernel boundary after k_check_funded):
+// lb = lb_start - need + transfers.  An epoch refused as a whole by the proof changes no bound
+// (nothing of it takes effect, so the caller can resubmit it: KME_E_UNFUNDED is not fatal).
+__global__ void k_commit_funded(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
     const int64_t need = S.acct_need[a], negx = S.acct_negx[a], xfer = S.acct_xfer[a];
     if (need == 0 && negx == 0 && xfer == 0) return;
+    const unsigned long long c = S.ctr[ci(C_ERR)];
+    const bool refused = c != ~0ull && (c & 0xFF) == KME_E_UNFUNDED && (c >> 16) == 0xFFFFFFFFFFFFull;
     const int64_t since = S.acct_since[a];
-    const int64_t lbs = since < io.seq_base ? S.acct_lb[a] : 0;
-    if (need > 0 && lbs - need - negx < 0) {
-        if (S.fallback) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull);   // k_serial takes the epoch
-        else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_NONE, -1);
-    }
-    if (since < io.seq_base + (int64_t)io.n) S.acct_lb[a] = lbs - need + xfer;
+    if (!refused && since < io.seq_base + (int64_t)io.n) S.acct_lb[a] = (since < io.seq_base ? S.acct_lb[a] : 0) - need + xfer;
     S.acct_need[a] = 0; S.acct_negx[a] = 0; S.acct_xfer[a] = 0;
 }
 
@@ -1778,14 +1801,16 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e || e - b <= (uint32_t)S.light_max) return;   // empty, or a light group (k_match_lanes)
-    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;
+    if (S.ctr[ci(C_FALLBACK)]) return;
+    const uint32_t lim = err_limit(S.ctr, iop->n);          // records from a fault on do not take effect
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
     w.load_group();
     KST(w.acc[ST_GROUP_IN] += stamp() - tk0;)
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
-    for (uint32_t k0 = b; k0 < e && !w.dead; k0 += 64) {
+    bool stop = false;
+    for (uint32_t k0 = b; k0 < e && !w.dead && !stop; k0 += 64) {
         KST(const unsigned long long tb0 = stamp();)
         const uint32_t k = k0 + lane;
         const bool valid = k < e;
@@ -1831,12 +1856,15 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         // once keeps the waitcnt pass from placing a vmcnt(0) at the loop header, which would make
         // every record wait for all stores of the record before it (stores share vmcnt on gfx9).
         __builtin_amdgcn_s_waitcnt(VMCNT0);
-        const int nb = (int)(e - k0 < 64 ? e - k0 : 64);
+        // the batch's records before the epoch's first fault (a group's records are in arrival order)
+        const int nb = (int)__popcll(__ballot(valid && B.i < lim));
+        stop = nb < (int)(e - k0 < 64 ? e - k0 : 64);
+        int done = nb;                // records of the batch that took effect (a fault ends the group)
         // per-record OUT fields collect in lane j of these registers; one store per field per batch
         int32_t o_act = 0, o_size = 0, o_plo = 0, o_phi = 0, o_ntr = 0;   // o_act: action | flags << 16
         KST(w.acc[ST_BATCH] += stamp() - tb0;)
 #pragma nounroll
-        for (int j = 0; j < nb && !w.dead; ++j) {
+        for (int j = 0; j < nb; ++j) {
             KST(const unsigned long long tr0 = stamp();)
             Rec r;
             r.i = (uint32_t)rl32((int32_t)B.i, j);
@@ -1850,6 +1878,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             r.lane = j;
             KST(w.acc[ST_REC_PICK] += stamp() - tr0;)
             const Out o = w.process(r, B);
+            if (w.dead) { done = j; break; }   // the faulting record is not answered
 #ifdef KME_STAMPS
             {
                 const unsigned long long dt = stamp() - tr0;
@@ -1870,9 +1899,9 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             o_ntr = me ? (int32_t)o.ntr : o_ntr;
             KST(w.acc[ST_REC_OUT] += stamp() - tr0;)
         }
-        n_rest += (uint32_t)__popcll(__ballot(lane < nb && ((o_act >> 16) & 2)));
-        n_cancel += (uint32_t)__popcll(__ballot(lane < nb && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
-        if (lane < nb && !w.dead) {   // one coalesced 32-B record per lane (k_unsort scatters them)
+        n_rest += (uint32_t)__popcll(__ballot(lane < done && ((o_act >> 16) & 2)));
+        n_cancel += (uint32_t)__popcll(__ballot(lane < done && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
+        if (lane < done) {   // one coalesced 32-B record per lane (k_unsort scatters them)
             KG int4* os = opaque_const(Sp).osort + 2 * (size_t)k;
             os[0] = make_int4((o_act & 0xFFFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 16), o_size, o_plo, o_phi);
             os[1] = make_int4(o_ntr, 0, 0, 0);
@@ -1911,7 +1940,7 @@ constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBL
 #ifndef KME_LANE_GROUPS
 #define KME_LANE_GROUPS 32
 #endif
-constexpr int LANE_TCH = 8;       // trade scratch slots a lane reserves at a time
+constexpr int LANE_TCH = kLaneTradeChunk;   // trade scratch slots a lane reserves at a time (sizing: kme_create)
 constexpr int LANE_GROUPS = KME_LANE_GROUPS;   // groups per wavefront (the other lanes idle): two
                                   // wavefronts per SIMD at 65,536 groups, so one issues while the other waits
 static_assert(LANE_GROUPS >= 1 && LANE_GROUPS <= 64, "k_match_lanes: one group per lane");
@@ -2188,7 +2217,8 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
     __shared__ int32_t fs[LFS][64];
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
-    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;
+    if (S.ctr[ci(C_FALLBACK)]) return;
+    const uint32_t lim = err_limit(S.ctr, io.n);             // records from a fault on do not take effect
     const int32_t g = (int32_t)(blockIdx.x * LANE_GROUPS + lane_id());
     uint32_t b = 0, e = 0;
     if (lane_id() < LANE_GROUPS && g < S.G) { b = S.seg[g]; e = S.seg[g + 1]; }
@@ -2205,6 +2235,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
         int4 n0 = S.prec[2 * (size_t)i_next], n1 = S.prec[2 * (size_t)i_next + 1];
         const int4 z = make_int4(0, 0, 0, 0);
         for (uint32_t k = b; k < e && !w.dead; ++k) {
+            if (i_next >= lim) break;                        // arrival order: the rest of the group too
             Rec r;
             r.i = i_next;
             const int4 p0 = n0, p1 = n1;
@@ -2330,14 +2361,14 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
 __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int only_fallback) {
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
-    if (failed(S.ctr)) return;
     if (only_fallback && !S.ctr[ci(C_FALLBACK)]) return;   // FUNDED epoch whose proof held
+    const uint32_t lim = err_limit(S.ctr, io.n);            // records before a fault raised by emap / route
     Core c(S, io);
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
-    for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
+    for (uint32_t k0 = 0; k0 < lim && !c.dead; k0 += 64) {
         const uint32_t k = k0 + lane;
-        const bool valid = k < io.n;
+        const bool valid = k < lim;
         // 64 records staged across the lanes, read with readlane (one gather per 64 records)
         const uint32_t bi = valid ? k : 0;
         const int32_t b_action = valid ? io.action[bi] : -1, b_price = valid ? io.price[bi] : 0;
@@ -2345,7 +2376,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
         const int64_t b_oid = valid ? io.oid[bi] : 0, b_aid = valid ? io.aid[bi] : 0, b_sid = valid ? io.sid[bi] : 0;
         const int64_t b_tgt = valid ? S.cancel_tgt[bi] : 0;
         const int32_t bgrp = valid ? S.route_grp[bi] : -1;
-        const int nb = (int)(io.n - k0 < 64 ? io.n - k0 : 64);
+        const int nb = (int)(lim - k0 < 64 ? lim - k0 : 64);
 #pragma nounroll
         for (int j = 0; j < nb && !c.dead; ++j) {
             Rec r;
@@ -2389,6 +2420,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     }
     c.store_group();
     if (lane_id() == 0) {
+        if (!c.dead && lim < io.n) io.trade_off[lim] = c.tnext;   // the trades before a fault raised by emap / route
         io.trade_off[io.n] = c.tnext;
         S.ctr[ci(C_TRADES)] = c.tnext;
         S.ctr[ci(C_RESTS)] = n_rest;
@@ -2482,9 +2514,11 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
 // record instead of five random partial-line writes (the C ABI's SoA arrays) in the matching loop.
 // Records without a symbol group were answered by k_route / k_ledger_funded already.
 __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
-    if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;   // a failed epoch: route's zero trade counts stay (k_scatter stays in bounds)
+    if (S.ctr[ci(C_FALLBACK)]) return;                   // k_serial answers the epoch
+    const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         if (S.route_grp[i] < 0) continue;
+        if (i >= lim) { io.n_trades[i] = 0; continue; }
         const KG int4* os = S.osort + 2 * (size_t)S.rank[i];
         const int4 a = os[0];
         const int32_t ntr = os[1].x;
@@ -2503,7 +2537,8 @@ constexpr uint32_t SCATTER_SUB = 8;   // blocks per shard region
 constexpr int SCATTER_ITEMS = 4;      // trades per thread and round
 __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const uint32_t* total) {
     const uint32_t s = blockIdx.x;
-    if (failed(S.ctr)) return;
+    if (S.ctr[ci(C_FALLBACK)]) return;
+    const uint32_t lim = err_limit(S.ctr, io.n);          // trades of the records that take effect only
     const bool fits = *total <= io.trades_cap;
     if (s == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (!fits) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, -1);
@@ -2534,10 +2569,10 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
             if (k < cnt) r[q] = S.ttmp[base + k];
         }
 #pragma unroll
-        for (int q = 0; q < SCATTER_ITEMS; ++q) off[q] = r[q].seq >= 0 ? io.trade_off[r[q].seq] : 0;
+        for (int q = 0; q < SCATTER_ITEMS; ++q) off[q] = r[q].seq >= 0 && (uint32_t)r[q].seq < lim ? io.trade_off[r[q].seq] : 0;
 #pragma unroll
         for (int q = 0; q < SCATTER_ITEMS; ++q)
-            if (r[q].seq >= 0) io.trades[off[q] + (uint32_t)r[q].ord] = r[q].t;
+            if (r[q].seq >= 0 && (uint32_t)r[q].seq < lim) io.trades[off[q] + (uint32_t)r[q].ord] = r[q].t;
     }
 }
 // The shard lines' rest / cancel counts into the counters block; the lines zeroed for the next epoch.
@@ -2653,6 +2688,7 @@ void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st) 
 void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (S.A == 0) return;
     hipLaunchKernelGGL(k_check_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_commit_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st) {
     if (io.n == 0) return;

@@ -1,6 +1,7 @@
 // kme_processor.cpp -- the Processor<String, Order> mirror over the epoch engine (kme.h).
 #include "kme_processor.hpp"
 
+#include <algorithm>
 #include <cstring>
 
 #include "kme_processor.h"
@@ -66,11 +67,25 @@ void MatchingEngine::flush() {
                          trade_off_.data(), trades_.data(), (uint32_t)trades_.size()};
     const kme_status rc = kme_submit_epoch(engine_, &in, n, &res, &last_);
     if (rc != KME_OK) {
+        // The reference forwards and commits every record before the one that throws (KP:97,
+        // 124-125) and then its stream thread dies: forward the records that took effect, commit
+        // them, then fail.  (Records the reference had forwarded for the faulting record itself --
+        // its IN echo, fills before the throw -- are not: whether its producer flushed them when
+        // the thread died is outside what the reference pins.)
+        forward_range(std::min<uint32_t>(last_.n_effective, n));
+        if (last_.n_effective > 0) context_->commit();
         dead_ = true;
         if (last_.error_index >= 0) last_.error_index += stream_base_;
         throw EngineError(rc, last_, std::string("epoch failed: ") + kme_strerror(rc) + " (" +
                                          kme_domain_str(last_.detail) + ")");
     }
+    forward_range(n);
+    context_->commit();
+    stream_base_ += n;
+    action_.clear(); oid_.clear(); aid_.clear(); sid_.clear(); price_.clear(); size_.clear();
+}
+
+void MatchingEngine::forward_range(uint32_t n) {
     // Forward in the reference's order: IN, (maker fill, taker fill) per trade, OUT (KP:97-124).
     for (uint32_t i = 0; i < n; ++i) {
         Order in_o;
@@ -97,9 +112,6 @@ void MatchingEngine::flush() {
         if (out_flags_[i] & KME_OUT_HAS_PREV) out_o.prev = out_prev_[i];
         context_->forward("OUT", out_o);
     }
-    context_->commit();
-    stream_base_ += n;
-    action_.clear(); oid_.clear(); aid_.clear(); sid_.clear(); price_.clear(); size_.clear();
 }
 
 }  // namespace kme

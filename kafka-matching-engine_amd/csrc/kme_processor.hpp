@@ -60,6 +60,7 @@ public:
 
 private:
     void flush();
+    void forward_range(uint32_t n);   // the reference's records of buffered inputs [0, n)
 
     kme_config cfg_;
     uint32_t epoch_records_;

@@ -184,8 +184,12 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.credit_div = cfg->credit_shards > 1 ? cfg->credit_shards : 1;
     S.trades_cap = cfg->max_trades;
     // trade scratch: TSHARDS shard regions (2x the even share, so only skewed load spills) and an
-    // overflow region that alone holds an epoch's worth of trades
-    const uint64_t ttmp_ov = funded ? (uint64_t)cfg->max_trades + 64 : 1;
+    // overflow region that alone holds an epoch's worth of trades plus what reservations can waste:
+    // k_match_lanes reserves LANE_TCH slots per lane at a time (up to LANE_TCH - 1 unused per light
+    // group, at most min(G, E) of them), and a reservation that straddles a shard region's end
+    // leaves the straddled part as holes (at most one per shard and matcher)
+    const uint64_t lane_waste = (uint64_t)(kLaneTradeChunk - 1) * std::min<uint64_t>(G, E);
+    const uint64_t ttmp_ov = funded ? (uint64_t)cfg->max_trades + 64 + lane_waste + 64ull * TSHARDS : 1;
     const uint64_t tshard_cap = funded ? std::max<uint64_t>(256, (2 * (uint64_t)cfg->max_trades + TSHARDS - 1) / TSHARDS) : 0;
     const uint64_t ttmp_total = ttmp_ov + (uint64_t)TSHARDS * tshard_cap;
     if (ttmp_total >= (1ull << 32)) { kme_destroy(e); return KME_E_INVALID; }
@@ -417,14 +421,23 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_maker_visits = c[ci(C_TRADES)];               // every maker visit is one trade (KP:238-242)
     s.n_cancel_ok = c[ci(C_CANCEL_OK)];
     s.serial_fallback = c[ci(C_FALLBACK)] ? 1u : 0u;
+    s.n_effective = e->last_n;
     if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
         const uint64_t ix = c[ci(C_ERR)] >> 16;
         s.error_index = ix == 0xFFFFFFFFFFFFull ? -1 : (int64_t)ix;
-        e->failed = 1;
-        e->fail_status = s.status;
-        e->fail_detail = s.detail;
+        // the records before the fault took effect (their results are valid), none after it
+        s.n_effective = s.error_index < 0 ? 0u : (uint32_t)std::min<int64_t>(s.error_index, e->last_n);
+        if (s.status == KME_E_UNFUNDED) {
+            // not fatal: the refused records changed nothing, so their sequence numbers are
+            // handed out again when they are resubmitted
+            e->seq_base -= (int64_t)(e->last_n - s.n_effective);
+        } else {
+            e->failed = 1;
+            e->fail_status = s.status;
+            e->fail_detail = s.detail;
+        }
     }
     if (e->timing) {
         for (int p = 0; p < PH_N; ++p) {
@@ -485,10 +498,12 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
 kme_status kme_checkpoint(kme_engine* e, const char* path) {
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
+    if (e->pending) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (ctr[ci(C_ERR)] != ~0ull) return KME_E_FAILED;   // the last epoch faulted: its state is not a checkpoint
     CkptHeader h{};
     std::memcpy(h.magic, kCkptMagic, sizeof h.magic);
     h.cfg = e->cfg;
@@ -515,30 +530,40 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
 kme_status kme_restore(kme_engine* e, const char* path) {
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
+    if (e->pending) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
     FILE* f = std::fopen(path, "rb");
     if (!f) return KME_E_INVALID;
     CkptHeader h{};
     bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, sizeof h.magic) == 0;
-    // the same store geometry (device, stream and timing choices may differ)
+    // the same store geometry (device, stream and timing choices may differ; max_epoch sizes the
+    // oid table, whose blob size is checked below)
     ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
          h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
          h.cfg.max_resting == e->cfg.max_resting && h.cfg.ledger_capacity == e->cfg.ledger_capacity &&
          h.cfg.credit_shards == e->cfg.credit_shards && h.cfg.flags == e->cfg.flags &&
          h.pool_used <= e->S.pool_cap;
-    std::vector<char> host;
-    for (const Blob& b : ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{}) {
+    // the whole file is read and checked before anything reaches the device: a mismatched or
+    // truncated checkpoint leaves the engine untouched
+    const std::vector<Blob> blobs = ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{};
+    std::vector<std::vector<char>> host(blobs.size());
+    for (size_t k = 0; ok && k < blobs.size(); ++k) {
         uint64_t n = 0;
-        ok = std::fread(&n, sizeof n, 1, f) == 1 && n == b.bytes;
+        ok = std::fread(&n, sizeof n, 1, f) == 1 && n == blobs[k].bytes;
         if (!ok) break;
-        host.resize(n);
-        ok = n == 0 || std::fread(host.data(), 1, n, f) == n;
-        if (!ok) break;
-        HIP_TRY(hipMemcpyAsync(b.dev, host.data(), n, hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(hipStreamSynchronize(e->stream));   // host buffer is reused
+        host[k].resize(n);
+        ok = n == 0 || std::fread(host[k].data(), 1, n, f) == n;
     }
+    ok = ok && std::fgetc(f) == EOF;   // nothing after the last blob
     std::fclose(f);
     if (!ok) return KME_E_INVALID;
+    // from here on a failure leaves a mix of old and restored state: the engine is dead
+    for (size_t k = 0; k < blobs.size(); ++k) {
+        if (hipMemcpy(blobs[k].dev, host[k].data(), blobs[k].bytes, hipMemcpyHostToDevice) != hipSuccess) {
+            e->failed = 1; e->fail_status = KME_E_HIP; e->fail_detail = KME_D_NONE;
+            return KME_E_HIP;
+        }
+    }
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
     ctr[ci(C_POOL_BUMP)] = h.pool_used;
@@ -644,9 +669,31 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme
         total.n_cancel_ok += es.n_cancel_ok;
         total.serial_fallback += es.serial_fallback;   // sub-epochs that ran serially
         if (rc != KME_OK) {
+            // the results of the records before the fault (the reference forwarded and committed
+            // them, KP:97, 124-125): out arrays, trade offsets and their trades
+            const uint32_t k = es.n_effective;
             total.status = es.status;
             total.detail = es.detail;
             total.error_index = es.error_index >= 0 ? es.error_index + a : -1;
+            total.n_effective = a + k;
+            total.n_trades = tbase;
+            if (k > 0) {
+                HIP_TRY(hipMemcpyAsync(out->trade_off + a + 1, e->d_trade_off + 1, k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                const uint32_t kt = out->trade_off[a + k];
+                if (tbase + kt <= out->trades_cap) {
+                    HIP_TRY(hipMemcpyAsync(out->out_action + a, e->d_out_action, k * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+                    HIP_TRY(hipMemcpyAsync(out->out_size + a, e->d_out_size, k * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+                    HIP_TRY(hipMemcpyAsync(out->out_prev + a, e->d_out_prev, k * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+                    HIP_TRY(hipMemcpyAsync(out->out_flags + a, e->d_out_flags, k * sizeof(uint8_t), hipMemcpyDeviceToHost, s));
+                    if (kt) HIP_TRY(hipMemcpyAsync(out->trades + tbase, e->d_trades, (size_t)kt * sizeof(kme_trade), hipMemcpyDeviceToHost, s));
+                    HIP_TRY(hipStreamSynchronize(s));
+                    for (uint32_t q = a + 1; q <= a + k; ++q) out->trade_off[q] += tbase;
+                    total.n_trades = tbase + kt;
+                } else {
+                    total.n_effective = a;   // (cannot happen: the device epoch fit its own buffer)
+                }
+            }
             if (st) *st = total;
             return rc;
         }
@@ -673,6 +720,7 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme
         if (n == 0) break;
     }
     total.n_trades = tbase;
+    total.n_effective = n;
     if (st) *st = total;
     return KME_OK;
 }

@@ -26,7 +26,7 @@ MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
           7: "FAILED"}
-ABI_VERSION = 3
+ABI_VERSION = 4
 FLAG_EXACT_LEDGER = 1
 FLAG_SERIAL_FALLBACK = 2   # FUNDED: an epoch whose funded proof fails runs serially (needs FLAG_EXACT_LEDGER)
 
@@ -57,7 +57,7 @@ class kme_epoch_status(C.Structure):
     _fields_ = [("status", C.c_int32), ("detail", C.c_int32), ("error_index", C.c_int64),
                 ("n_inputs", C.c_uint32), ("n_trades", C.c_uint32), ("n_orders", C.c_uint64),
                 ("n_rests", C.c_uint64), ("n_maker_visits", C.c_uint64), ("n_cancel_ok", C.c_uint64),
-                ("serial_fallback", C.c_uint32), ("_pad", C.c_uint32)]
+                ("serial_fallback", C.c_uint32), ("n_effective", C.c_uint32)]
 
 
 FORWARD_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t)
@@ -241,7 +241,14 @@ class Engine:
         del keep
         res.status = st
         if rc:
-            raise KmeError(rc, "kme_submit_epoch", st)
+            # the results of the records that took effect before the fault (kme.h, n_effective)
+            k = int(st.n_effective)
+            err = KmeError(rc, "kme_submit_epoch", st)
+            err.result = EpochResult(res.out_action[:k].copy(), res.out_size[:k].copy(), res.out_prev[:k].copy(),
+                                     res.out_flags[:k].copy(), res.trade_off[: k + 1].copy(),
+                                     res.trades[: int(res.trade_off[k])].copy(), st)
+            err.n_effective = k
+            raise err
         res.trades = res.trades[: int(res.trade_off[n])].copy()
         return res
 

@@ -1,0 +1,235 @@
+"""Faults and refusals, through the C ABI on the GPU:
+
+* a domain fault mid-epoch: the reference forwards and commits every record before the one that
+  throws (KP:97, 124-125), so the processor forwards exactly the oracle's tape of those records,
+  in both modes, for faults found before matching (k_emap / k_route) and during it (H5 NPE in
+  k_match or k_match_lanes while other symbol groups run past the fault in parallel);
+* KME_E_UNFUNDED is not fatal: nothing of a refused order epoch takes effect, the engine accepts
+  the next epoch and the refused records can be resubmitted after a top-up;
+* capacity and persistence edges from the round-1 advisor: trade scratch with one trade per light
+  group, restore of a mismatched / truncated checkpoint, checkpoint of a failed or in-flight epoch.
+"""
+import numpy as np
+import pytest
+
+import hazards
+from kme import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _funded_cfg(kme, G, accounts=64, E=1 << 16, P=1 << 18, light_max=0, max_trades=None):
+    return kme.default_config(kme.MODE_FUNDED, max_symbols=G, max_epoch=E, max_resting=P, max_accounts=accounts,
+                              light_max=light_max, max_trades=max_trades)
+
+
+def _exact_cfg(kme, G=64, E=1 << 16, P=1 << 18):
+    return kme.default_config(kme.MODE_EXACT, max_symbols=G, max_epoch=E, max_resting=P, ledger_capacity=1 << 16)
+
+
+def _prefix_tape(oracle_mod, orders, k):
+    o = oracle_mod.Oracle()
+    o.process(orders.slice(0, k))
+    return o.tape_text()
+
+
+def _with_overshoot(n_body=6000, seed=3):
+    """A funded body over symbols 3..40 with the H5 overshoot of symbol 1 in the middle: 48 bids on
+    levels 0..47, then a SELL at 0 whose sweep NPEs (KP:234-235, 252-253) -- other symbols' records
+    after it are matched in parallel on the device but must not be answered."""
+    rows, _ = hazards.domain_streams()["log10_overshoot"]
+    setup = [r for r in rows if r[0] in (W.CREATE_BALANCE, W.TRANSFER, W.ADD_SYMBOL)]
+    setup += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(3, 41)]
+    hot = [r for r in rows if r[0] in (W.BUY, W.SELL)]
+    body = W.uniform(n_body, n_symbols=38, n_accounts=4, seed=seed, sid_base=3, aid_base=1, oid_base=10_000)
+    half = n_body // 2
+    return W.Orders.concat([W.Orders.from_rows(setup), body.slice(0, half), W.Orders.from_rows(hot),
+                            body.slice(half, n_body)])
+
+
+def _inject(orders, i, row):
+    o = W.Orders.concat([orders.slice(0, i), W.Orders.from_rows([row]), orders.slice(i + 1, len(orders))])
+    return o
+
+
+def _fault_cases():
+    setup = W.funded_setup(64, range(1, 65))
+    body = W.uniform(20_000, n_symbols=64, n_accounts=64, seed=17)
+    base = W.Orders.concat([setup, body])
+    i = len(setup) + 12_345
+    dup_oid = int(body.oid[100]) if body.action[100] in (W.BUY, W.SELL) else int(body.oid[101])
+    return {
+        # k_emap: a BUY/SELL reusing the oid of a live order (KP:221 would corrupt the lists)
+        "dup_oid": (lambda: _inject(base, i, (W.BUY, dup_oid, 5, 7, 50, 3)), ("funded", "exact"), 8),
+        # k_emap: FUNDED price outside 0..100
+        "funded_range": (lambda: _inject(base, i, (W.BUY, 99_999_999, 5, 7, 101, 3)), ("funded",), 9),
+        # k_match / k_match_lanes: the H5 NPE while other groups run on
+        "overshoot_parallel": (_with_overshoot, ("funded", "exact"), 2),
+    }
+
+
+@pytest.mark.parametrize("case,mode,light_max", [(c, m, lm) for c, (_, modes, _) in sorted(_fault_cases().items())
+                                                 for m in modes for lm in ((0, -1, 1 << 30) if m == "funded" else (0,))])
+def test_processor_forwards_the_records_before_a_fault(kme_mod, oracle_mod, case, mode, light_max):
+    make, _, detail = _fault_cases()[case]
+    orders = make()
+    cfg = _funded_cfg(kme_mod, 65, light_max=light_max) if mode == "funded" else _exact_cfg(kme_mod)
+    p = kme_mod.Processor(cfg, epoch_records=1 << 16)
+    for line in orders.to_json_lines():
+        assert p.process_json(line) == 0
+    rc = p.close()
+    assert kme_mod.STATUS[rc] == "DOMAIN"
+    st = p.last_status()
+    assert st.detail == detail
+    k = int(st.error_index)
+    assert k > len(orders) // 3 and st.n_effective == k
+    if case == "overshoot_parallel":
+        o = oracle_mod.Oracle()
+        with pytest.raises(oracle_mod.OracleError) as oe:
+            o.process(orders)
+        assert oe.value.index == k
+    want = _prefix_tape(oracle_mod, orders, k)
+    got = p.tape_text()
+    assert got == want
+    assert p.commits == 1
+
+
+@pytest.mark.parametrize("light_max", [0, 1 << 30])
+def test_engine_results_before_a_fault(kme_mod, oracle_mod, light_max):
+    """The host-buffer ABI: kme_submit_epoch fills out_* / trade_off / trades for the records
+    [0, n_effective) of a faulting submission (here spanning an account sub-epoch and an order one)."""
+    orders = _with_overshoot(n_body=20_000, seed=5)
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, 65, light_max=light_max))
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(orders)
+    assert ke.value.detail == 2
+    k = ke.value.index
+    assert ke.value.n_effective == k > 0
+    part = orders.slice(0, k)
+    assert ke.value.result.tape_json(part) == _prefix_tape(oracle_mod, orders, k)
+    # a failed engine accepts nothing further
+    with pytest.raises(kme_mod.KmeError) as again:
+        eng.process(orders.slice(0, 10))
+    assert kme_mod.STATUS[again.value.status] == "FAILED"
+
+
+@pytest.mark.parametrize("light_max", [0, 1 << 30])
+def test_unfunded_epoch_is_refused_without_effect(kme_mod, oracle_mod, light_max):
+    n_sym, n_acc = 16, 8
+    setup = W.Orders.from_rows([r for a in range(n_acc) for r in ((W.CREATE_BALANCE, 0, a, 0, 0, 0),
+                                                                  (W.TRANSFER, 0, a, 0, 0, 200_000))]
+                               + [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)])
+    first = W.uniform(200, n_symbols=n_sym, n_accounts=n_acc, seed=1, oid_base=1)
+    big = W.uniform(3000, n_symbols=n_sym, n_accounts=n_acc, seed=2, oid_base=10_000)   # ~375 orders/account: unprovable
+    topup = W.Orders.from_rows([(W.TRANSFER, 0, a, 0, 0, 2_000_000_000) for a in range(n_acc)])
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=n_acc, light_max=light_max))
+    got = eng.process(setup).tape_json(setup) + eng.process(first).tape_json(first)
+    books = eng.snapshot_books()
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(big)
+    assert kme_mod.STATUS[ke.value.status] == "UNFUNDED"
+    assert eng.snapshot_books() == books                      # nothing of it took effect
+    got += eng.process(topup).tape_json(topup)                 # the engine is alive
+    got += eng.process(big).tape_json(big)                     # and takes the records now
+    o = oracle_mod.Oracle()
+    for part in (setup, first, topup, big):
+        o.process(part)
+    assert got == o.tape_text()
+    assert eng.snapshot_books() == o.dump_books()
+
+
+def test_unfunded_debit_keeps_the_records_before_it(kme_mod, oracle_mod):
+    """A TRANSFER debit that cannot be proven (KP:142) stops an account epoch at its index: the
+    records before it took effect, the engine goes on."""
+    n_acc = 4
+    setup = W.Orders.from_rows([r for a in range(n_acc) for r in ((W.CREATE_BALANCE, 0, a, 0, 0, 0),
+                                                                  (W.TRANSFER, 0, a, 0, 0, 1000))]
+                               + [(W.ADD_SYMBOL, 0, 0, 1, 0, 0)])
+    acct = W.Orders.from_rows([(W.TRANSFER, 0, 0, 0, 0, 50), (W.CREATE_BALANCE, 0, 7, 0, 0, 0),
+                               (W.TRANSFER, 0, 1, 0, 0, -5000), (W.TRANSFER, 0, 2, 0, 0, 70)])
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, 2, accounts=8))
+    eng.process(setup)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(acct)
+    assert kme_mod.STATUS[ke.value.status] == "UNFUNDED" and ke.value.index == 2
+    after = W.Orders.from_rows([(W.BUY, 5, 0, 1, 50, 20), (W.SELL, 6, 7, 1, 40, 0), (W.BUY, 8, 2, 1, 10, 1)])
+    got = eng.process(after).tape_json(after)
+    o = oracle_mod.Oracle()
+    o.process(setup)
+    o.process(acct.slice(0, 2))
+    o.clear_tape()
+    o.process(after)
+    assert got == o.tape_text()
+
+
+def test_trade_scratch_one_trade_per_light_group(kme_mod, oracle_mod):
+    """Advisor (round 1): k_match_lanes reserves trade scratch 8 slots per lane; an epoch of
+    16,384 one-trade light groups with max_trades = max_epoch must still fit."""
+    G, E = 16384, 16384
+    setup = W.funded_setup(8, range(1, G + 1))
+    rest = W.Orders.from_rows([(W.SELL, 1_000_000 + s, s % 8, s, 50, 3) for s in range(1, G + 1)])
+    take = W.Orders.from_rows([(W.BUY, 2_000_000 + s, (s + 1) % 8, s, 50, 2) for s in range(1, G + 1)])
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, G + 1, accounts=8, E=E, P=1 << 16, max_trades=E))
+    o = oracle_mod.Oracle()
+    got = ""
+    for part in (setup, rest, take):
+        r = eng.process(part)
+        got += r.tape_json(part)
+        o.process(part)
+    assert int(r.status.n_trades) == G
+    assert got == o.tape_text()
+
+
+def test_restore_refuses_mismatched_or_truncated_checkpoints(kme_mod, oracle_mod, tmp_path):
+    """Advisor (round 1): a checkpoint of another geometry (max_epoch sizes the oid table) or a
+    truncated file is refused before anything reaches the device; the engine stays usable."""
+    setup = W.funded_setup(32, range(1, 17))
+    a_part = W.uniform(4000, n_symbols=16, n_accounts=32, seed=8, oid_base=1)
+    b_part = W.uniform(4000, n_symbols=16, n_accounts=32, seed=9, oid_base=100_000)
+    src = kme_mod.Engine(_funded_cfg(kme_mod, 17, accounts=32, E=1 << 14))
+    src.process(setup)
+    src.process(a_part)
+    ck = tmp_path / "a.ckpt"
+    src.checkpoint(ck)
+    raw = ck.read_bytes()
+    (tmp_path / "short.ckpt").write_bytes(raw[: len(raw) - 100])
+    for path, E in ((ck, 1 << 18), (tmp_path / "short.ckpt", 1 << 14)):
+        dst = kme_mod.Engine(_funded_cfg(kme_mod, 17, accounts=32, E=E))
+        dst.process(setup)
+        before = dst.snapshot_books()
+        with pytest.raises(kme_mod.KmeError) as ke:
+            dst.restore(path)
+        assert kme_mod.STATUS[ke.value.status] == "INVALID"
+        assert dst.snapshot_books() == before
+        got = dst.process(b_part).tape_json(b_part)          # untouched and alive
+        o = oracle_mod.Oracle()
+        o.process(setup)
+        o.clear_tape()
+        o.process(b_part)
+        assert got == o.tape_text()
+        dst.close()
+
+
+def test_checkpoint_refuses_failed_or_pending_epochs(kme_mod, tmp_path):
+    import torch
+
+    rows, _ = hazards.domain_streams()["remove_nonempty"]
+    orders = hazards.as_orders(rows)
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, 8, accounts=8))
+    with pytest.raises(kme_mod.KmeError):
+        eng.process(orders)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.checkpoint(tmp_path / "f.ckpt")
+    assert kme_mod.STATUS[ke.value.status] == "FAILED"
+    # an epoch in flight (submitted, not yet waited for)
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, 8, accounts=8))
+    setup = W.funded_setup(8, range(1, 8))
+    eng.process(setup)
+    part = W.uniform(1000, n_symbols=7, n_accounts=8, seed=4)
+    cols = {k: torch.from_numpy(np.ascontiguousarray(getattr(part, k))).cuda() for k in ("action", "oid", "aid", "sid", "price", "size")}
+    eng.submit_device({k: t.data_ptr() for k, t in cols.items()}, len(part))
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.checkpoint(tmp_path / "p.ckpt")
+    assert kme_mod.STATUS[ke.value.status] == "INVALID"
+    eng.wait()
+    eng.checkpoint(tmp_path / "ok.ckpt")

@@ -39,9 +39,11 @@ def _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, light_max, epoch=E)
     eng.close()
 
 
-@pytest.mark.parametrize("light_max", [-1, 0])
+@pytest.mark.parametrize("light_max", [-1, 0, 1 << 30])
 def test_c5_cancel_replace_at_scale(kme_mod, oracle_mod, light_max):
-    """C5 (1,024 symbols, 4,096 accounts): cancels of orders swept earlier in the epoch."""
+    """C5 (1,024 symbols, 4,096 accounts): cancels of orders swept earlier in the epoch; with
+    light_max = 2^30 every group (~1,500 records per epoch) runs in k_match_lanes, so the lanes
+    kernel's cancel path sees the churn at scale."""
     n_sym, n_acc, n = 1024, 4096, 6 * E
     stream = W.cancel_replace(n, n_symbols=n_sym, n_accounts=n_acc, seed=1000)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1),
@@ -53,6 +55,53 @@ def test_c3_uniform_at_scale(kme_mod, oracle_mod):
     """C3's shape (65,536 symbols and accounts): light groups in lanes, busy ones in wavefronts."""
     n_sym, n_acc, n = 65536, 65536, 4 * E
     stream = W.uniform(n, n_symbols=n_sym, n_accounts=n_acc, seed=1000)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
+
+
+@pytest.mark.timeout(600)
+def test_c3_bench_stream_at_bench_shape(kme_mod, oracle_mod):
+    """The bench's own C3 stream (bench.make_workload: seed 1000, 65,536 symbols and accounts) in
+    its own epoch size, 2^22 records, for six epochs: ~64 records per group per epoch, free-list
+    blocks recycled across epochs, and an oid-table rebuild (kme_wait: (used + max_epoch) * 2 >
+    capacity) between epochs 5 and 6.  Every epoch's tape is compared in binary (tests/tapes.py)
+    with the oracle's, the books at the end line by line."""
+    import bench
+    import tapes
+
+    E22, n_ep, max_resting = 1 << 22, 6, 4_000_000
+    setup, stream, sids, nacc, _, _ = bench.make_workload("c3", n_ep * E22, 0, 1)
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=int(sids.max()) + 1, max_epoch=E22,
+                                                max_resting=max_resting, max_trades=2 * E22 + (1 << 16),
+                                                max_accounts=nacc))
+    # the oid table's capacity (kme_create) and the epoch after which kme_wait rebuilds it
+    pool = max_resting + (int(sids.max()) + 2) * 64
+    cap = 1 << (2 * (pool + E22) - 1).bit_length()
+    bs_per_epoch = [int(np.count_nonzero(np.isin(stream.action[k * E22:(k + 1) * E22], (W.BUY, W.SELL)))) for k in range(n_ep)]
+    assert (sum(bs_per_epoch[:5]) + E22) * 2 > cap > (sum(bs_per_epoch[:4]) + E22) * 2
+    o = oracle_mod.Oracle()
+    o.process(setup)
+    eng.process(setup)
+    o.clear_tape()
+    for k in range(n_ep):
+        part = stream.slice(k * E22, (k + 1) * E22)
+        r = eng.process(part)
+        o.process(part)
+        want = o.tape()
+        o.clear_tape()
+        got = tapes.engine_tape(part, r, oracle_mod.REC_DTYPE)
+        d = tapes.first_difference(got, want)
+        assert d is None, f"epoch {k}: tape row {d}: got {got[d] if d < len(got) else None} want {want[d] if d < len(want) else None}"
+        assert r.status.n_trades > 1_000_000
+    assert eng.snapshot_books() == o.dump_books()
+    eng.close()
+
+
+def test_c4_zipf_65536_symbols(kme_mod, oracle_mod):
+    """C4 at its own universe, 65,536 symbols (Zipf 1.1: the hottest symbol takes ~12% of the
+    records, thousands of orders deep, in k_match; the tail in k_match_lanes)."""
+    n_sym, n_acc, n = 65536, 65536, 2 * E
+    stream = W.zipf(n, n_symbols=n_sym, n_accounts=n_acc, seed=1002)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
     _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
 

@@ -62,3 +62,33 @@ def test_funded_setup_covers_worst_case_reservations():
     n, acc = 1_000_000, 64
     k = W.funded_transfers_needed(n, acc, big=True)
     assert k * W.INT_MAX >= 2 * (n // acc) * 50_000 * 70
+
+
+def test_binary_tape_helper_matches_oracle(oracle_mod):
+    """tests/tapes.engine_tape rebuilds the oracle's tape from per-input results (the GPU scale
+    tests compare binary tapes this way): derive the results from an oracle tape and rebuild it."""
+    import kme
+    import tapes
+
+    setup = W.funded_setup(64, range(1, 33))
+    body = W.cancel_replace(4000, n_symbols=32, n_accounts=64, seed=5)
+    orders = W.Orders.concat([setup, body])
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    tape = o.tape()
+    starts = np.flatnonzero(tape["key"] == 0)
+    assert len(starts) == len(orders)
+    ends = np.r_[starts[1:], len(tape)] - 1
+    ntr = (ends - starts - 1) // 2
+    T = np.r_[0, np.cumsum(ntr)].astype(np.uint32)
+    fill_rows = np.concatenate([np.arange(s + 1, e, 2) for s, e in zip(starts, ends)]) if ntr.sum() else np.zeros(0, int)
+    trades = np.zeros(len(fill_rows), kme.TRADE_DTYPE)
+    trades["maker_oid"], trades["maker_aid"], trades["maker_sid"] = tape["oid"][fill_rows], tape["aid"][fill_rows], tape["sid"][fill_rows]
+    trades["size"] = tape["size"][fill_rows]
+    taker_price = orders.price[np.repeat(np.arange(len(orders)), ntr)]
+    trades["maker_price"] = taker_price - tape["price"][fill_rows + 1]
+    res = kme.EpochResult(tape["action"][ends].astype(np.int32), tape["size"][ends].astype(np.int32),
+                          tape["prev"][ends].astype(np.int64), tape["has_prev"][ends].astype(np.uint8), T, trades, None)
+    assert ntr.sum() > 100
+    got = tapes.engine_tape(orders, res, oracle_mod.REC_DTYPE)
+    assert tapes.first_difference(got, tape) is None
