@@ -373,7 +373,8 @@ def main():
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
             "market_data": {"symbols": int(sum(len(p) for p in per_rank)), "bytes_per_epoch": int(world * rows * 16),
-                            "collective": "RCCL all_gather_into_tensor per epoch" if world > 1 else "none (N = 1)",
+                            "collective": ("gloo all_gather (one-GPU rehearsal)" if rehearsal else "RCCL all_gather_into_tensor per epoch")
+                            if world > 1 else "none (N = 1)",
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},

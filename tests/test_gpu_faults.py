@@ -23,7 +23,7 @@ def _funded_cfg(kme, G, accounts=64, E=1 << 16, P=1 << 18, light_max=0, max_trad
                               light_max=light_max, max_trades=max_trades)
 
 
-def _exact_cfg(kme, G=64, E=1 << 16, P=1 << 18):
+def _exact_cfg(kme, G=65, E=1 << 16, P=1 << 18):
     return kme.default_config(kme.MODE_EXACT, max_symbols=G, max_epoch=E, max_resting=P, ledger_capacity=1 << 16)
 
 
@@ -77,9 +77,10 @@ def test_processor_forwards_the_records_before_a_fault(kme_mod, oracle_mod, case
     p = kme_mod.Processor(cfg, epoch_records=1 << 16)
     for line in orders.to_json_lines():
         assert p.process_json(line) == 0
-    rc = p.close()
+    rc = p.punctuate()
     assert kme_mod.STATUS[rc] == "DOMAIN"
     st = p.last_status()
+    assert p.close() == 0   # a dead processor has nothing left to flush
     assert st.detail == detail
     k = int(st.error_index)
     assert k > len(orders) // 3 and st.n_effective == k

@@ -6,7 +6,7 @@ OUT=gpurun_out/${1:-quick}
 shift || true
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -5 $OUT/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 for args in "$@"; do
