@@ -186,6 +186,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
+    ap.add_argument("--lane-stamps", action="store_true", help="diagnostic: print k_match_lanes step-segment shares and exit")
     ap.add_argument("--serialize", action="store_true",
                     help="also print each epoch's MatchOut tape on the GPU (kme_tape_json_device) inside the step")
     return ap.parse_args(argv)
@@ -202,6 +203,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.stamps:  # diagnostic build with in-kernel s_memtime stamps (never the bench line)
         os.environ["KME_LIB"] = os.path.join(ROOT, "kafka-matching-engine_amd", "kme", "libkme_stamps.so")
+    if args.lane_stamps:
+        os.environ["KME_LIB"] = os.path.join(ROOT, "kafka-matching-engine_amd", "kme", "libkme_lstamps.so")
 
     import torch
     import torch.distributed as dist
@@ -313,6 +316,14 @@ def main():
         print(f"rank {rank}: market data check failed (own snapshot vs full-range: {md_local}, "
               f"all-gathered block: {md_gather})", file=sys.stderr, flush=True)
 
+    if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)
+        d = eng.debug_counters().astype(np.float64).reshape(-1)[:8]
+        names = ["drain", "gather1", "gather2", "record", "out", "record.try_match", "record.rest"]
+        tot = d[:5].sum()
+        print(json.dumps({"lane_stamps": {"share": {n: d[q] / tot for q, n in enumerate(names)},
+                                          "cycles_per_step": {n: d[q] / max(1, d[7]) for q, n in enumerate(names)},
+                                          "steps": d[7], "ms_per_epoch_match": float(np.mean(match_ms))}}), flush=True)
+        return
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
         rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 32)
         hot = int(np.argmax(rows_[:, 7]))   # the group with the most k_match cycles (C4: the hot symbol)
@@ -377,6 +388,7 @@ def main():
                             if world > 1 else "none (N = 1)",
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
+            "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "
                                    "one wavefront each, concurrent)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -63,6 +63,22 @@ KDEV unsigned long long stamp() {
 #else
 #define KST(x)
 #endif
+// -DKME_LANE_STAMPS: the same for k_match_lanes, per wavefront step (every lane's step shares the
+// wavefront's timeline): drain of the previous step's vector operations, first gather, second
+// gather, the record (try_match, rest), the OUT echo; each segment ends with an explicit wait, so
+// the build serialises what the product build overlaps (quote shares, not times).
+#ifdef KME_LANE_STAMPS
+KDEV unsigned long long lstamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define LST(...) __VA_ARGS__
+#else
+#define LST(...)
+#endif
 // Broadcast lane 0's value with readfirstlane (SGPR result): the compiler then knows it is
 // wave-uniform.  (__shfl lowers to ds_bpermute, whose result the divergence analysis treats as
 // per-lane; everything computed from it would turn into exec-masked VALU code.)
@@ -299,7 +315,13 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                 if ((uint32_t)(prev >> 32) == fp && v != OT_DEAD) {
                     if (v & OT_PENDING) {
                         const uint32_t j = v & ~OT_PENDING;
-                        if (io.oid[j] == oid) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i > j ? i : j); break; }
+                        if (io.oid[j] == oid) {
+                            // the later of the two is the fault; the earlier one takes effect and
+                            // keeps its entry (cancels before the fault must find it), so it goes on
+                            // probing past a later one that got there first
+                            raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i > j ? i : j);
+                            if (j < i) break;
+                        }
                     } else if (S.pool[v].live && S.pool[v].oid == oid) {
                         raise_thread(S.ctr, KME_E_DOMAIN, KME_D_DUP_OID, i);
                         break;
@@ -1937,6 +1959,12 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
 // records in the epoch stay with k_match (which skips the light ones); both kernels keep the
 // same persistent group format (GroupState, Level, Node, free-slot blocks).
 constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBLK-slot blocks)
+#ifndef KME_DIAG_NO_OUT
+#define KME_DIAG_NO_OUT 0       // diagnostic builds only: skip the OUT echo stores of k_match_lanes
+#endif
+#ifndef KME_DIAG_NO_TRADE
+#define KME_DIAG_NO_TRADE 0     // diagnostic builds only: skip the trade-record stores of k_match_lanes
+#endif
 #ifndef KME_LANE_GROUPS
 #define KME_LANE_GROUPS 32
 #endif
@@ -2076,6 +2104,7 @@ struct GroupLane {
             if (dead) return;
         }
         const size_t pos = tpos++;
+        if (KME_DIAG_NO_TRADE) return;
         const int64_t msid = msneg ? -(int64_t)g : (int64_t)g;
         KG int4* r = reinterpret_cast<KG int4*>(&S.ttmp[pos]);
         KG int2* r2 = reinterpret_cast<KG int2*>(&S.ttmp[pos]);
@@ -2234,8 +2263,16 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
         uint32_t i_after = b + 1 < e ? perm[b + 1] : 0;
         int4 n0 = S.prec[2 * (size_t)i_next], n1 = S.prec[2 * (size_t)i_next + 1];
         const int4 z = make_int4(0, 0, 0, 0);
+        LST(unsigned long long lacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lt = lstamp();)
+        // the previous record's OUT echo: stored after this record's first gather is issued, so the
+        // gather's wait does not include it (vmcnt counts loads and stores in issue order)
+        uint32_t pend_k = 0;
+        int4 pend_a = make_int4(0, 0, 0, 0);
+        int32_t pend_ntr = 0;
+        bool pend = false;
         for (uint32_t k = b; k < e && !w.dead; ++k) {
             if (i_next >= lim) break;                        // arrival order: the rest of the group too
+            LST({ const unsigned long long t1 = lstamp(); lacc[0] += t1 - lt; lt = t1; lacc[7] += 1; })
             Rec r;
             r.i = i_next;
             const int4 p0 = n0, p1 = n1;
@@ -2294,6 +2331,13 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     vslot = S.rest_slot[-(r.tgt + 2)];
                 }
             }
+            if (pend && !KME_DIAG_NO_OUT) {
+                KG int4* os = S.osort + 2 * (size_t)pend_k;
+                os[0] = pend_a;
+                os[1] = make_int4(pend_ntr, 0, 0, 0);
+            }
+            pend = false;
+            LST({ const unsigned long long t1 = lstamp(); lacc[1] += t1 - lt; lt = t1; })
             // ---- second gather
             int32_t ms = -1;
             int64_t lqty = 0;
@@ -2309,13 +2353,17 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
             }
             if (w.dead) break;
+            LST({ const unsigned long long t1 = lstamp(); lacc[2] += t1 - lt; lt = t1; })
             // ---- the record
             if (order) {
                 uint32_t ntr = 0;
+                LST(const unsigned long long tq0 = lstamp();)
                 if (tm) filled = w.try_match(r.price, tsize, is_buy, os, ntr, pb, ms, lqty, m0, m1);
+                LST(const unsigned long long tq1 = lstamp(); lacc[5] += tq1 - tq0;)
                 o.ntr = ntr;
                 if (w.dead) break;
                 if (!filled) { w.rest(r, tsize, o, own_pre, lo0, lo1); if (w.dead) break; }
+                LST(lacc[6] += lstamp() - tq1;)
                 ok = true;
                 o.size = tsize;
             } else if (cxl) {
@@ -2334,15 +2382,25 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 if (r.action == PAYOUT) ok = false;
             }                                                // BUY / SELL without book or balance: REJECT
             o.action = ok ? r.action : (int32_t)REJECT;
-            {   // the OUT echo in sorted order: this lane's writes walk consecutive lines
+            LST({ const unsigned long long t1 = lstamp(); lacc[3] += t1 - lt; lt = t1; })
+            {   // the OUT echo in sorted order (this lane's writes walk consecutive lines), stored
+                // next step
                 const int64_t pv = o.has_prev ? o.prev : 0;
-                KG int4* os = S.osort + 2 * (size_t)k;
-                os[0] = make_int4((o.action & 0xFFFF) | ((o.has_prev ? KME_OUT_HAS_PREV : 0) << 16), o.size, lo32(pv), hi32(pv));
-                os[1] = make_int4((int32_t)o.ntr, 0, 0, 0);
+                pend_k = k;
+                pend_a = make_int4((o.action & 0xFFFF) | ((o.has_prev ? KME_OUT_HAS_PREV : 0) << 16), o.size, lo32(pv), hi32(pv));
+                pend_ntr = (int32_t)o.ntr;
+                pend = true;
             }
             n_rest += o.rested ? 1u : 0u;
             n_cancel += (cxl && ok) ? 1u : 0u;
+            LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
         }
+        if (pend && !KME_DIAG_NO_OUT) {
+            KG int4* os = S.osort + 2 * (size_t)pend_k;
+            os[0] = pend_a;
+            os[1] = make_int4(pend_ntr, 0, 0, 0);
+        }
+        LST(if (lane_id() == __ffsll((long long)__ballot(1)) - 1) for (int q = 0; q < 8; ++q) atomicAdd(&S.dbg[q], lacc[q]);)
         w.store_group();
     }
     // per-wavefront sums onto the shard line (k_tsh_fold adds the lines up)

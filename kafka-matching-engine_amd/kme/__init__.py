@@ -81,8 +81,9 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"libkme.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    path = os.environ.get("KME_LIB") or LIB_PATH   # (diagnostic builds are selected at load time)
+    if not os.path.exists(path):
+        raise RuntimeError(f"libkme.so not built ({path}); run __graft_entry__.build()")
     # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.  Loading torch first
     # makes libkme's NEEDED libamdhip64.so.7 resolve to that already-loaded copy (same SONAME);
     # loading libkme first would map a second HIP/HSA runtime and neither would see the GPU.
@@ -90,7 +91,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, st, u32, i32, i64 = C.c_void_p, C.c_int, C.c_uint32, C.c_int32, C.c_int64
     sig = {
         "kme_create": (st, [C.POINTER(kme_config), C.POINTER(vp)]),
