@@ -695,6 +695,7 @@ struct Rec {
     int64_t oid, aid, sid, tgt;
     int32_t lane;                 // lane of the record in its batch
 };
+constexpr uint32_t OS_MAX_NTR = 1u << 23;   // trades of one record the packed OUT echo (osort) can count
 // What process() decided for one record (the OUT echo fields and its trade count).
 struct Out {
     int32_t action, size;
@@ -1923,11 +1924,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         }
         n_rest += (uint32_t)__popcll(__ballot(lane < done && ((o_act >> 16) & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < done && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
-        if (lane < done) {   // one coalesced 32-B record per lane (k_unsort scatters them)
-            KG int4* os = opaque_const(Sp).osort + 2 * (size_t)k;
-            os[0] = make_int4((o_act & 0xFFFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 16), o_size, o_plo, o_phi);
-            os[1] = make_int4(o_ntr, 0, 0, 0);
-        }
+        if (__ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR)) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
+        if (lane < done)   // one coalesced 16-B record per lane (k_unsort scatters them)
+            opaque_const(Sp).osort[k] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
+                                                  o_size, o_plo, o_phi);
     }
     KST(const unsigned long long to0 = stamp();)
     w.flush_trades();
@@ -1973,6 +1973,20 @@ constexpr int LANE_GROUPS = KME_LANE_GROUPS;   // groups per wavefront (the othe
                                   // wavefronts per SIMD at 65,536 groups, so one issues while the other waits
 static_assert(LANE_GROUPS >= 1 && LANE_GROUPS <= 64, "k_match_lanes: one group per lane");
 
+// OUT echo layout (DevState::osort, 16 B per record: action | has_prev << 8 | n_trades << 9, size,
+// prev).  A busy group's records sit at their sorted position k; a light group's (when os_lanes)
+// step-major behind os_base: the record a k_match_lanes wavefront handles in step s of lane l goes
+// to wave * (LANE_GROUPS * light_max) + s * LANE_GROUPS + l, so every step's stores of a wavefront
+// form one contiguous run instead of 32 scattered half lines.
+KDEV size_t os_pos_light(const DevState& S, int32_t g, uint32_t step) {
+    return (size_t)S.os_base + (size_t)(g / LANE_GROUPS) * (LANE_GROUPS * (uint32_t)S.light_max) +
+           (size_t)step * LANE_GROUPS + (uint32_t)(g % LANE_GROUPS);
+}
+KDEV int4 os_pack(int32_t action, bool has_prev, uint32_t ntr, int32_t size, int64_t prev) {
+    return make_int4((action & 0xFF) | (has_prev ? 1 << 8 : 0) | (int32_t)(ntr << 9), size, lo32(prev), hi32(prev));
+}
+
+
 struct GroupLane {
     const DevState& S;
     const EpochIO& io;
@@ -1986,6 +2000,7 @@ struct GroupLane {
     uint32_t cur;
     bool dead;
     size_t tpos, tlim;            // this lane's reserved trade scratch [tpos, tlim) (LANE_TCH at a time)
+    LST(uint32_t nload = 0;)      // (stamps build) maker loads of the sweep beyond the first
 
     KDEV GroupLane(const DevState& s, const EpochIO& e, int32_t (*f)[64], int32_t gg)
         : S(s), io(e), fs(f), tsh(s.tsh + (size_t)(blockIdx.x & (TSHARDS - 1)) * CTR_STRIDE),
@@ -2162,6 +2177,7 @@ struct GroupLane {
             }
             m0 = reinterpret_cast<const KG int4*>(&S.pool[ms])[0];
             m1 = reinterpret_cast<const KG int4*>(&S.pool[ms])[1];
+            LST(++nload;)
         }
     }
 
@@ -2263,12 +2279,11 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
         uint32_t i_after = b + 1 < e ? perm[b + 1] : 0;
         int4 n0 = S.prec[2 * (size_t)i_next], n1 = S.prec[2 * (size_t)i_next + 1];
         const int4 z = make_int4(0, 0, 0, 0);
-        LST(unsigned long long lacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lt = lstamp();)
+        LST(unsigned long long lacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lt = lstamp();)
         // the previous record's OUT echo: stored after this record's first gather is issued, so the
         // gather's wait does not include it (vmcnt counts loads and stores in issue order)
-        uint32_t pend_k = 0;
+        size_t pend_pos = 0;
         int4 pend_a = make_int4(0, 0, 0, 0);
-        int32_t pend_ntr = 0;
         bool pend = false;
         for (uint32_t k = b; k < e && !w.dead; ++k) {
             if (i_next >= lim) break;                        // arrival order: the rest of the group too
@@ -2331,11 +2346,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     vslot = S.rest_slot[-(r.tgt + 2)];
                 }
             }
-            if (pend && !KME_DIAG_NO_OUT) {
-                KG int4* os = S.osort + 2 * (size_t)pend_k;
-                os[0] = pend_a;
-                os[1] = make_int4(pend_ntr, 0, 0, 0);
-            }
+            if (pend && !KME_DIAG_NO_OUT) S.osort[pend_pos] = pend_a;
             pend = false;
             LST({ const unsigned long long t1 = lstamp(); lacc[1] += t1 - lt; lt = t1; })
             // ---- second gather
@@ -2357,9 +2368,12 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
             // ---- the record
             if (order) {
                 uint32_t ntr = 0;
-                LST(const unsigned long long tq0 = lstamp();)
+                LST(const unsigned long long tq0 = lstamp(); w.nload = 0;)
                 if (tm) filled = w.try_match(r.price, tsize, is_buy, os, ntr, pb, ms, lqty, m0, m1);
-                LST(const unsigned long long tq1 = lstamp(); lacc[5] += tq1 - tq0;)
+                LST(const unsigned long long tq1 = lstamp(); lacc[5] += tq1 - tq0;
+                    { uint32_t mx = w.nload; for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+                      uint32_t sm = w.nload; for (int off = 32; off > 0; off >>= 1) sm += (uint32_t)__shfl_xor((int)sm, off);
+                      lacc[8] += mx > 0; lacc[9] += sm; lacc[10] += mx; })
                 o.ntr = ntr;
                 if (w.dead) break;
                 if (!filled) { w.rest(r, tsize, o, own_pre, lo0, lo1); if (w.dead) break; }
@@ -2383,24 +2397,19 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
             }                                                // BUY / SELL without book or balance: REJECT
             o.action = ok ? r.action : (int32_t)REJECT;
             LST({ const unsigned long long t1 = lstamp(); lacc[3] += t1 - lt; lt = t1; })
-            {   // the OUT echo in sorted order (this lane's writes walk consecutive lines), stored
+            {   // the OUT echo (step-major: the wavefront's stores of a step are one run), stored
                 // next step
-                const int64_t pv = o.has_prev ? o.prev : 0;
-                pend_k = k;
-                pend_a = make_int4((o.action & 0xFFFF) | ((o.has_prev ? KME_OUT_HAS_PREV : 0) << 16), o.size, lo32(pv), hi32(pv));
-                pend_ntr = (int32_t)o.ntr;
+                if (o.ntr >= OS_MAX_NTR) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
+                pend_pos = S.os_lanes ? os_pos_light(S, g, k - b) : (size_t)k;
+                pend_a = os_pack(o.action, o.has_prev, o.ntr, o.size, o.has_prev ? o.prev : 0);
                 pend = true;
             }
             n_rest += o.rested ? 1u : 0u;
             n_cancel += (cxl && ok) ? 1u : 0u;
             LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
         }
-        if (pend && !KME_DIAG_NO_OUT) {
-            KG int4* os = S.osort + 2 * (size_t)pend_k;
-            os[0] = pend_a;
-            os[1] = make_int4(pend_ntr, 0, 0, 0);
-        }
-        LST(if (lane_id() == __ffsll((long long)__ballot(1)) - 1) for (int q = 0; q < 8; ++q) atomicAdd(&S.dbg[q], lacc[q]);)
+        if (pend && !KME_DIAG_NO_OUT) S.osort[pend_pos] = pend_a;
+        LST(if (lane_id() == __ffsll((long long)__ballot(1)) - 1) for (int q = 0; q < 12; ++q) atomicAdd(&S.dbg[q], lacc[q]);)
         w.store_group();
     }
     // per-wavefront sums onto the shard line (k_tsh_fold adds the lines up)
@@ -2575,16 +2584,29 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     if (S.ctr[ci(C_FALLBACK)]) return;                   // k_serial answers the epoch
     const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
-        if (S.route_grp[i] < 0) continue;
+        const int32_t act = io.action[i];
+        if (act == BUY || act == SELL) {   // k_table's work, fused (the oid-table entry of the order)
+            const uint32_t h = S.epos[i];
+            if (h != OT_DEAD) {
+                const int32_t rs = S.rest_slot[i];
+                S.otab[h] = hentry(oid_fp(io.oid[i]), rs >= 0 ? (uint32_t)rs : OT_DEAD);
+            }
+        }
+        const int32_t g = S.route_grp[i];
+        if (g < 0) continue;
         if (i >= lim) { io.n_trades[i] = 0; continue; }
-        const KG int4* os = S.osort + 2 * (size_t)S.rank[i];
-        const int4 a = os[0];
-        const int32_t ntr = os[1].x;
-        io.out_action[i] = a.x & 0xFFFF;
-        io.out_flags[i] = (uint8_t)((a.x >> 16) & KME_OUT_HAS_PREV);
+        const uint32_t k = (uint32_t)S.rank[i];
+        size_t pos = k;
+        if (S.os_lanes) {   // a light group's record: step-major (os_pos_light)
+            const uint32_t b = S.seg[g], e = S.seg[g + 1];
+            if (e - b <= (uint32_t)S.light_max) pos = os_pos_light(S, g, k - b);
+        }
+        const int4 a = S.osort[pos];
+        io.out_action[i] = a.x & 0xFF;
+        io.out_flags[i] = (uint8_t)((a.x >> 8) & KME_OUT_HAS_PREV);
         io.out_size[i] = a.y;
         io.out_prev[i] = mk64(a.z, a.w);
-        io.n_trades[i] = (uint32_t)ntr;
+        io.n_trades[i] = (uint32_t)a.x >> 9;
     }
 }
 
@@ -2650,7 +2672,8 @@ __global__ void __launch_bounds__(256) k_tsh_fold(DevState S) {
 // Each BUY/SELL's pending entry (k_emap) becomes its rest slot, or OT_DEAD if it did not rest: one
 // plain store at the recorded position, no probe.  An order that rested and left the book later in
 // the epoch keeps a stale slot entry, dropped by validation like every lazily deleted one.
-__global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io) {
+__global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io, int funded) {
+    if (funded && !S.ctr[ci(C_FALLBACK)]) return;   // k_unsort did it (FUNDED epochs matched in parallel)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
         if (a != BUY && a != SELL) continue;
@@ -2797,7 +2820,9 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
-    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);   // one thread per record, as k_unsort
+    const int funded = S.mode == KME_MODE_FUNDED;
+    if (funded && !S.fallback) return;   // only a serial (fallback) epoch needs it after k_unsort
+    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io, funded);   // one thread per record, as k_unsort
 }
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);

@@ -11,6 +11,7 @@ constexpr int RADIX_BITS = 9;        // digit width of the partition passes
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
 constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT_MAX overrides)
 constexpr int kLaneTradeChunk = 8;    // trade scratch slots a k_match_lanes lane reserves at a time
+constexpr int kOsLanesMaxLight = 512;  // light_max up to which light groups' OUT echo goes step-major
 
 // FUNDED pipeline
 void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch

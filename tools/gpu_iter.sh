@@ -18,6 +18,7 @@ for args in "$@"; do
   rc=$?; echo "bench [$args] rc=$rc"
   [ $rc -eq 0 ] || { tail -5 $OUT/bench.err; exit $rc; }
 done
+[ -f $OUT/bench.jsonl ] || exit 0
 python3 - $OUT/bench.jsonl <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
