@@ -28,6 +28,12 @@
 
 namespace kme {
 
+#if defined(__HIPCC__)
+#define KDEV_HOST_INLINE __host__ __device__ inline
+#else
+#define KDEV_HOST_INLINE inline
+#endif
+
 constexpr int NLEV = 128;          // price levels 0..126 (+1 pad)
 constexpr int NACT = 11;
 
@@ -67,11 +73,17 @@ struct TradeRec {                  // == kme_trade
 };
 static_assert(sizeof(TradeRec) == 32, "TradeRec");
 
-struct TradeTmp {                  // unordered trade scratch written by the group wavefronts
-    TradeRec t;
-    int32_t seq, ord;
+struct TradeTmp {                  // unordered trade scratch written by the group wavefronts, two
+    int64_t moid, maid;            // 16-B parts (one store each): the maker, then
+    int32_t seq;                   //   the taker's input index (-1: a hole k_scatter skips),
+    uint32_t ordp;                 //   the trade's ordinal | maker price << 23 | (maker sid < 0) << 30,
+    int32_t size, group;           //   the size and the symbol group (the maker's sid is +-group)
 };
-static_assert(sizeof(TradeTmp) == 40, "TradeTmp");
+static_assert(sizeof(TradeTmp) == 32, "TradeTmp");
+constexpr uint32_t TT_ORD_BITS = 23;       // a record's trade ordinals (OS_MAX_NTR) fit
+KDEV_HOST_INLINE uint32_t tt_ordp(uint32_t ord, int32_t price, bool sneg) {
+    return ord | ((uint32_t)price << TT_ORD_BITS) | (sneg ? 1u << 30 : 0u);
+}
 
 struct PosEntry { int64_t k0, k1, v0, v1; };   // Positions: UUID(aid,sid) -> UUID(amount,available)
 

@@ -696,6 +696,7 @@ struct Rec {
     int32_t lane;                 // lane of the record in its batch
 };
 constexpr uint32_t OS_MAX_NTR = 1u << 23;   // trades of one record the packed OUT echo (osort) can count
+static_assert(OS_MAX_NTR == 1u << TT_ORD_BITS, "a trade's ordinal in TradeTmp::ordp");
 // What process() decided for one record (the OUT echo fields and its trade count).
 struct Out {
     int32_t action, size;
@@ -1525,11 +1526,8 @@ struct GroupWave {
         if (lane < tcnt) {
             const int4 a = L.trd[2 * lane], b = L.trd[2 * lane + 1];
             KG int4* r = reinterpret_cast<KG int4*>(&ttmp[pos + lane]);
-            KG int2* r2 = reinterpret_cast<KG int2*>(&ttmp[pos + lane]);
-            const int64_t sid = (b.x >> 8) & 1 ? -(int64_t)g : (int64_t)g;
             r[0] = a;
-            r[1] = make_int4(lo32(sid), hi32(sid), b.x & 0xFF, b.y);
-            r2[4] = make_int2(b.z, b.w);
+            r[1] = make_int4(b.z, (int32_t)tt_ordp((uint32_t)b.w, b.x & 0xFF, (b.x >> 8) & 1), b.y, g);
         }
         sync_lds();
         set_gs(GS_TCNT, 0);
@@ -2000,6 +1998,8 @@ struct GroupLane {
     uint32_t cur;
     bool dead;
     size_t tpos, tlim;            // this lane's reserved trade scratch [tpos, tlim) (LANE_TCH at a time)
+    uint32_t tspare;              // a spare reservation (shard offset), valid if has_spare: requested
+    bool has_spare;               //   with a record's first gather, so running out costs no round trip
     LST(uint32_t nload = 0;)      // (stamps build) maker loads of the sweep beyond the first
 
     KDEV GroupLane(const DevState& s, const EpochIO& e, int32_t (*f)[64], int32_t gg)
@@ -2009,6 +2009,7 @@ struct GroupLane {
         exists = 0; free_head = -1; chunk_next = chunk_end = 0; fsp = 0;
         cur = 0; dead = false;
         tpos = tlim = 0;
+        tspare = 0; has_spare = false;
     }
     KDEV void die(int status, int detail) { raise_thread(S.ctr, status, detail, (int64_t)cur); dead = true; }
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
@@ -2022,9 +2023,12 @@ struct GroupLane {
         b0l = (uint64_t)mk64(a.x, a.y); b0m = (uint64_t)mk64(a.z, a.w);
         b1l = (uint64_t)mk64(b.x, b.y); b1m = (uint64_t)mk64(b.z, b.w);
         exists = c.x; free_head = c.y; chunk_next = c.z; chunk_end = c.w;
+        if (free_head >= 0) load_block();                   // once per epoch, before the first record
     }
     KDEV void store_group() {
-        while (tpos < tlim) mark_hole(tpos++);               // the reservation's unused slots
+        while (tpos < tlim) mark_hole(tpos++);               // the reservations' unused slots
+        if (has_spare)
+            for (uint32_t q = tspare; q < tspare + LANE_TCH && q < S.tshard_cap; ++q) mark_hole((size_t)tbase + q);
         while (fsp > 0) spill_block(fsp > FBLK ? fsp - FBLK : 0);
         KG int4* gs = reinterpret_cast<KG int4*>(&S.grp[g]);
         gs[0] = make_int4(lo32((int64_t)b0l), hi32((int64_t)b0l), lo32((int64_t)b0m), hi32((int64_t)b0m));
@@ -2048,23 +2052,25 @@ struct GroupLane {
         free_head = host;
         fsp = b;
     }
+    // the free-list block at free_head onto the (empty) stack: its ids and the block's own slot
+    KDEV void load_block() {
+        const int32_t blk = free_head;
+        const KG int4* d = reinterpret_cast<const KG int4*>(&S.pool[blk]);
+        int4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = d[k];
+        const int32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                               v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+        const int32_t cnt = w[1];
+        fs[0][lane] = blk;
+#pragma unroll
+        for (int k = 0; k < FBLK - 1; ++k) if (k < cnt) fs[1 + k][lane] = w[2 + k];
+        fsp = cnt + 1;
+        free_head = w[0];
+    }
     KDEV int32_t alloc_slot() {
+        if (fsp == 0 && free_head >= 0) load_block();       // (a load in the record's step)
         if (fsp > 0) return fs[--fsp][lane];
-        if (free_head >= 0) {
-            const int32_t blk = free_head;
-            const KG int4* d = reinterpret_cast<const KG int4*>(&S.pool[blk]);
-            int4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = d[k];
-            const int32_t w[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
-                                   v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
-            const int32_t cnt = w[1];
-#pragma unroll
-            for (int k = 0; k < FBLK - 1; ++k) if (k < cnt) fs[k][lane] = w[2 + k];
-            fsp = cnt;
-            free_head = w[0];
-            return blk;
-        }
         if (chunk_next >= chunk_end) {
             // one bump reservation for every lane of the wavefront that needs a chunk now
             const unsigned long long need = __ballot(1);
@@ -2088,9 +2094,7 @@ struct GroupLane {
     // ---------------- trades: one TradeTmp per trade.  Each lane reserves LANE_TCH slots at a time
     // (one atomic per wavefront for the lanes that run out), so most trades need no returning
     // atomic on the record's chain; unused slots are holes (seq = -1) that k_scatter skips.
-    KDEV void mark_hole(size_t pos) {
-        reinterpret_cast<KG int2*>(&S.ttmp[pos])[4] = make_int2(-1, 0);
-    }
+    KDEV void mark_hole(size_t pos) { S.ttmp[pos].seq = -1; }
     KDEV void refill_trades() {
         const unsigned long long need = __ballot(1);
         const int leader = __ffsll((long long)need) - 1;
@@ -2113,19 +2117,30 @@ struct GroupLane {
         tpos = (size_t)TSHARDS * S.tshard_cap + ob;
         tlim = tpos + LANE_TCH;
     }
+    // with the record's first gather: a spare reservation for a lane about to run out (one
+    // returning atomic per lane, in flight with the gather)
+    KDEV void request_spare() {
+        if (!has_spare && tlim - tpos <= 2) {
+            tspare = (uint32_t)atomicAdd(&tsh[TS_USED], (unsigned long long)LANE_TCH);
+            has_spare = true;
+        }
+    }
     KDEV void emit(uint32_t ord, int64_t moid, int64_t maid, int32_t msneg, int32_t mprice, int32_t ts) {
         if (tpos == tlim) {
-            refill_trades();
-            if (dead) return;
+            if (has_spare && tspare + LANE_TCH <= S.tshard_cap) {
+                tpos = (size_t)tbase + tspare;
+                tlim = tpos + LANE_TCH;
+                has_spare = false;
+            } else {
+                refill_trades();
+                if (dead) return;
+            }
         }
         const size_t pos = tpos++;
         if (KME_DIAG_NO_TRADE) return;
-        const int64_t msid = msneg ? -(int64_t)g : (int64_t)g;
         KG int4* r = reinterpret_cast<KG int4*>(&S.ttmp[pos]);
-        KG int2* r2 = reinterpret_cast<KG int2*>(&S.ttmp[pos]);
         r[0] = make_int4(lo32(moid), hi32(moid), lo32(maid), hi32(maid));
-        r[1] = make_int4(lo32(msid), hi32(msid), mprice, ts);
-        r2[4] = make_int2((int32_t)cur, (int32_t)ord);
+        r[1] = make_int4((int32_t)cur, (int32_t)tt_ordp(ord, mprice, msneg != 0), ts, g);
     }
 
     // ---------------- tryMatch, KP:225-263: the loop of GroupWave::try_match (no sweep scan), from
@@ -2346,6 +2361,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     vslot = S.rest_slot[-(r.tgt + 2)];
                 }
             }
+            if (order) w.request_spare();
             if (pend && !KME_DIAG_NO_OUT) S.osort[pend_pos] = pend_a;
             pend = false;
             LST({ const unsigned long long t1 = lstamp(); lacc[1] += t1 - lt; lt = t1; })
@@ -2652,7 +2668,15 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
         for (int q = 0; q < SCATTER_ITEMS; ++q) off[q] = r[q].seq >= 0 && (uint32_t)r[q].seq < lim ? io.trade_off[r[q].seq] : 0;
 #pragma unroll
         for (int q = 0; q < SCATTER_ITEMS; ++q)
-            if (r[q].seq >= 0 && (uint32_t)r[q].seq < lim) io.trades[off[q] + (uint32_t)r[q].ord] = r[q].t;
+            if (r[q].seq >= 0 && (uint32_t)r[q].seq < lim) {
+                const uint32_t ordp = r[q].ordp;
+                TradeRec t;
+                t.moid = r[q].moid; t.maid = r[q].maid;
+                t.msid = (ordp >> 30) & 1 ? -(int64_t)r[q].group : (int64_t)r[q].group;
+                t.mprice = (int32_t)((ordp >> TT_ORD_BITS) & 0x7F);
+                t.size = r[q].size;
+                io.trades[off[q] + (ordp & ((1u << TT_ORD_BITS) - 1))] = t;
+            }
     }
 }
 // The shard lines' rest / cancel counts into the counters block; the lines zeroed for the next epoch.

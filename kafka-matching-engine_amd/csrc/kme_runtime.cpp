@@ -185,10 +185,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.trades_cap = cfg->max_trades;
     // trade scratch: TSHARDS shard regions (2x the even share, so only skewed load spills) and an
     // overflow region that alone holds an epoch's worth of trades plus what reservations can waste:
-    // k_match_lanes reserves LANE_TCH slots per lane at a time (up to LANE_TCH - 1 unused per light
-    // group, at most min(G, E) of them), and a reservation that straddles a shard region's end
-    // leaves the straddled part as holes (at most one per shard and matcher)
-    const uint64_t lane_waste = (uint64_t)(kLaneTradeChunk - 1) * std::min<uint64_t>(G, E);
+    // k_match_lanes reserves LANE_TCH slots per lane at a time and holds one spare reservation (up
+    // to 2 LANE_TCH - 1 unused per light group, at most min(G, E) of them), and a reservation that
+    // straddles a shard region's end leaves the straddled part as holes (at most one per shard and
+    // matcher)
+    const uint64_t lane_waste = (uint64_t)(2 * kLaneTradeChunk - 1) * std::min<uint64_t>(G, E);
     const uint64_t ttmp_ov = funded ? (uint64_t)cfg->max_trades + 64 + lane_waste + 64ull * TSHARDS : 1;
     const uint64_t tshard_cap = funded ? std::max<uint64_t>(256, (2 * (uint64_t)cfg->max_trades + TSHARDS - 1) / TSHARDS) : 0;
     const uint64_t ttmp_total = ttmp_ov + (uint64_t)TSHARDS * tshard_cap;
