@@ -317,14 +317,15 @@ def main():
               f"all-gathered block: {md_gather})", file=sys.stderr, flush=True)
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)
-        d = eng.debug_counters().astype(np.float64).reshape(-1)[:16]
-        steps = max(1.0, d[0])
-        names = ["steps", "loop_top_cycles", "step_cycles", "lane_steps", "lane_steps_waiting", "trade_refills",
-                 "freelist_block_loads", "pool_bumps", "blocking_level_loads", "records", "head_waits", "maker_waits",
-                 "level_waits", "cancel_node_waits"]
-        print(json.dumps({"lane_stamps": {"per_wave_step": {n: d[q] / steps for q, n in enumerate(names)},
-                                          "totals": {n: d[q] for q, n in enumerate(names)},
-                                          "ms_per_epoch_match": float(np.mean(match_ms))}}), flush=True)
+        d = eng.debug_counters().astype(np.float64).reshape(-1)[:12]
+        names = ["drain", "gather1", "gather2", "record", "out", "record.try_match", "record.rest"]
+        tot = d[:5].sum()
+        print(json.dumps({"lane_stamps": {"share": {n: d[q] / tot for q, n in enumerate(names)},
+                                          "cycles_per_step": {n: d[q] / max(1, d[7]) for q, n in enumerate(names)},
+                                          "sweep": {"steps_with_extra_maker_load": d[8] / max(1, d[7]),
+                                                    "extra_loads_per_lane_step": d[9] / max(1, d[7]) / 32,
+                                                    "max_extra_loads_per_step": d[10] / max(1, d[7])},
+                                          "steps": d[7], "ms_per_epoch_match": float(np.mean(match_ms))}}), flush=True)
         return
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
         rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 32)

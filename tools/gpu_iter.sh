@@ -24,7 +24,7 @@ import json, sys
 for l in open(sys.argv[1]):
     d = json.loads(l)
     if "lane_stamps" in d:
-        print({k: round(v, 3) for k, v in d["lane_stamps"]["per_wave_step"].items()}, round(d["lane_stamps"]["ms_per_epoch_match"], 3))
+        print({k: round(v) for k, v in d["lane_stamps"]["cycles_per_step"].items()}, round(d["lane_stamps"]["ms_per_epoch_match"], 3))
         continue
     print(d["config"]["symbols_per_gpu_rank0"], d["config"]["epoch_records"], round(d["value"] / 1e6, 1), "M/s p99",
           round(d["p99_epoch_ms"], 2), {k: v for k, v in d["phase_ms_last_epoch"].items() if v})
