@@ -226,7 +226,7 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     E = args.epoch
-    total = max(args.orders, (args.warmup + args.steps) * E)
+    total = max(args.orders, (args.warmup + args.steps + 1) * E)   # + 1: the phase-breakdown epoch
     setup, stream, sids, nacc, shards, desc = make_workload(
         args.workload, total, rank, world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
     max_sid = int(sids.max())
@@ -243,7 +243,7 @@ def main():
     torch.cuda.set_stream(work)
     assert work.cuda_stream != 0
     eng.set_stream(work.cuda_stream)
-    eng.enable_timing(True)
+    eng.enable_timing("match")   # timed epochs: events around the matching kernels only
     eng.process(setup)  # CREATE_BALANCE / TRANSFER / ADD_SYMBOL records (host path)
 
     # inputs resident in HBM before timing
@@ -252,7 +252,7 @@ def main():
         "aid": torch.from_numpy(stream.aid).to(dev), "sid": torch.from_numpy(stream.sid).to(dev),
         "price": torch.from_numpy(stream.price).to(dev), "size": torch.from_numpy(stream.size).to(dev),
     }
-    orders_per_epoch = [int(stream.slice(k * E, (k + 1) * E).n_orders()) for k in range(args.warmup + args.steps)]
+    orders_per_epoch = [int(stream.slice(k * E, (k + 1) * E).n_orders()) for k in range(args.warmup + args.steps + 1)]
     # market data: this rank's symbols' top of book, all-gathered (16 B per symbol)
     rows, per_rank = market_data_layout(world, args.workload, args.symbols)
     groups = torch.from_numpy(sids.astype(np.int32)).to(dev)
@@ -302,7 +302,12 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    assert n_orders == sum(orders_per_epoch[args.warmup:]), "device order count mismatch"
+    assert n_orders == sum(orders_per_epoch[args.warmup:args.warmup + args.steps]), "device order count mismatch"
+    # the phase breakdown, from one more epoch with every phase's events (outside the timed region:
+    # the events serialise the stream)
+    eng.enable_timing("all")
+    run_epoch(args.warmup + args.steps)
+    phases_all = eng.phase_times()
 
     # market data check (outside the timed region): this rank's rows of the full-range snapshot,
     # its own compact snapshot, and its block of the all-gathered one agree
@@ -390,7 +395,7 @@ def main():
                             "collective": ("gloo all_gather (one-GPU rehearsal)" if rehearsal else "RCCL all_gather_into_tensor per epoch")
                             if world > 1 else "none (N = 1)",
                             "verified": md_all},
-            "phase_ms_last_epoch": {k: round(v, 4) for k, v in eng.phase_times().items()},
+            "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "

@@ -232,6 +232,10 @@ kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uin
 #define KME_MAX_PHASES 16
 kme_status kme_phase_times(kme_engine* e, float* ms, int* n_phases);
 const char* kme_phase_name(int i);
+/* 0 = off, KME_TIMING_ALL (1) = every phase, KME_TIMING_MATCH = the matching phase only (timing
+ * events serialise the stream around them, ~10 us each) */
+#define KME_TIMING_ALL 1
+#define KME_TIMING_MATCH 2
 kme_status kme_enable_timing(kme_engine* e, int enable);
 
 /* Serialises a processed epoch exactly as consumer.js prints MatchOut (consumer.js:19):

@@ -554,16 +554,24 @@ __global__ void __launch_bounds__(256) k_radix_hist(DevState S, EpochIO io, int 
     for (int q = 0; q < RADIX_PER_T; ++q) S.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
 }
 
+KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
+
+// One tile's scatter, staged in LDS: the tile is first ordered by digit in LDS (stable: the
+// wavefront match-any ranks of the chunk loop), then written out in that order, so that each
+// digit's run of the tile leaves in consecutive lanes (coalesced stores) instead of one scattered
+// 4-B store per element and array.
 __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, int pass, int src) {
-    __shared__ uint32_t running[RADIX_DIGITS];
+    static_assert(RADIX_DIGITS == 512, "two digits per thread");
+    __shared__ uint32_t running[RADIX_DIGITS];   // the tile histogram, then the next free local slot
+    __shared__ uint32_t gdelta[RADIX_DIGITS];    // digit d's global offset minus its local start
     __shared__ uint32_t wcnt[4][RADIX_DIGITS];
+    __shared__ uint32_t lkey[RADIX_TILE], lval[RADIX_TILE];
+    __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    for (int q = 0; q < RADIX_PER_T; ++q) running[t + 256 * q] = S.ghist[(t + 256 * q) * gridDim.x + blockIdx.x];
     const uint32_t base = blockIdx.x * RADIX_TILE;
     const int dst = src ^ 1;
+    const int shift = RADIX_BITS * pass;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    // the tile's keys and values are loaded up front: a load issued inside the loop would wait for
-    // the previous chunk's scattered stores too (vmcnt counts both, in order)
     constexpr int RJ = RADIX_TILE / 256;
     uint32_t keys[RJ], vals[RJ];
 #pragma unroll
@@ -575,16 +583,30 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
             vals[j] = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
         }
     }
+    for (int q = 0; q < RADIX_PER_T; ++q) running[t + 256 * q] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RJ; ++j)
+        if (base + j * 256 + t < io.n) atomicAdd(&running[(keys[j] >> shift) & (RADIX_DIGITS - 1)], 1u);
+    __syncthreads();
+    {   // local starts (exclusive scan of the tile histogram) and the global offsets (k_radix_hist + scan)
+        const uint32_t h0 = running[2 * t], h1 = running[2 * t + 1];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_256(h0 + h1, wsum, tot);
+        running[2 * t] = ex;
+        running[2 * t + 1] = ex + h0;
+        gdelta[2 * t] = S.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - ex;
+        gdelta[2 * t + 1] = S.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - (ex + h0);
+    }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
         for (int q = 0; q < RADIX_PER_T; ++q) {
             wcnt[0][t + 256 * q] = 0; wcnt[1][t + 256 * q] = 0; wcnt[2][t + 256 * q] = 0; wcnt[3][t + 256 * q] = 0;
         }
         __syncthreads();
-        const uint32_t k = base + j * 256 + t;
-        const bool valid = k < io.n;
-        const uint32_t key = keys[j], val = vals[j];
-        const uint32_t d = (key >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1);
+        const bool valid = base + j * 256 + t < io.n;
+        const uint32_t d = (keys[j] >> shift) & (RADIX_DIGITS - 1);
         // lanes of this wavefront with the same digit (match-any over the digit bits)
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < RADIX_BITS; ++b) {
@@ -597,9 +619,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
         if (valid) {
             uint32_t pos = running[d] + rank;
             for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][d];
-            (dst ? S.rkeys[1] : S.rkeys[0])[pos] = key;
-            (dst ? S.rvals[1] : S.rvals[0])[pos] = val;
-            if (pass == S.passes - 1 && S.rank) S.rank[val] = (int32_t)pos;
+            lkey[pos] = keys[j];
+            lval[pos] = vals[j];
         }
         __syncthreads();
         for (int q = 0; q < RADIX_PER_T; ++q) {
@@ -607,6 +628,21 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
             running[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
         }
         __syncthreads();
+    }
+    const uint32_t cnt = io.n - base < (uint32_t)RADIX_TILE ? io.n - base : (uint32_t)RADIX_TILE;
+    KG uint32_t* okeys = dst ? S.rkeys[1] : S.rkeys[0];
+    KG uint32_t* ovals = dst ? S.rvals[1] : S.rvals[0];
+    const bool last = pass == S.passes - 1 && S.rank;
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const uint32_t e = j * 256 + t;
+        if (e < cnt) {
+            const uint32_t key = lkey[e], val = lval[e];
+            const uint32_t pos = gdelta[(key >> shift) & (RADIX_DIGITS - 1)] + e;
+            okeys[pos] = key;
+            ovals[pos] = val;
+            if (last) S.rank[val] = (int32_t)pos;
+        }
     }
 }
 

@@ -6,7 +6,10 @@
 
 namespace kme {
 
-constexpr int RADIX_TILE = 4096;     // inputs per partition tile (256 threads x 16)
+#ifndef KME_RADIX_TILE
+#define KME_RADIX_TILE 4096
+#endif
+constexpr int RADIX_TILE = KME_RADIX_TILE;   // inputs per partition tile (256 threads x 16)
 constexpr int RADIX_BITS = 9;        // digit width of the partition passes
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
 constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT_MAX overrides)

@@ -63,7 +63,7 @@ struct kme_engine {
     bool pending = false;
     int failed = 0;
     int fail_status = 0, fail_detail = 0;
-    bool timing = false;
+    int timing = 0;                      // KME_TIMING_* (kme.h)
     hipEvent_t ev[PH_N * 2] = {};
     bool ev_used[PH_N] = {};
     float phase_ms[KME_MAX_PHASES] = {};
@@ -95,13 +95,18 @@ static kme_status dalloc(kme_engine* e, T** p, size_t count) {
         if (_s != KME_OK) { kme_destroy(e); return _s; } \
     } while (0)
 
+// Timing events serialise the stream around them (~10 us each, measured), so KME_TIMING_MATCH
+// brackets only the matching kernels.
+static bool timed(const kme_engine* e, int ph) {
+    return e->timing == KME_TIMING_ALL || (e->timing == KME_TIMING_MATCH && ph == PH_MATCH);
+}
 static void phase_begin(kme_engine* e, int ph, hipStream_t s = nullptr) {
-    if (!e->timing) return;
+    if (!timed(e, ph)) return;
     (void)hipEventRecord(e->ev[2 * ph], s ? s : e->stream);
     e->ev_used[ph] = true;
 }
 static void phase_end(kme_engine* e, int ph, hipStream_t s = nullptr) {
-    if (!e->timing) return;
+    if (!timed(e, ph)) return;
     (void)hipEventRecord(e->ev[2 * ph + 1], s ? s : e->stream);
 }
 
@@ -313,7 +318,7 @@ kme_status kme_set_stream(kme_engine* e, void* s) {
 
 kme_status kme_enable_timing(kme_engine* e, int enable) {
     if (!e) return KME_E_INVALID;
-    e->timing = enable != 0;
+    e->timing = enable == KME_TIMING_MATCH ? KME_TIMING_MATCH : enable != 0 ? KME_TIMING_ALL : 0;
     return KME_OK;
 }
 

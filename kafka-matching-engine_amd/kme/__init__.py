@@ -272,8 +272,10 @@ class Engine:
         if rc:
             raise KmeError(rc, "kme_set_stream")
 
-    def enable_timing(self, on: bool = True):
-        self._L.kme_enable_timing(self._h, 1 if on else 0)
+    def enable_timing(self, on=True):
+        """True / "all": every phase; "match": the matching phase only; False: off."""
+        mode = {"all": 1, "match": 2}.get(on, 1) if on else 0
+        self._L.kme_enable_timing(self._h, mode)
 
     def phase_times(self) -> dict:
         ms = (C.c_float * 16)()
