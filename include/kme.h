@@ -261,6 +261,33 @@ kme_status kme_order_from_json(const char* json, size_t len, int32_t* action, in
 /* Kafka's default keyed partitioner over decimal(|sid|) (murmur2, toPositive, % n). */
 uint32_t kme_shard_of(int64_t sid, uint32_t n_shards);
 
+/* Partition router (replaces kme/sharding.py PartitionRouter on the product
+ * path).  One MatchIn stream over n engines, each input answered by exactly one of them:
+ * BUY/SELL/ADD_SYMBOL/REMOVE_SYMBOL/PAYOUT -> kme_shard_of(sid, n); CANCEL (no symbol,
+ * exchange_test.js:101) -> the partition of the last BUY/SELL with its oid (a directory kept by the
+ * router; an unknown oid -> 0, which rejects it, KP:290); CREATE_BALANCE/TRANSFER -> every
+ * partition (KME_ROUTE_ALL; echoed by partition 0 only); anything else -> 0.  Not thread-safe. */
+typedef struct kme_router kme_router;
+#define KME_ROUTE_ALL (-1)
+typedef struct kme_orders_buf {   /* writable kme_orders */
+    int32_t* action;
+    int64_t* oid;
+    int64_t* aid;
+    int64_t* sid;
+    int32_t* price;
+    int32_t* size;
+} kme_orders_buf;
+kme_status kme_router_create(uint32_t n_partitions, uint64_t directory_capacity, kme_router** out);
+kme_status kme_router_destroy(kme_router* r);
+/* dest[i] = partition of input i (or KME_ROUTE_ALL); updates the oid directory. */
+kme_status kme_router_route(kme_router* r, const kme_orders* in, uint32_t n, int32_t* dest);
+/* Routes and splits: partition k's records, in arrival order, into parts[k] (arrays of capacity
+ * n), counts[k] of them; optional echo[k][j] = 1 if partition k answers its j-th record (0 for the
+ * copies of account records on partitions > 0) and index[k][j] = its input index. */
+kme_status kme_router_split(kme_router* r, const kme_orders* in, uint32_t n, const kme_orders_buf* parts,
+                            uint32_t* counts, uint8_t* const* echo, uint32_t* const* index);
+uint64_t kme_router_directory_size(const kme_router* r);
+
 /* Diagnostics: per-symbol-group words written by a -DKME_STAMPS build of the match kernel
  * (in-kernel s_memtime stamps; zero in the product build).  Copies min(n, max_symbols * 32). */
 #define KME_DBG_WORDS 32

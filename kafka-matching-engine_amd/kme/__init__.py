@@ -71,6 +71,7 @@ EXPORTS = [
     "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
+    "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
 ]
 
 _lib = None
@@ -128,6 +129,11 @@ def lib():
         "kme_processor_punctuate": (st, [vp]),
         "kme_processor_close": (st, [vp]),
         "kme_processor_last_status": (st, [vp, C.POINTER(kme_epoch_status)]),
+        "kme_router_create": (st, [u32, C.c_uint64, C.POINTER(vp)]),
+        "kme_router_destroy": (st, [vp]),
+        "kme_router_route": (st, [vp, C.POINTER(kme_orders), u32, vp]),
+        "kme_router_split": (st, [vp, C.POINTER(kme_orders), u32, vp, vp, vp, vp]),
+        "kme_router_directory_size": (C.c_uint64, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -422,3 +428,78 @@ def tape_json_from(orders: Orders, res: EpochResult) -> str:
 
 def shard_of(sid: int, n: int) -> int:
     return int(lib().kme_shard_of(int(sid), int(n)))
+
+
+class kme_orders_buf(C.Structure):
+    _fields_ = [("action", C.c_void_p), ("oid", C.c_void_p), ("aid", C.c_void_p), ("sid", C.c_void_p),
+                ("price", C.c_void_p), ("size", C.c_void_p)]
+
+
+class Router:
+    """The C-ABI partition router (kme_router_*, include/kme.h): kme/sharding.py PartitionRouter's
+    rules in native code, for the product path."""
+
+    def __init__(self, n: int, directory_capacity: int = 1 << 20):
+        self._L = lib()
+        self.n = n
+        h = C.c_void_p()
+        rc = self._L.kme_router_create(n, directory_capacity, C.byref(h))
+        if rc:
+            raise KmeError(rc, "kme_router_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.kme_router_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def route(self, orders) -> np.ndarray:
+        """Partition of every record (-1 = every partition); updates the oid directory."""
+        ko, keep = _soa(orders)
+        dest = np.empty(len(orders), np.int32)
+        rc = self._L.kme_router_route(self._h, C.byref(ko), len(orders), dest.ctypes.data_as(C.c_void_p))
+        if rc:
+            raise KmeError(rc, "kme_router_route")
+        return dest
+
+    def split(self, orders):
+        """-> (parts, echo, seqs) as PartitionRouter.route: per partition its Orders, the mask of
+        the records it answers, and their input indices."""
+        from .workloads import Orders
+
+        n = len(orders)
+        ko, keep = _soa(orders)
+        bufs = [{"action": np.empty(n, np.int32), "oid": np.empty(n, np.int64), "aid": np.empty(n, np.int64),
+                 "sid": np.empty(n, np.int64), "price": np.empty(n, np.int32), "size": np.empty(n, np.int32)}
+                for _ in range(self.n)]
+        parts_c = (kme_orders_buf * self.n)(*[kme_orders_buf(*[b[f].ctypes.data for f in
+                                                               ("action", "oid", "aid", "sid", "price", "size")])
+                                              for b in bufs])
+        counts = np.zeros(self.n, np.uint32)
+        echo = [np.empty(n, np.uint8) for _ in range(self.n)]
+        index = [np.empty(n, np.uint32) for _ in range(self.n)]
+        echo_p = (C.c_void_p * self.n)(*[e.ctypes.data for e in echo])
+        index_p = (C.c_void_p * self.n)(*[x.ctypes.data for x in index])
+        rc = self._L.kme_router_split(self._h, C.byref(ko), n, C.cast(parts_c, C.c_void_p),
+                                      counts.ctypes.data_as(C.c_void_p), C.cast(echo_p, C.c_void_p),
+                                      C.cast(index_p, C.c_void_p))
+        if rc:
+            raise KmeError(rc, "kme_router_split")
+        parts, echos, seqs = [], [], []
+        for k in range(self.n):
+            c = int(counts[k])
+            b = bufs[k]
+            parts.append(Orders(b["action"][:c].copy(), b["oid"][:c].copy(), b["aid"][:c].copy(), b["sid"][:c].copy(),
+                                b["price"][:c].copy(), b["size"][:c].copy(), None))
+            echos.append(echo[k][:c].astype(bool))
+            seqs.append(index[k][:c].astype(np.int64))
+        return parts, echos, seqs
+
+    def directory_size(self) -> int:
+        return int(self._L.kme_router_directory_size(self._h))

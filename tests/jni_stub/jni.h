@@ -1,0 +1,40 @@
+/* A declaration subset of the JNI C interface (the types and the function-table members that
+ * integration/jni/kme_jni.c uses), for a compile-only check of that file in this container, which
+ * has no JDK.  Member order is NOT the JDK's: nothing compiled against this header may be linked
+ * or run.  integration/jni/build.sh builds against the real $JAVA_HOME/include/jni.h. */
+#ifndef KME_TEST_JNI_STUB_H
+#define KME_TEST_JNI_STUB_H
+#include <stdint.h>
+
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#define JNI_ABORT 2
+
+typedef int32_t jint;
+typedef int64_t jlong;
+typedef int8_t jbyte;
+typedef uint8_t jboolean;
+typedef jint jsize;
+typedef struct _jobject* jobject;
+typedef jobject jclass;
+typedef jobject jstring;
+typedef jobject jarray;
+typedef jarray jintArray;
+typedef jarray jlongArray;
+typedef jarray jbyteArray;
+typedef jobject jthrowable;
+
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_* JNIEnv;
+struct JNINativeInterface_ {
+    jclass (*FindClass)(JNIEnv* env, const char* name);
+    jint (*ThrowNew)(JNIEnv* env, jclass clazz, const char* msg);
+    jsize (*GetArrayLength)(JNIEnv* env, jarray array);
+    void* (*GetPrimitiveArrayCritical)(JNIEnv* env, jarray array, jboolean* isCopy);
+    void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
+    void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
+    jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
+    const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
+    void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
+};
+#endif

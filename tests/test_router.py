@@ -1,0 +1,63 @@
+"""The C-ABI partition router (kme_router_*, kme_router.cpp) against kme/sharding.py's
+PartitionRouter, the rules INTEGRATION.md §6 states: same partition for every record, the same
+per-partition streams, echo masks and input indices -- on the C2/C3, C5 (cancel/replace) and
+exchange_test.js streams, across several epochs (the oid directory carries over)."""
+import time
+
+import numpy as np
+import pytest
+
+import kme
+from kme import sharding, workloads as W
+
+
+def _streams():
+    setup = W.funded_setup(64, range(1, 257))
+    return {
+        "c3": W.Orders.concat([setup, W.uniform(40_000, n_symbols=256, n_accounts=64, seed=3)]),
+        "c5": W.Orders.concat([setup, W.cancel_replace(40_000, n_symbols=256, n_accounts=64, seed=4)]),
+        "exchange": W.exchange_test(5_000, seed=6),
+    }
+
+
+@pytest.mark.parametrize("name", ["c3", "c5", "exchange"])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_router_matches_partition_router(name, n):
+    orders = _streams()[name]
+    py = sharding.PartitionRouter(n)
+    cr = kme.Router(n, directory_capacity=1024)      # grows past its initial capacity
+    step = 7_919
+    for a in range(0, len(orders), step):
+        part = orders.slice(a, min(len(orders), a + step))
+        pp, pe, ps = py.route(part)
+        cp, ce, cs = cr.split(part)
+        for k in range(n):
+            for f in ("action", "oid", "aid", "sid", "price", "size"):
+                assert np.array_equal(getattr(cp[k], f), getattr(pp[k], f)), (k, f)
+            assert np.array_equal(ce[k], pe[k]), k
+            assert np.array_equal(cs[k] + a, ps[k]), k
+    assert cr.directory_size() == len(py.directory)
+
+
+def test_router_route_codes_and_unknown_cancel():
+    r = kme.Router(4)
+    o = W.Orders.from_rows([(W.CREATE_BALANCE, 0, 1, 0, 0, 0), (W.BUY, 77, 1, 12, 50, 3), (W.CANCEL, 77, 1, 0, 0, 0),
+                            (W.CANCEL, 78, 1, 0, 0, 0), (W.ADD_SYMBOL, 0, 0, 12, 0, 0), (9, 0, 0, 5, 0, 0),
+                            (W.SELL, -1, 1, -12, 40, 1), (W.CANCEL, -1, 1, 0, 0, 0)])
+    d = r.route(o)
+    p12 = kme.lib().kme_shard_of(12, 4)
+    assert d.tolist() == [-1, p12, p12, 0, p12, 0, p12, p12]
+
+
+def test_router_rate():
+    """The router is one pass with an oid-directory probe per BUY/SELL/CANCEL; it must not be the
+    bottleneck of a host feeding one engine (reported, loosely bounded)."""
+    orders = W.uniform(1 << 20, n_symbols=65_536, n_accounts=65_536, seed=9)
+    r = kme.Router(8, directory_capacity=1 << 21)
+    r.route(orders.slice(0, 1 << 16))
+    t = time.perf_counter()
+    r.route(orders)
+    dt = time.perf_counter() - t
+    rate = len(orders) / dt
+    print(f"router: {rate / 1e6:.1f} M records/s (one thread)")
+    assert rate > 5e6
