@@ -169,6 +169,73 @@ def reduce_stats(dist, torch, elapsed: float, n_orders: int, n_trades: int, ok: 
     return float(t.item()), float(sums[0].item()), float(sums[1].item()), bool(flag.item())
 
 
+def measure_host_path(eng, stream, first, n_epochs, E, dev, max_trades):
+    """The product path of a host caller at rate: epochs in pinned host memory,
+    H2D of epoch k+1 on one stream and D2H of epoch k's results on another while epoch k+1's kernels
+    run (double-buffered device inputs and results).  Timed from the first H2D to the last D2H;
+    PCIe-inclusive, so it is a secondary field, never the headline value."""
+    import torch
+
+    cols = ("action", "oid", "aid", "sid", "price", "size")
+    n_rec = n_epochs * E
+    a0 = first * E
+    host_in = {c: torch.from_numpy(np.ascontiguousarray(getattr(stream, c)[a0:a0 + n_rec])).pin_memory() for c in cols}
+    dev_in = [{c: torch.empty(E, dtype=host_in[c].dtype, device=dev) for c in cols} for _ in range(2)]
+    shapes = {"out_action": (E, torch.int32), "out_size": (E, torch.int32), "out_prev": (E, torch.int64),
+              "out_flags": (E, torch.uint8), "trade_off": (E + 1, torch.int32), "trades": (4 * max_trades, torch.int64)}
+    dev_out = [{k: torch.empty(n, dtype=t, device=dev) for k, (n, t) in shapes.items()} for _ in range(2)]
+    host_out = [{k: torch.empty(n, dtype=t).pin_memory() for k, (n, t) in shapes.items()} for _ in range(2)]
+    work = torch.cuda.current_stream(dev)
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_done = [torch.cuda.Event() for _ in range(2)]
+    ev_out = [torch.cuda.Event() for _ in range(2)]
+    n_trades = []
+
+    def h2d_copy(k):
+        b = k % 2
+        with torch.cuda.stream(h2d):
+            for c in cols:
+                dev_in[b][c].copy_(host_in[c][k * E:(k + 1) * E], non_blocking=True)
+            ev_in[b].record(h2d)
+
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    h2d_copy(0)
+    for k in range(n_epochs):
+        b = k % 2
+        work.wait_event(ev_in[b])
+        out = {key: t.data_ptr() for key, t in dev_out[b].items()}
+        out["trades_cap"] = max_trades
+        eng.submit_device({c: t.data_ptr() for c, t in dev_in[b].items()}, E, out=out)
+        ev_done[b].record(work)
+        if k + 1 < n_epochs:
+            h2d_copy(k + 1)          # dev_in[(k+1) % 2] was read by epoch k-1, finished at its wait()
+        with torch.cuda.stream(d2h):
+            d2h.wait_event(ev_done[b])
+            for key, t in dev_out[b].items():
+                if key != "trades":
+                    host_out[b][key].copy_(t, non_blocking=True)
+            ev_out[b].record(d2h)
+        st = eng.wait()
+        nt = int(st.n_trades)
+        n_trades.append(nt)
+        if nt:                       # this epoch's trades (count known now), behind its other results
+            with torch.cuda.stream(d2h):
+                host_out[b]["trades"][:4 * nt].copy_(dev_out[b]["trades"][:4 * nt], non_blocking=True)
+                ev_out[b].record(d2h)
+        ev_out[(k + 1) % 2].synchronize()   # host_out[(k+1) % 2] free for the next epoch
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    h2d_b = 36 * E
+    d2h_b = 21 * E + 4 + 32 * (sum(n_trades) / n_epochs)
+    return {"value": n_rec / dt, "unit": "records/s", "epochs": n_epochs, "epoch_records": E,
+            "h2d_bytes_per_epoch": h2d_b, "d2h_bytes_per_epoch": int(d2h_b),
+            "pcie_GBps_each_way": round(max(h2d_b, d2h_b) * n_epochs / dt / 1e9, 2),
+            "path": "pinned host SoA -> H2D (stream 1) | kernels (engine stream) | results D2H (stream 2), "
+                    "double-buffered; PCIe-inclusive, not the headline value"}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +251,9 @@ def parse_args(argv=None):
     ap.add_argument("--light-max", type=int, default=0,
                     help="diagnostic: kme_config.light_max (0 = default 128 records per group and epoch)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    ap.add_argument("--host-path-epochs", type=int, default=3,
+                    help="N = 1: epochs of the host-buffer path (pinned H2D + kernels + D2H, pipelined) "
+                         "measured after the device-resident ones (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
     ap.add_argument("--lane-stamps", action="store_true", help="diagnostic: print k_match_lanes step-segment shares and exit")
@@ -226,7 +296,9 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     E = args.epoch
-    total = max(args.orders, (args.warmup + args.steps + 1) * E)   # + 1: the phase-breakdown epoch
+    host_epochs = args.host_path_epochs if world == 1 else 0
+    # + 1: the phase-breakdown epoch; then the host-path epochs
+    total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs) * E)
     setup, stream, sids, nacc, shards, desc = make_workload(
         args.workload, total, rank, world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
     max_sid = int(sids.max())
@@ -308,6 +380,7 @@ def main():
     eng.enable_timing("all")
     run_epoch(args.warmup + args.steps)
     phases_all = eng.phase_times()
+    eng.enable_timing(False)
 
     # market data check (outside the timed region): this rank's rows of the full-range snapshot,
     # its own compact snapshot, and its block of the all-gathered one agree
@@ -320,6 +393,9 @@ def main():
     if not md_ok:
         print(f"rank {rank}: market data check failed (own snapshot vs full-range: {md_local}, "
               f"all-gathered block: {md_gather})", file=sys.stderr, flush=True)
+    # the host-buffer path (after the market-data check: its epochs move the books on)
+    host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, dev, cfg.max_trades) \
+        if host_epochs else None
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)
         d = eng.debug_counters().astype(np.float64).reshape(-1)[:12]
@@ -396,6 +472,7 @@ def main():
                             if world > 1 else "none (N = 1)",
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
+            "host_path": host_path,
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "

@@ -260,9 +260,15 @@ class Engine:
         return res
 
     # ---- device-resident epochs (bench): torch tensors or raw device pointers
-    def submit_device(self, ptrs: dict, n: int):
+    def submit_device(self, ptrs: dict, n: int, out: dict | None = None):
+        """Device epoch; `out` (device pointers out_action, out_size, out_prev, out_flags, trade_off,
+        trades, and trades_cap) receives the results instead of the engine-owned buffers."""
         s = kme_orders(*[C.c_void_p(int(ptrs[k])) for k in ("action", "oid", "aid", "sid", "price", "size")])
-        rc = self._L.kme_submit_epoch_device(self._h, C.byref(s), n, None)
+        r = None
+        if out is not None:
+            r = kme_epoch_result(*[C.c_void_p(int(out[k])) for k in ("out_action", "out_size", "out_prev", "out_flags",
+                                                                      "trade_off", "trades")], int(out["trades_cap"]))
+        rc = self._L.kme_submit_epoch_device(self._h, C.byref(s), n, C.byref(r) if r is not None else None)
         if rc:
             raise KmeError(rc, "kme_submit_epoch_device")
 
