@@ -251,6 +251,9 @@ def parse_args(argv=None):
     ap.add_argument("--light-max", type=int, default=0,
                     help="diagnostic: kme_config.light_max (0 = default 128 records per group and epoch)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    ap.add_argument("--pipeline", action="store_true",
+                    help="queue epoch k+1 before waiting for epoch k (+1.3% orders/s measured, p99 epoch "
+                         "latency 1.9 -> 3.7 ms: an epoch then waits behind the previous one)")
     ap.add_argument("--host-path-epochs", type=int, default=3,
                     help="N = 1: epochs of the host-buffer path (pinned H2D + kernels + D2H, pipelined) "
                          "measured after the device-resident ones (0 = skip)")
@@ -328,7 +331,8 @@ def main():
     # market data: this rank's symbols' top of book, all-gathered (16 B per symbol)
     rows, per_rank = market_data_layout(world, args.workload, args.symbols)
     groups = torch.from_numpy(sids.astype(np.int32)).to(dev)
-    tob = torch.full((rows, 4), -1, dtype=torch.int32, device=dev)
+    tobs = [torch.full((rows, 4), -1, dtype=torch.int32, device=dev) for _ in range(2)]
+    tob = tobs[0]
     tob_all = torch.zeros((world * rows, 4), dtype=torch.int32, device=dev)
 
     def epoch_ptrs(k):
@@ -337,11 +341,18 @@ def main():
     tape_buf = torch.empty(args.serialize * (512 * E + (1 << 20)), dtype=torch.uint8, device=dev)
     tape_bytes = []
 
-    def run_epoch(k):
+    def submit_epoch(k):
+        """Queue epoch k and its market-data snapshot (double-buffered: the next epoch may be queued
+        before this one is waited for)."""
+        nonlocal tob
+        tob = tobs[k % 2]
         eng.submit_device(epoch_ptrs(k), E)
         eng.top_of_book_groups(groups.data_ptr(), len(sids), tob.data_ptr())
         if world > 1:
             exchange_market_data(dist, tob, tob_all)   # market-data snapshot over RCCL / xGMI
+
+    def run_epoch(k):
+        submit_epoch(k)
         st = eng.wait()
         if args.serialize:  # MatchOut text of the epoch, printed on the GPU, left in HBM
             tape_bytes.append(eng.tape_json_device_into(epoch_ptrs(k), E, tape_buf.data_ptr(), tape_buf.numel()))
@@ -352,15 +363,29 @@ def main():
 
     lat, match_ms, bytes_alg, n_orders, n_trades = [], [], [], 0, 0
     mix = {"inputs": 0, "trades": 0, "rests": 0, "maker_visits": 0, "cancels_ok": 0}
+    # --pipeline: two epochs in flight (kme.h), epoch k + 1 queued before epoch k is waited for, so
+    # the GPU never idles on the host's turnaround between epochs (--serialize reads the
+    # engine-owned results of each epoch, so it runs them one at a time)
+    pipelined = args.pipeline and not args.serialize
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    t_sub = {}
     for j in range(args.steps):
         k = args.warmup + j
-        e0 = time.perf_counter()
-        st = run_epoch(k)
-        lat.append((time.perf_counter() - e0) * 1e3)
+        if pipelined:
+            if j == 0:
+                t_sub[k] = time.perf_counter()
+                submit_epoch(k)
+            if j + 1 < args.steps:
+                t_sub[k + 1] = time.perf_counter()
+                submit_epoch(k + 1)
+            st = eng.wait()
+        else:
+            t_sub[k] = time.perf_counter()
+            st = run_epoch(k)
+        lat.append((time.perf_counter() - t_sub[k]) * 1e3)   # submit -> results ready
         ph = eng.phase_times()
         match_ms.append(ph["match"])
         bytes_alg.append(algorithmic_bytes(st))

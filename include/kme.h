@@ -191,6 +191,12 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n,
  * orders of a just-created account (kme_submit_epoch does that split for host callers). */
 kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in_dev, uint32_t n,
                                    const kme_epoch_result* out_dev);
+/* Completes the OLDEST device epoch in flight.  Up to two device epochs may be in flight: a second
+ * kme_submit_epoch_device before kme_wait queues the next epoch behind the first on the stream (the
+ * GPU does not idle on the caller's turnaround; give each its own `out_dev`, the engine-owned
+ * buffers hold only the newest epoch's results).  A third submit, kme_submit_epoch, checkpoint and
+ * restore return KME_E_INVALID while epochs are in flight.  An epoch refused with KME_E_UNFUNDED
+ * while a later one is in flight fails the engine (that one ran without the refused records). */
 kme_status kme_wait(kme_engine* e, kme_epoch_status* st);
 /* Engine-owned device result buffers of the last device epoch. */
 kme_status kme_device_results(kme_engine* e, kme_epoch_result* out_dev);

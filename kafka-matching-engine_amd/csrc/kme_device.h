@@ -98,6 +98,8 @@ enum Ctr : int {
     C_ACCT_OPS,        // FUNDED: account records in the epoch
     C_BAL_USED, C_POS_USED,
     C_FALLBACK,        // FUNDED + KME_FLAG_SERIAL_FALLBACK: nonzero = this epoch runs serially
+    C_BUSY,            // FUNDED: groups k_match took this epoch (the host's stream choice for the next)
+    C_REBUILD_FAIL,    // oid-table rebuild: entries that found no slot (persistent, zeroed by the rebuild)
     C_NCTR = 16
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line

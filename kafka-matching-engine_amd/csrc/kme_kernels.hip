@@ -1860,6 +1860,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     if (b >= e || e - b <= (uint32_t)S.light_max) return;   // empty, or a light group (k_match_lanes)
     if (S.ctr[ci(C_FALLBACK)]) return;
     const uint32_t lim = err_limit(S.ctr, iop->n);          // records from a fault on do not take effect
+    if (threadIdx.x == 0) atomicAdd(&S.ctr[ci(C_BUSY)], 1ull);
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
     w.load_group();
@@ -2750,7 +2751,8 @@ __global__ void __launch_bounds__(256) k_otab_refill(DevState S, uint32_t nslots
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x) {
         if (S.pool[s].live) {
             if (otab_insert(S, S.pool[s].oid, (int32_t)s)) ++n_ins;
-            else raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_OIDTAB, -1);
+            else atomicAdd(&S.ctr[ci(C_REBUILD_FAIL)], 1ull);   // (not the per-epoch error word:
+                                                                 // an epoch may be in flight)
         }
     }
     const uint32_t tot = block_sum_256(n_ins, red);
@@ -2810,7 +2812,7 @@ __global__ void k_init_state(DevState S) {
 __global__ void k_epoch_reset(DevState S) {
     const int k = threadIdx.x;
     if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
-    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK) S.ctr[ci(k)] = 0ull;
+    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY) S.ctr[ci(k)] = 0ull;
 }
 
 // ------------------------------------------------------------------ launchers
@@ -2896,6 +2898,7 @@ void launch_resync_funded(const DevState& S, const EpochIO& io, hipStream_t st) 
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
     (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);
     (void)hipMemsetAsync(&S.ctr[ci(C_OTAB_USED)], 0, sizeof(unsigned long long), st);
+    (void)hipMemsetAsync(&S.ctr[ci(C_REBUILD_FAIL)], 0, sizeof(unsigned long long), st);
     const uint32_t n = std::min(used_slots, S.pool_cap);
     hipLaunchKernelGGL(k_otab_refill, dim3(std::min<uint32_t>(cdiv(n > 0 ? n : 1, 256), STREAM_BLOCKS)), dim3(256), 0, st, S, n);
 }

@@ -40,6 +40,7 @@ struct kme_engine {
     hipStream_t own_stream = nullptr;
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    uint64_t last_busy = 1;              // groups k_match took in the last epoch (C_BUSY)
     hipStream_t stream = nullptr;
     DevState S{};
     DevState* d_S = nullptr;
@@ -52,20 +53,26 @@ struct kme_engine {
     uint8_t* d_out_flags = nullptr;
     uint32_t *d_ntrades = nullptr, *d_trade_off = nullptr;
     TradeRec* d_trades = nullptr;
-    unsigned long long* h_ctr = nullptr;  // pinned copy of the counters block
+    unsigned long long* h_ctr = nullptr;  // pinned copies of the counters block: one per epoch slot
+                                          // (two epochs may be in flight), a third for the rebuild
     // device serializer scratch: per-input byte counts, offsets, scan partials, u64 total
     uint32_t *d_ser_len = nullptr, *d_ser_off = nullptr, *d_ser_tmp = nullptr;
     unsigned long long* d_ser_total = nullptr;
     unsigned long long* h_ser_total = nullptr;
     std::vector<void*> allocs;
     int64_t seq_base = 0;
-    uint32_t last_n = 0;
-    bool pending = false;
+    // epochs in flight: submitted to the stream, not yet waited for (at most two; slot = submission
+    // number & 1; kme_wait takes the oldest)
+    int inflight = 0;
+    uint32_t sub_count = 0;
+    uint32_t fl_n[2] = {};
+    int cur_slot = 0;
+    hipEvent_t ev_end[2] = {};
     int failed = 0;
     int fail_status = 0, fail_detail = 0;
     int timing = 0;                      // KME_TIMING_* (kme.h)
-    hipEvent_t ev[PH_N * 2] = {};
-    bool ev_used[PH_N] = {};
+    hipEvent_t ev[2][PH_N * 2] = {};
+    bool ev_used[2][PH_N] = {};
     float phase_ms[KME_MAX_PHASES] = {};
     uint64_t otab_cap = 0;
 };
@@ -102,12 +109,12 @@ static bool timed(const kme_engine* e, int ph) {
 }
 static void phase_begin(kme_engine* e, int ph, hipStream_t s = nullptr) {
     if (!timed(e, ph)) return;
-    (void)hipEventRecord(e->ev[2 * ph], s ? s : e->stream);
-    e->ev_used[ph] = true;
+    (void)hipEventRecord(e->ev[e->cur_slot][2 * ph], s ? s : e->stream);
+    e->ev_used[e->cur_slot][ph] = true;
 }
 static void phase_end(kme_engine* e, int ph, hipStream_t s = nullptr) {
     if (!timed(e, ph)) return;
-    (void)hipEventRecord(e->ev[2 * ph + 1], s ? s : e->stream);
+    (void)hipEventRecord(e->ev[e->cur_slot][2 * ph + 1], s ? s : e->stream);
 }
 
 extern "C" {
@@ -164,7 +171,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
     e->stream = e->own_stream;
-    for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
+    for (auto& evs : e->ev)
+        for (auto& ev : evs) HIP_TRY(hipEventCreate(&ev));
+    for (auto& ev : e->ev_end) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 
     const bool funded = cfg->mode == KME_MODE_FUNDED;
     const uint32_t G = cfg->max_symbols;
@@ -267,7 +276,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(e->d_S, 1);
     ALLOC(e->d_io, 1);
     HIP_TRY(hipHostMalloc((void**)&e->h_ser_total, sizeof(unsigned long long), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&e->h_ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&e->h_ctr, 3 * (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipHostMallocDefault));
 
     // initial store contents: every group absent, empty tables
     hipStream_t st = e->stream;
@@ -301,7 +310,9 @@ kme_status kme_destroy(kme_engine* e) {
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
-    for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    for (auto& evs : e->ev)
+        for (auto& ev : evs) if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : e->ev_end) if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->lane_stream) (void)hipStreamDestroy(e->lane_stream);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -325,6 +336,9 @@ kme_status kme_enable_timing(kme_engine* e, int enable) {
 static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
     if (e->failed) return KME_E_FAILED;
     if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
+    if (e->inflight == 2) return KME_E_INVALID;   // two epochs in flight: kme_wait the older first
+    const int slot = (int)(e->sub_count & 1);
+    e->cur_slot = slot;
     const bool funded = e->cfg.mode == KME_MODE_FUNDED;
     DevState& S = e->S;
     hipStream_t st = e->stream;
@@ -343,7 +357,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     io.n_trades = e->d_ntrades;
     io.n = n;
     io.seq_base = e->seq_base;
-    for (bool& u : e->ev_used) u = false;
+    for (bool& u : e->ev_used[slot]) u = false;
 
     // per-epoch counters: error = none, stats = 0 (pool bump / table usage persist)
     launch_epoch_reset(S, st);
@@ -365,14 +379,20 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         const int buf = launch_partition(S, io, st);
         phase_end(e, PH_PART);
         phase_begin(e, PH_MATCH);
-        if (S.light_max > 0) {   // light groups one lane each, concurrently with k_match's heavy ones
+        // light groups one lane each, concurrently with k_match's busy ones (a second stream).  When
+        // the last epoch had no busy group both go on the engine stream: the fork / join costs
+        // ~30 us per epoch (measured), k_match then only finds empty work (~16 us at C3).
+        const bool fork = S.light_max > 0 && e->last_busy != 0;
+        if (fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, st));
             HIP_TRY(hipStreamWaitEvent(e->lane_stream, e->ev_fork, 0));
             launch_match_lanes(S, e->d_S, e->d_io, buf, e->lane_stream);
             HIP_TRY(hipEventRecord(e->ev_join, e->lane_stream));
+        } else if (S.light_max > 0) {
+            launch_match_lanes(S, e->d_S, e->d_io, buf, st);
         }
         launch_match(S, e->d_S, e->d_io, buf, st);
-        if (S.light_max > 0) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
+        if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);
         launch_compact(S, io, st);
@@ -399,10 +419,12 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     launch_table(S, io, st);
     phase_end(e, PH_TABLE);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->h_ctr, S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(e->h_ctr + slot * (size_t)C_NCTR * CTR_STRIDE, S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(e->ev_end[slot], st));
     e->seq_base += n;
-    e->last_n = n;
-    e->pending = true;
+    e->fl_n[slot] = n;
+    ++e->sub_count;
+    ++e->inflight;
     return KME_OK;
 }
 
@@ -416,34 +438,39 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     if (!e) return KME_E_INVALID;
     kme_epoch_status s{};
     s.error_index = -1;
-    if (!e->pending) {
+    if (e->inflight == 0) {
         s.status = e->failed ? e->fail_status : KME_OK;
         if (st) *st = s;
         return (kme_status)s.status;
     }
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    e->pending = false;
-    const unsigned long long* c = e->h_ctr;
-    s.n_inputs = e->last_n;
+    const int slot = (int)((e->sub_count - (uint32_t)e->inflight) & 1);   // the older epoch in flight
+    HIP_TRY(hipEventSynchronize(e->ev_end[slot]));
+    --e->inflight;
+    const uint32_t last_n = e->fl_n[slot];
+    const unsigned long long* c = e->h_ctr + slot * (size_t)C_NCTR * CTR_STRIDE;
+    s.n_inputs = last_n;
     s.n_trades = (uint32_t)c[ci(C_TRADES)];
     s.n_orders = c[ci(C_ORDERS)];
     s.n_rests = c[ci(C_RESTS)];
     s.n_maker_visits = c[ci(C_TRADES)];               // every maker visit is one trade (KP:238-242)
     s.n_cancel_ok = c[ci(C_CANCEL_OK)];
     s.serial_fallback = c[ci(C_FALLBACK)] ? 1u : 0u;
-    s.n_effective = e->last_n;
+    s.n_effective = last_n;
+    e->last_busy = c[ci(C_BUSY)];
     if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
         const uint64_t ix = c[ci(C_ERR)] >> 16;
         s.error_index = ix == 0xFFFFFFFFFFFFull ? -1 : (int64_t)ix;
         // the records before the fault took effect (their results are valid), none after it
-        s.n_effective = s.error_index < 0 ? 0u : (uint32_t)std::min<int64_t>(s.error_index, e->last_n);
-        if (s.status == KME_E_UNFUNDED) {
+        s.n_effective = s.error_index < 0 ? 0u : (uint32_t)std::min<int64_t>(s.error_index, last_n);
+        if (s.status == KME_E_UNFUNDED && e->inflight == 0) {
             // not fatal: the refused records changed nothing, so their sequence numbers are
             // handed out again when they are resubmitted
-            e->seq_base -= (int64_t)(e->last_n - s.n_effective);
+            e->seq_base -= (int64_t)(last_n - s.n_effective);
         } else {
+            // (an UNFUNDED epoch with a later one already in flight: that one ran without the refused
+            // records, out of the caller's order -- the engine fails)
             e->failed = 1;
             e->fail_status = s.status;
             e->fail_detail = s.detail;
@@ -452,16 +479,23 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     if (e->timing) {
         for (int p = 0; p < PH_N; ++p) {
             e->phase_ms[p] = 0.f;
-            if (e->ev_used[p]) (void)hipEventElapsedTime(&e->phase_ms[p], e->ev[2 * p], e->ev[2 * p + 1]);
+            if (e->ev_used[slot][p]) (void)hipEventElapsedTime(&e->phase_ms[p], e->ev[slot][2 * p], e->ev[slot][2 * p + 1]);
         }
     }
-    // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild
-    if (!e->failed && (c[ci(C_OTAB_USED)] + e->cfg.max_epoch) * 2 > e->otab_cap) {
-        launch_otab_rebuild(e->S, (uint32_t)std::min<uint64_t>(c[ci(C_POOL_BUMP)], e->S.pool_cap), e->stream);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(e->h_ctr, e->S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+    // oid table maintenance: stale (lazily deleted) entries are dropped by a rebuild, early enough
+    // that the epoch still in flight and the next one fit (each adds at most max_epoch entries).
+    // The rebuild drains the stream first (the in-flight epoch finishes; its counters are already
+    // copied) and reports through its own counter, not the per-epoch error word.
+    if (!e->failed && (c[ci(C_OTAB_USED)] + (uint64_t)(1 + e->inflight) * e->cfg.max_epoch) * 2 > e->otab_cap) {
         HIP_TRY(hipStreamSynchronize(e->stream));
-        if (e->h_ctr[ci(C_ERR)] != ~0ull || e->h_ctr[ci(C_OTAB_USED)] * 4 > e->otab_cap * 3) {
+        // the pool slots to scan: the newest bump (the in-flight epoch's copy, complete after the drain)
+        const unsigned long long* latest = e->inflight ? e->h_ctr + (slot ^ 1) * (size_t)C_NCTR * CTR_STRIDE : c;
+        launch_otab_rebuild(e->S, (uint32_t)std::min<uint64_t>(latest[ci(C_POOL_BUMP)], e->S.pool_cap), e->stream);
+        HIP_TRY(hipGetLastError());
+        unsigned long long* rc = e->h_ctr + 2 * (size_t)C_NCTR * CTR_STRIDE;
+        HIP_TRY(hipMemcpyAsync(rc, e->S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (rc[ci(C_REBUILD_FAIL)] != 0 || rc[ci(C_OTAB_USED)] * 4 > e->otab_cap * 3) {
             e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_OIDTAB;
         }
     }
@@ -508,7 +542,7 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
 kme_status kme_checkpoint(kme_engine* e, const char* path) {
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
-    if (e->pending) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
+    if (e->inflight) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
@@ -540,7 +574,7 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
 kme_status kme_restore(kme_engine* e, const char* path) {
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
-    if (e->pending) return KME_E_INVALID;
+    if (e->inflight) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
     FILE* f = std::fopen(path, "rb");
     if (!f) return KME_E_INVALID;
@@ -637,6 +671,7 @@ const char* kme_phase_name(int i) { return (i >= 0 && i < PH_N) ? kPhaseNames[i]
 // records so that the reservation proof never has to reason across a CREATE/TRANSFER boundary.
 kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme_epoch_result* out,
                             kme_epoch_status* st) {
+    if (e && e->inflight) return KME_E_INVALID;   // device epochs still in flight: kme_wait them first
     if (!e || !in || !out) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
     kme_epoch_status total{};
