@@ -51,3 +51,24 @@ def test_bench_byte_model():
     exec(src[start:end], ns)
     st = types.SimpleNamespace(n_inputs=10, n_trades=3, n_rests=4, n_maker_visits=3, n_cancel_ok=2)
     assert ns["algorithmic_bytes"](st) == 52 * 10 + 36 * 3 + 32 * 4 + 32 * 3 + 48 * 2
+
+
+def test_credit_split_probe_counts_the_first_failing_epoch():
+    import numpy as np
+    import credit_split_probe as probe
+
+    # one account, two shards, four BUY/SELL of risk 10 at records 0, 1, 5, 6 (epochs of 4 records):
+    # shard 0 gets three of them (30 > 40 // 2 = 20 from the third on, record 6 -> epoch 1)
+    aid = np.zeros(4, np.int64)
+    shard = np.array([0, 0, 1, 0], np.int64)
+    risk = np.full(4, 10, np.int64)
+    pos = np.array([0, 1, 5, 6], np.int64)
+    st = probe.fallback_stats(aid, shard, risk, pos, 8, 1, 2, 1.0, 4)
+    assert st["epochs"] == 2 and st["fallback_epochs"] == 1 and st["first_fallback_epoch"] == 1
+    assert st["failing_pairs"] == 1 and st["failing_accounts"] == 1
+    # one shard: the whole credit, nothing fails; twice the credit on two shards: nothing fails
+    assert probe.fallback_stats(aid, np.zeros(4, np.int64), risk, pos, 8, 1, 1, 1.0, 4)["fallback_epochs"] == 0
+    assert probe.fallback_stats(aid, shard, risk, pos, 8, 1, 2, 2.0, 4)["fallback_epochs"] == 0
+    # the max risk of checkBalance (KP:172-176): BUY size * price, SELL size * (100 - price)
+    r = probe.max_risk(np.array([2, 3, 4]), np.array([30, 30, 0]), np.array([10, 10, 0]))
+    assert r.tolist() == [300, 700, 0]
