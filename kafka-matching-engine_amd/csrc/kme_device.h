@@ -117,11 +117,10 @@ struct DevState {
     int32_t light_max;                // FUNDED: groups with at most this many records in the epoch
                                       // run in k_match_lanes (one lane each); 0 = none
     int32_t fallback;                 // KME_FLAG_SERIAL_FALLBACK
-    int32_t os_lanes;                 // FUNDED: light groups leave their OUT echo step-major (kme_kernels.hip
-                                      // "OUT echo layout"); 0 = every record at its sorted position
+    int32_t os_lanes;                 // reserved (0): the OUT echo is stored at the input index
     uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
     uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
-    uint32_t os_base, _pad1;          // start of the light groups' OUT echo region (= max_epoch)
+    uint32_t os_base, _pad1;          // osort records (= max_epoch)
     KG GroupState* grp;
     KG Level* lev;
     KG Node* pool;
@@ -150,10 +149,10 @@ struct DevState {
                                       // size, oid, aid, cancel target (slot | -(j + 2) | -1), the
                                       // target's level (price | side << 8 | 1 << 9; 0 = unknown)
     KG int4* osort;                   // FUNDED: the OUT echo of the matched records, 16 B each
-                                      // (action | has_prev << 8 | n_trades << 9, size, prev); k_unsort
-                                      // puts it in input order.  [0, os_base): busy groups' records at
-                                      // their sorted position; from os_base: light groups' step-major
-    KG int32_t* rank;                 // FUNDED: sorted position of input i (last partition pass)
+                                      // (action | has_prev << 8 | n_trades << 9, size, prev) at the
+                                      // record's input index; k_unsort spreads it over the SoA results
+    KG int32_t* rank;                 // sorted position of input i (last partition pass), when allocated
+                                      // (nullptr: nothing reads it)
     KG uint32_t* rkeys[2];
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;

@@ -556,15 +556,18 @@ __global__ void __launch_bounds__(256) k_radix_hist(DevState S, EpochIO io, int 
 
 KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
 
-// One tile's scatter, staged in LDS: the tile is first ordered by digit in LDS (stable: the
-// wavefront match-any ranks of the chunk loop), then written out in that order, so that each
-// digit's run of the tile leaves in consecutive lanes (coalesced stores) instead of one scattered
-// 4-B store per element and array.
+// One tile's scatter, staged in LDS: the tile is first ordered by digit in LDS (stable), then
+// written out in that order, so that each digit's run of the tile leaves in consecutive lanes
+// (coalesced stores) instead of one scattered 4-B store per element and array.  Ranking is per
+// wavefront: wavefront w owns the tile's w-th quarter (contiguous, so index order = wavefront,
+// round, lane) and counts its digits in its own LDS row round by round (match-any over the digit
+// bits; the first lane of each digit adds the run), so the only block barriers are the few
+// between the counting, the per-digit offsets and the placement.
 __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, int pass, int src) {
     static_assert(RADIX_DIGITS == 512, "two digits per thread");
-    __shared__ uint32_t running[RADIX_DIGITS];   // the tile histogram, then the next free local slot
+    static_assert(RADIX_TILE % 256 == 0, "whole rounds");
+    __shared__ uint32_t wh[4][RADIX_DIGITS];     // wavefront w's count of digit d, then its first local slot
     __shared__ uint32_t gdelta[RADIX_DIGITS];    // digit d's global offset minus its local start
-    __shared__ uint32_t wcnt[4][RADIX_DIGITS];
     __shared__ uint32_t lkey[RADIX_TILE], lval[RADIX_TILE];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -573,62 +576,66 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
     const int shift = RADIX_BITS * pass;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     constexpr int RJ = RADIX_TILE / 256;
-    uint32_t keys[RJ], vals[RJ];
+    constexpr int WCH = RADIX_TILE / 4;          // elements per wavefront
+    uint32_t keys[RJ], vals[RJ], wr[RJ];
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-        const uint32_t k = base + j * 256 + t;
+        const uint32_t k = base + w * WCH + j * 64 + lane;
         keys[j] = 0; vals[j] = 0;
         if (k < io.n) {
             keys[j] = radix_key(S, pass, src, k);
             vals[j] = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
         }
     }
-    for (int q = 0; q < RADIX_PER_T; ++q) running[t + 256 * q] = 0;
-    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < RJ; ++j)
-        if (base + j * 256 + t < io.n) atomicAdd(&running[(keys[j] >> shift) & (RADIX_DIGITS - 1)], 1u);
-    __syncthreads();
-    {   // local starts (exclusive scan of the tile histogram) and the global offsets (k_radix_hist + scan)
-        const uint32_t h0 = running[2 * t], h1 = running[2 * t + 1];
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan_256(h0 + h1, wsum, tot);
-        running[2 * t] = ex;
-        running[2 * t + 1] = ex + h0;
-        gdelta[2 * t] = S.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - ex;
-        gdelta[2 * t + 1] = S.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - (ex + h0);
-    }
-    __syncthreads();
+    for (int q = 0; q < RADIX_DIGITS / 64; ++q) wh[w][lane + 64 * q] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-        for (int q = 0; q < RADIX_PER_T; ++q) {
-            wcnt[0][t + 256 * q] = 0; wcnt[1][t + 256 * q] = 0; wcnt[2][t + 256 * q] = 0; wcnt[3][t + 256 * q] = 0;
-        }
-        __syncthreads();
-        const bool valid = base + j * 256 + t < io.n;
+        const bool valid = base + w * WCH + j * 64 + lane < io.n;
         const uint32_t d = (keys[j] >> shift) & (RADIX_DIGITS - 1);
-        // lanes of this wavefront with the same digit (match-any over the digit bits)
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < RADIX_BITS; ++b) {
             const unsigned long long bb = __ballot(valid && ((d >> b) & 1));
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
         const uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
-        if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = running[d] + rank;
-            for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][d];
+        const uint32_t old = valid ? wh[w][d] : 0u;
+        wr[j] = old + rank;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && rank == 0) wh[w][d] = old + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    {   // digits 2t and 2t + 1: local start (block scan of the tile histogram), each wavefront's first
+        // slot, and the global offset (k_radix_hist + scan)
+        uint32_t c0[4], c1[4], t0 = 0, t1 = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) { c0[ww] = wh[ww][2 * t]; c1[ww] = wh[ww][2 * t + 1]; t0 += c0[ww]; t1 += c1[ww]; }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_256(t0 + t1, wsum, tot);
+        uint32_t r0 = ex, r1 = ex + t0;
+        gdelta[2 * t] = S.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - r0;
+        gdelta[2 * t + 1] = S.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - r1;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) { wh[ww][2 * t] = r0; wh[ww][2 * t + 1] = r1; r0 += c0[ww]; r1 += c1[ww]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        if (base + w * WCH + j * 64 + lane < io.n) {
+            const uint32_t pos = wh[w][(keys[j] >> shift) & (RADIX_DIGITS - 1)] + wr[j];
             lkey[pos] = keys[j];
             lval[pos] = vals[j];
         }
-        __syncthreads();
-        for (int q = 0; q < RADIX_PER_T; ++q) {
-            const int dd = t + 256 * q;
-            running[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
-        }
-        __syncthreads();
     }
+    __syncthreads();
     const uint32_t cnt = io.n - base < (uint32_t)RADIX_TILE ? io.n - base : (uint32_t)RADIX_TILE;
     KG uint32_t* okeys = dst ? S.rkeys[1] : S.rkeys[0];
     KG uint32_t* ovals = dst ? S.rvals[1] : S.rvals[0];
@@ -676,6 +683,63 @@ KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total) {
     total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
     return off + inc - v;
+}
+
+// Exclusive scan in two launches (reduce, then scan): k_tile_sums writes each 4,096-item tile's
+// sum; k_scan_tiles gives every tile its prefix from those sums (at most a few thousand, read by
+// every block from L2) and scans the tile in LDS.  Replaces the three-kernel scan (blocks, sums,
+// add) and the copy of the total on the epoch path.  (A single-pass decoupled look-back was
+// measured slower: with every tile resident at once the inclusive prefixes resolve 64 tiles per
+// L2 round trip, ~16 round trips for the 1,024 tiles of a 4M-record epoch.)
+constexpr int LB_ITEMS = 16;
+constexpr int LB_TILE = 256 * LB_ITEMS;
+KDEV uint32_t lb_pad(uint32_t k) { return k + (k >> 5); }
+__global__ void __launch_bounds__(256) k_tile_sums(const uint32_t* in, uint32_t L, uint32_t* sums) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t base = blockIdx.x * LB_TILE;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) {
+        const uint32_t k = base + j * 256 + threadIdx.x;
+        sum += k < L ? in[k] : 0u;
+    }
+    uint32_t tot;
+    (void)block_excl_scan_256(sum, wsum, tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t* out, uint32_t L, const uint32_t* sums,
+                                                    uint32_t* total_out, int write_end) {
+    __shared__ uint32_t buf[LB_TILE + LB_TILE / 32];
+    __shared__ uint32_t wsum[4];
+    const int t = threadIdx.x;
+    const uint32_t tile = blockIdx.x, base = tile * LB_TILE;
+    uint32_t pre = 0;                                  // this thread's share of the tiles before this one
+    for (uint32_t q = t; q < tile; q += 256) pre += sums[q];
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) {
+        const uint32_t k = j * 256 + t;
+        buf[lb_pad(k)] = base + k < L ? in[base + k] : 0u;
+    }
+    uint32_t excl;
+    (void)block_excl_scan_256(pre, wsum, excl);        // (its barriers also order the LDS stores above)
+    uint32_t v[LB_ITEMS], sum = 0;
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) { v[j] = buf[lb_pad(LB_ITEMS * t + j)]; sum += v[j]; }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_256(sum, wsum, tot);
+    if (t == 0 && tile == gridDim.x - 1) {
+        if (total_out) *total_out = excl + tot;
+        if (write_end) out[L] = excl + tot;
+    }
+    uint32_t run = excl + ex;
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) { buf[lb_pad(LB_ITEMS * t + j)] = run; run += v[j]; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) {
+        const uint32_t k = j * 256 + t;
+        if (base + k < L) out[base + k] = buf[lb_pad(k)];
+    }
 }
 
 __global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum) {
@@ -1960,8 +2024,8 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         n_rest += (uint32_t)__popcll(__ballot(lane < done && ((o_act >> 16) & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < done && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
         if (__ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR)) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
-        if (lane < done)   // one coalesced 16-B record per lane (k_unsort scatters them)
-            opaque_const(Sp).osort[k] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
+        if (lane < done)   // one 16-B record per lane, at the record's input index (k_unsort reads them in order)
+            opaque_const(Sp).osort[B.i] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
                                                   o_size, o_plo, o_phi);
     }
     KST(const unsigned long long to0 = stamp();)
@@ -2008,15 +2072,8 @@ constexpr int LANE_GROUPS = KME_LANE_GROUPS;   // groups per wavefront (the othe
                                   // wavefronts per SIMD at 65,536 groups, so one issues while the other waits
 static_assert(LANE_GROUPS >= 1 && LANE_GROUPS <= 64, "k_match_lanes: one group per lane");
 
-// OUT echo layout (DevState::osort, 16 B per record: action | has_prev << 8 | n_trades << 9, size,
-// prev).  A busy group's records sit at their sorted position k; a light group's (when os_lanes)
-// step-major behind os_base: the record a k_match_lanes wavefront handles in step s of lane l goes
-// to wave * (LANE_GROUPS * light_max) + s * LANE_GROUPS + l, so every step's stores of a wavefront
-// form one contiguous run instead of 32 scattered half lines.
-KDEV size_t os_pos_light(const DevState& S, int32_t g, uint32_t step) {
-    return (size_t)S.os_base + (size_t)(g / LANE_GROUPS) * (LANE_GROUPS * (uint32_t)S.light_max) +
-           (size_t)step * LANE_GROUPS + (uint32_t)(g % LANE_GROUPS);
-}
+// OUT echo (DevState::osort, 16 B per record at its input index): action | has_prev << 8 |
+// n_trades << 9, size, prev.
 KDEV int4 os_pack(int32_t action, bool has_prev, uint32_t ntr, int32_t size, int64_t prev) {
     return make_int4((action & 0xFF) | (has_prev ? 1 << 8 : 0) | (int32_t)(ntr << 9), size, lo32(prev), hi32(prev));
 }
@@ -2453,7 +2510,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
             {   // the OUT echo (step-major: the wavefront's stores of a step are one run), stored
                 // next step
                 if (o.ntr >= OS_MAX_NTR) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
-                pend_pos = S.os_lanes ? os_pos_light(S, g, k - b) : (size_t)k;
+                pend_pos = (size_t)r.i;
                 pend_a = os_pack(o.action, o.has_prev, o.ntr, o.size, o.has_prev ? o.prev : 0);
                 pend = true;
             }
@@ -2629,9 +2686,9 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
 }
 
 // ------------------------------------------------------------------ (3') OUT echo to input order
-// The matching kernels leave each record's OUT echo in group-sorted order (coalesced / sequential
-// lines); here every input takes its own from position rank[i]: one random 32-B read per matched
-// record instead of five random partial-line writes (the C ABI's SoA arrays) in the matching loop.
+// The matching kernels leave each record's OUT echo as one packed 16-B record at its input index
+// (one random 16-B store in the matching loop instead of five partial-line stores to the C ABI's SoA
+// arrays); here it is read in order and spread over those arrays (sequential lines both ways).
 // Records without a symbol group were answered by k_route / k_ledger_funded already.
 __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     if (S.ctr[ci(C_FALLBACK)]) return;                   // k_serial answers the epoch
@@ -2648,13 +2705,7 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
         const int32_t g = S.route_grp[i];
         if (g < 0) continue;
         if (i >= lim) { io.n_trades[i] = 0; continue; }
-        const uint32_t k = (uint32_t)S.rank[i];
-        size_t pos = k;
-        if (S.os_lanes) {   // a light group's record: step-major (os_pos_light)
-            const uint32_t b = S.seg[g], e = S.seg[g + 1];
-            if (e - b <= (uint32_t)S.light_max) pos = os_pos_light(S, g, k - b);
-        }
-        const int4 a = S.osort[pos];
+        const int4 a = S.osort[i];
         io.out_action[i] = a.x & 0xFF;
         io.out_flags[i] = (uint8_t)((a.x >> 8) & KME_OUT_HAS_PREV);
         io.out_size[i] = a.y;
@@ -2843,6 +2894,14 @@ void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, 
     hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, bsum, nb, total);
     hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(256), 0, st, out, L, bsum);
 }
+// Exclusive scan of in[0, L) into out (in place allowed): tile sums, then the tiles (sums scratch:
+// cdiv(L, LB_TILE) words).
+static void launch_scan2(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, int write_end,
+                         hipStream_t st) {
+    const uint32_t nb = cdiv(L > 0 ? L : 1, LB_TILE);
+    hipLaunchKernelGGL(k_tile_sums, dim3(nb), dim3(256), 0, st, in, L, sums);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end);
+}
 int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     const uint32_t ntiles = cdiv(io.n > 0 ? io.n : 1, RADIX_TILE);
     int src = 0;
@@ -2850,9 +2909,7 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(256), 0, st, S, io, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
         const uint32_t L = RADIX_DIGITS * ntiles;
-        uint32_t* bsum = S.ghist + L;
-        uint32_t* total = bsum + cdiv(L, SCAN_BLOCK) + 1;
-        launch_scan(S.ghist, S.ghist, L, bsum, total, st);
+        launch_scan2(S.ghist, S.ghist, L, S.ghist + L, nullptr, 0, st);
         hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(256), 0, st, S, io, pass, src);
         src ^= 1;
     }
@@ -2871,11 +2928,8 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     // wait for its previous record's stores before its next loads (vmcnt counts both, in order)
     if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);
     // trade_off[0..n] = exclusive scan of n_trades; bsum/total scratch in ghist
-    uint32_t* bsum = S.ghist;
-    const uint32_t nb = cdiv(io.n > 0 ? io.n : 1, SCAN_BLOCK);
-    uint32_t* total = bsum + nb + 1;
-    launch_scan(io.n_trades, io.trade_off, io.n, bsum, total, st);
-    (void)hipMemcpyAsync(io.trade_off + io.n, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    uint32_t* total = S.ghist;   // (the partition's histograms are dead by now)
+    launch_scan2(io.n_trades, io.trade_off, io.n, S.ghist + 64, total, 1, st);
     hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1, SCATTER_SUB), dim3(256), 0, st, S, io, (const uint32_t*)total);
     static_assert(TSHARDS == 256, "k_tsh_fold: one thread per shard line");
     hipLaunchKernelGGL(k_tsh_fold, dim3(1), dim3(256), 0, st, S);

@@ -247,12 +247,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
     if (funded) ALLOC(S.prec, 2 * (size_t)E);
-    // OUT echo: E sorted positions, then (light groups, step-major) one 16-B slot per lane and step
-    // of every k_match_lanes wavefront: at most (G + 64) * light_max
+    // OUT echo: one 16-B record per input index, stored by the matching kernels where the record
+    // arrived (k_unsort then reads it sequentially; no sorted-position map)
     S.os_base = E;
-    S.os_lanes = funded && S.light_max > 0 && S.light_max <= kOsLanesMaxLight ? 1 : 0;
-    if (funded) ALLOC(S.osort, (size_t)E + (S.os_lanes ? ((size_t)G + 64) * (size_t)S.light_max : 0));
-    if (funded) ALLOC(S.rank, E);
+    S.os_lanes = 0;
+    if (funded) ALLOC(S.osort, (size_t)E);
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
         ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);
