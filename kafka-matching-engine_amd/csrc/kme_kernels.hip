@@ -274,6 +274,12 @@ KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
     return false;
 }
 
+// A BUY/SELL's pending entry (k_emap) becomes its rest slot, or OT_DEAD when it did not rest: the
+// entry's low word only (the fingerprint stays), stored by the matching kernel that decided it.
+KDEV void otab_final(decltype(DevState::otab) otab, int32_t h, int32_t slot) {
+    if (h >= 0) reinterpret_cast<KG uint32_t*>(otab)[2 * (size_t)h] = slot >= 0 ? (uint32_t)slot : OT_DEAD;
+}
+
 // ------------------------------------------------------------------ epoch kernels: emap / ledger / route
 // Sum of a per-thread count over a 256-thread block (DPP wave scans, then LDS); valid in thread 0.
 KDEV uint32_t block_sum_256(uint32_t v, uint32_t* red) {
@@ -521,6 +527,9 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
     if (grp >= 0) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
+        // a BUY/SELL's word 6 is its oid-table entry's position (k_emap), which the matching kernel
+        // finalises (otab_final); a cancel's is its target
+        if (a == BUY || a == SELL) { const uint32_t h = S.epos[i]; tgt = h == OT_DEAD ? -1 : (int64_t)h; }
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
@@ -1787,6 +1796,7 @@ struct GroupWave {
         if (lane < 4) reinterpret_cast<KG int4*>(&pool[slot])[lane] = make_int4(x, y, z, w);
         mark_dirty(slot);
         rest_slot[r.i] = slot;
+        otab_final(cold().otab, (int32_t)r.tgt, slot);
         o.rested = true;
         KST(acc[ST_REST_NODE] += stamp() - ts2;)
     }
@@ -1887,7 +1897,7 @@ struct GroupWave {
             break;
         case BUY:
         case SELL: {
-            if (!gsv(GS_EXISTS) || !r.acct_ok) break;               // books.get(sid) == null / balances.get == null
+            if (!gsv(GS_EXISTS) || !r.acct_ok) { otab_final(cold().otab, (int32_t)r.tgt, -1); break; }   // books.get(sid) == null / balances.get == null
             const bool is_buy = r.action == BUY;
             const int os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
             int32_t tsize = r.size;
@@ -1898,6 +1908,7 @@ struct GroupWave {
             o.ntr = ntr;
             if (dead) return o;
             if (!filled) { rest(r, tsize, o); if (dead) return o; }
+            else otab_final(cold().otab, (int32_t)r.tgt, -1);
             ok = true;
             o.size = tsize;
             break;
@@ -2322,6 +2333,7 @@ struct GroupLane {
         nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
         nd[3] = make_int4(p, r.action, 1, 0);
         S.rest_slot[r.i] = slot;
+        otab_final(S.otab, (int32_t)r.tgt, slot);
         o.rested = true;
     }
 
@@ -2514,6 +2526,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 pend_a = os_pack(o.action, o.has_prev, o.ntr, o.size, o.has_prev ? o.prev : 0);
                 pend = true;
             }
+            if ((r.action == BUY || r.action == SELL) && !o.rested) otab_final(S.otab, (int32_t)r.tgt, -1);
             n_rest += o.rested ? 1u : 0u;
             n_cancel += (cxl && ok) ? 1u : 0u;
             LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
@@ -2694,15 +2707,17 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     if (S.ctr[ci(C_FALLBACK)]) return;                   // k_serial answers the epoch
     const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
-        const int32_t act = io.action[i];
-        if (act == BUY || act == SELL) {   // k_table's work, fused (the oid-table entry of the order)
-            const uint32_t h = S.epos[i];
-            if (h != OT_DEAD) {
-                const int32_t rs = S.rest_slot[i];
-                S.otab[h] = hentry(oid_fp(io.oid[i]), rs >= 0 ? (uint32_t)rs : OT_DEAD);
+        const int32_t g = S.route_grp[i];
+        if (g < 0 || i >= lim) {   // k_table's work for the BUY/SELL no matching kernel finalised (otab_final)
+            const int32_t act = io.action[i];
+            if (act == BUY || act == SELL) {
+                const uint32_t h = S.epos[i];
+                if (h != OT_DEAD) {
+                    const int32_t rs = S.rest_slot[i];
+                    S.otab[h] = hentry(oid_fp(io.oid[i]), rs >= 0 ? (uint32_t)rs : OT_DEAD);
+                }
             }
         }
-        const int32_t g = S.route_grp[i];
         if (g < 0) continue;
         if (i >= lim) { io.n_trades[i] = 0; continue; }
         const int4 a = S.osort[i];
