@@ -245,7 +245,7 @@ KDEV int32_t otab_lookup(const DevState& S, int64_t oid) {
 }
 // removeOrder's orders.get(oid) at input i (KP:290): an order of this epoch submitted before i
 // (returns -(j + 2)), else a resting order's slot, else -1.
-KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oid, uint32_t i) {
+KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oid, uint32_t i, uint32_t& pos) {
     const uint32_t fp = oid_fp(oid);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
     for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
@@ -255,7 +255,7 @@ KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oi
         if ((uint32_t)(e >> 32) == fp && v != OT_DEAD) {
             if (v & OT_PENDING) {
                 const uint32_t j = v & ~OT_PENDING;
-                if (j < i && io.oid[j] == oid) return -((int64_t)j + 2);
+                if (j < i && io.oid[j] == oid) { pos = h; return -((int64_t)j + 2); }
             } else if (S.pool[v].live && S.pool[v].oid == oid) {
                 return (int64_t)v;
             }
@@ -278,6 +278,13 @@ KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
 // entry's low word only (the fingerprint stays), stored by the matching kernel that decided it.
 KDEV void otab_final(decltype(DevState::otab) otab, int32_t h, int32_t slot) {
     if (h >= 0) reinterpret_cast<KG uint32_t*>(otab)[2 * (size_t)h] = slot >= 0 ? (uint32_t)slot : OT_DEAD;
+}
+
+// The rest slot of a BUY/SELL of this epoch from its entry at position h (otab_final has run for it:
+// the matchers take a group's records in arrival order), or -1 when it did not rest.
+KDEV int32_t otab_epoch_slot(decltype(DevState::otab) otab, int32_t h) {
+    const uint32_t v = reinterpret_cast<const KG uint32_t*>(otab)[2 * (size_t)h];
+    return (v & OT_PENDING) ? -1 : (int32_t)v;
 }
 
 // ------------------------------------------------------------------ epoch kernels: emap / ledger / route
@@ -466,6 +473,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     const int32_t a = io.action[i];
     int32_t grp = -1, vlev = 0;
     int64_t tgt = -1;
+    int64_t ptgt = 0;             // PRec word 6 when it differs from tgt (a same-epoch cancel target)
     S.rest_slot[i] = -1;
     io.n_trades[i] = 0;
     bool direct = false, ok = false, acct_ok = false;
@@ -495,13 +503,14 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         // the target's level (price | side << 8 | 1 << 9) rides along for k_match_lanes, which then
         // fetches the node and its level in one step (checked against the node there)
         const int64_t oid = io.oid[i];
-        const int64_t t = otab_cancel_target(S, io, oid, i);
+        uint32_t hpos = 0;
+        const int64_t t = otab_cancel_target(S, io, oid, i, hpos);
         if (t <= -2) {
             const uint32_t j = (uint32_t)(-(t + 2));
             const int64_t sj = io.sid[j];
             const int32_t gj = group_of(sj, S.G);
             if (gj >= 0) {
-                grp = gj; tgt = t;
+                grp = gj; tgt = t; ptgt = -((int64_t)hpos + 2);
                 const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
                 vlev = (io.price[j] & 0xFF) | (side << 8) | (1 << 9);
             }
@@ -529,7 +538,9 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         const int64_t oid = io.oid[i], aid = io.aid[i];
         // a BUY/SELL's word 6 is its oid-table entry's position (k_emap), which the matching kernel
         // finalises (otab_final); a cancel's is its target
+        // (a same-epoch cancel target: -(its entry's position + 2), the slot read from the entry)
         if (a == BUY || a == SELL) { const uint32_t h = S.epos[i]; tgt = h == OT_DEAD ? -1 : (int64_t)h; }
+        else if (ptgt <= -2) tgt = ptgt;
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
@@ -1795,7 +1806,6 @@ struct GroupWave {
         const int32_t w = q1 ? (q0 ? 0 : g) : (q0 ? -1 : hi32(r.aid));
         if (lane < 4) reinterpret_cast<KG int4*>(&pool[slot])[lane] = make_int4(x, y, z, w);
         mark_dirty(slot);
-        rest_slot[r.i] = slot;
         otab_final(cold().otab, (int32_t)r.tgt, slot);
         o.rested = true;
         KST(acc[ST_REST_NODE] += stamp() - ts2;)
@@ -1830,7 +1840,7 @@ struct GroupWave {
     KDEV bool cancel(const Rec& r, const Lanes& B) {
         int32_t slot = -1;
         if (r.tgt >= 0) slot = (int32_t)r.tgt;
-        else if (r.tgt <= -2) slot = U32(rest_slot[-(r.tgt + 2)]);
+        else if (r.tgt <= -2) slot = U32(otab_epoch_slot(cold().otab, (int32_t)(-(r.tgt + 2))));
         if (slot < 0) return false;                          // orders.get(oid) == null
         Victim o;
         if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
@@ -1950,7 +1960,6 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         const KC DevState& C = opaque_const(Sp);
         const KG uint32_t* perm = buf ? C.rvals[1] : C.rvals[0];
         const KG int4* prec = C.prec;
-        const KG int32_t* rest_slot = C.rest_slot;
         const KG Node* pool = C.pool;
         Lanes B;
         B.i = valid ? perm[k] : 0;
@@ -1964,11 +1973,11 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         const int32_t b_action = B.w0 & 0xFF;
         // cancels: the target node, if it came to rest before this batch (an earlier epoch, or an
         // earlier batch of this group), is fetched now; valid unless written since (dirty filter)
-        const uint32_t i_first = (uint32_t)rl32((int32_t)B.i, 0);
         B.pf_slot = -1;
         if (valid && b_action == CANCEL) {
             if (B.tgt >= 0) B.pf_slot = B.tgt;
-            else if (B.tgt <= -2 && (uint32_t)(-(B.tgt + 2)) < i_first) B.pf_slot = rest_slot[-(B.tgt + 2)];
+            else if (B.tgt <= -2) B.pf_slot = otab_epoch_slot(C.otab, -(B.tgt + 2));   // final unless the
+                                                      // order is in this batch (then still pending: -1)
         }
         B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
         if (B.pf_slot >= 0) {
@@ -2332,7 +2341,6 @@ struct GroupLane {
         nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
         nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
         nd[3] = make_int4(p, r.action, 1, 0);
-        S.rest_slot[r.i] = slot;
         otab_final(S.otab, (int32_t)r.tgt, slot);
         o.rested = true;
     }
@@ -2464,7 +2472,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                     c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
                 } else if (r.tgt <= -2) {
-                    vslot = S.rest_slot[-(r.tgt + 2)];
+                    vslot = otab_epoch_slot(S.otab, (int32_t)(-(r.tgt + 2)));
                 }
             }
             if (order) w.request_spare();
@@ -2711,11 +2719,9 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
         if (g < 0 || i >= lim) {   // k_table's work for the BUY/SELL no matching kernel finalised (otab_final)
             const int32_t act = io.action[i];
             if (act == BUY || act == SELL) {
-                const uint32_t h = S.epos[i];
-                if (h != OT_DEAD) {
-                    const int32_t rs = S.rest_slot[i];
-                    S.otab[h] = hentry(oid_fp(io.oid[i]), rs >= 0 ? (uint32_t)rs : OT_DEAD);
-                }
+                const uint32_t h = S.epos[i];   // still pending: the order did not rest
+                if (h != OT_DEAD && (reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)h] & OT_PENDING))
+                    otab_final(S.otab, (int32_t)h, -1);
             }
         }
         if (g < 0) continue;
