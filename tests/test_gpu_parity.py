@@ -390,3 +390,36 @@ def test_serial_fallback_needs_exact_ledger(kme_mod):
                                  flags=kme_mod.FLAG_SERIAL_FALLBACK)
     with pytest.raises(kme_mod.KmeError):
         kme_mod.Engine(cfg)
+
+
+@pytest.mark.parametrize("light_max", LIGHT)
+def test_funded_cancels_of_orders_of_the_same_epoch(kme_mod, oracle_mod, light_max):
+    """Cancels of orders submitted earlier in the same epoch, whose oid-table entry the matching
+    kernel finalises (rest slot or DEAD) before the cancel reads it: an order that rested, one
+    cancelled twice, one filled at once, one rejected for its book, one rejected for its account,
+    one filled later in the epoch, next to cancels of orders of earlier epochs (KP:289-323)."""
+    B, S, C = W.BUY, W.SELL, W.CANCEL
+    setup = W.funded_setup(8, range(1, 5))
+    e1 = W.Orders.from_rows([
+        (B, 10, 1, 1, 50, 40), (S, 11, 2, 2, 60, 10), (B, 12, 3, 3, 30, 7)])
+    e2 = W.Orders.from_rows([
+        (B, 20, 1, 1, 40, 10), (C, 20, 1, 0, 0, 0), (C, 20, 1, 0, 0, 0),      # rested, cancelled twice
+        (S, 21, 2, 1, 50, 30), (C, 21, 2, 0, 0, 0),                          # filled against 10
+        (B, 22, 3, 9, 40, 5), (C, 22, 3, 0, 0, 0),                           # no book for sid 9
+        (B, 23, 200, 3, 40, 5), (C, 23, 200, 0, 0, 0),                       # no balance (account beyond the table)
+        (C, 10, 1, 0, 0, 0),                                                 # earlier epoch, partly filled
+        (B, 24, 4, 2, 45, 5), (S, 25, 5, 2, 45, 5), (C, 24, 4, 0, 0, 0), (C, 25, 5, 0, 0, 0),
+        (B, 26, 6, 4, 55, 8), (S, 27, 7, 4, 50, 3), (C, 26, 6, 0, 0, 0),     # partly filled, then cancelled
+        (C, 11, 1, 0, 0, 0), (C, 11, 2, 0, 0, 0),                            # wrong account, then the owner
+        (B, 28, 3, 3, 31, 4), (S, 29, 4, 3, 30, 11), (C, 28, 3, 0, 0, 0), (C, 12, 3, 0, 0, 0)])
+    e3 = W.Orders.from_rows([
+        (C, 24, 4, 0, 0, 0), (C, 26, 6, 0, 0, 0), (C, 29, 4, 0, 0, 0), (B, 30, 1, 1, 41, 2), (C, 30, 1, 0, 0, 0)])
+    eng = _funded_engine(kme_mod, 10, accounts=128, light_max=light_max)
+    o = oracle_mod.Oracle()
+    got, want = [], []
+    for part in (setup, e1, e2, e3):
+        got.append(eng.process(part).tape_json(part))
+        o.process(part)
+    want = o.tape_text()
+    assert "".join(got) == want, _first_diff("".join(got), want)
+    assert eng.snapshot_books() == o.dump_books()
