@@ -2044,9 +2044,14 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         n_rest += (uint32_t)__popcll(__ballot(lane < done && ((o_act >> 16) & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < done && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
         if (__ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR)) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
-        if (lane < done)   // one 16-B record per lane, at the record's input index (k_unsort reads them in order)
-            opaque_const(Sp).osort[B.i] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
-                                                  o_size, o_plo, o_phi);
+        {   // one 16-B record per lane, at the record's input index (k_unsort reads them in order); lanes
+            // past the batch's last answered record store to a dump slot behind the array instead of
+            // branching: a divergent branch here joins the loop latch, and the uniformity analysis then
+            // takes the batch loop's exit (w.dead) as divergent, demoting its state to lane masks
+            const size_t dst = lane < done ? (size_t)B.i : (size_t)opaque_const(Sp).os_base + (size_t)lane;
+            opaque_const(Sp).osort[dst] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
+                                                    o_size, o_plo, o_phi);
+        }
     }
     KST(const unsigned long long to0 = stamp();)
     w.flush_trades();

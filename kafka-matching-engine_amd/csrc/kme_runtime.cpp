@@ -251,7 +251,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     // arrived (k_unsort then reads it sequentially; no sorted-position map)
     S.os_base = E;
     S.os_lanes = 0;
-    if (funded) ALLOC(S.osort, (size_t)E);
+    if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
         ALLOC(S.rvals[0], E); ALLOC(S.rvals[1], E);
