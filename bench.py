@@ -307,7 +307,7 @@ def main():
     max_sid = int(sids.max())
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=max_sid + 1, max_epoch=E,
-                             max_resting=args.max_resting or min(total, 1 << 30), max_trades=2 * E + (1 << 16),
+                             max_resting=args.max_resting or min(total, (1 << 29) - 64 * (max_sid + 2) - E), max_trades=2 * E + (1 << 16),
                              max_accounts=nacc, device=local_rank, light_max=args.light_max)
     cfg.credit_shards = shards
     eng = kme.Engine(cfg)

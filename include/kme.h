@@ -101,7 +101,8 @@ typedef struct kme_config {
     uint32_t max_epoch;        /* max records per submitted epoch */
     uint32_t max_trades;       /* max trades per epoch (each trade = 2 fill records) */
     uint64_t max_resting;      /* resting orders the Orders store holds (FUNDED adds 64 node slots per
-                                  symbol for the per-group allocation chunks; total < 2^31) */
+                                  symbol for the per-group allocation chunks; total < 2^31; FUNDED:
+                                  max_resting + 64 (max_symbols + 1) + max_epoch <= 2^29) */
     uint64_t ledger_capacity;  /* EXACT: hash capacity of Balances and of Positions */
     int32_t device;            /* HIP device ordinal */
     uint32_t credit_shards;    /* FUNDED: number of symbol shards an account's credit is split over

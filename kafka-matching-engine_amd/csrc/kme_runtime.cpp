@@ -153,8 +153,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         cfg->max_epoch > (1u << 30) || cfg->max_resting == 0 || cfg->max_resting >= (1ull << 31) ||
         cfg->max_trades == 0)
         return KME_E_INVALID;
+    // FUNDED: the oid table (a power of two >= 2 (pool + epoch) entries) stays within 2^30 entries,
+    // so an entry's position rides in a packed record's signed 32-bit word (k_route, otab_final)
     if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28) ||
-                                         cfg->max_resting + (uint64_t)(cfg->max_symbols + 1) * POOL_CHUNK >= (1ull << 31)))
+                                         cfg->max_resting + (uint64_t)(cfg->max_symbols + 1) * POOL_CHUNK +
+                                                 cfg->max_epoch > (1ull << 29)))
         return KME_E_INVALID;
     if ((cfg->flags & ~(KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK)) != 0 ||
         ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1) ||   // a shard sees part of the ledger only

@@ -144,3 +144,12 @@ def test_invalid_config_rejected_before_touching_the_device(kme_mod):
     with pytest.raises(kme_mod.KmeError) as e:
         kme_mod.Engine(cfg)
     assert e.value.status == 1
+
+
+def test_funded_capacity_bound_on_the_oid_table(kme_mod):
+    # FUNDED: max_resting + 64 (max_symbols + 1) + max_epoch <= 2^29 (kme.h), so that the oid table
+    # stays within 2^30 entries and an entry's position fits the packed record's signed word
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, 8, 1024, (1 << 29) - 64 * 9 - 1024 + 1, max_accounts=8)
+    with pytest.raises(kme_mod.KmeError) as e:
+        kme_mod.Engine(cfg)
+    assert e.value.status == 1                                   # KME_E_INVALID, before any device call

@@ -26,7 +26,7 @@ def main():
     setup, stream, nsym, nacc, desc = bench.make_workload(args.workload, args.total, 0, 1)
     E = args.epoch
     eng = kme.Engine(kme.default_config(kme.MODE_FUNDED, max_symbols=nsym + 1, max_epoch=max(E, len(setup)),
-                                        max_resting=min(args.total, 1 << 30), max_trades=2 * E + (1 << 16),
+                                        max_resting=min(args.total, 1 << 28), max_trades=2 * E + (1 << 16),
                                         max_accounts=nacc, light_max=args.light_max))
     o = oracle.Oracle()
     for part in [setup] + [stream.slice(a, min(args.records, a + E)) for a in range(0, args.records, E)]:
