@@ -302,6 +302,13 @@ KDEV uint32_t block_sum_256(uint32_t v, uint32_t* red) {
 // (a counter hit by one atomic per wavefront serialises the whole kernel on its L2 line).
 constexpr uint32_t STREAM_BLOCKS = 2048;
 
+KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int32_t size, bool has_prev, int64_t prev) {
+    io.out_action[i] = ok ? action : (int32_t)REJECT;
+    io.out_size[i] = size;
+    io.out_prev[i] = has_prev ? prev : 0;
+    io.out_flags[i] = has_prev ? (uint8_t)KME_OUT_HAS_PREV : (uint8_t)0;
+}
+
 // BUY/SELL oid -> input index of this epoch; duplicate / sentinel oid checks; FUNDED: range domain
 // and per-account reservation need (max over adj of checkBalance's risk, KP:172-176).
 __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
@@ -346,14 +353,29 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
             else S.epos[i] = OT_DEAD;
             if (funded) {
                 const int32_t price = io.price[i], size = io.size[i];
+                const int64_t aid = io.aid[i];
                 if (price < 0 || price > 100 || size < 0) {
                     raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
+                } else if (aid >= 0 && aid < S.A) {
+                    const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
+                    atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
+                }
+                // k_route's work for the order, done here while its fields are in registers (the
+                // streaming stores overlap this kernel's atomics): symbol group, the packed record
+                // with the order's oid-table position, or the books.get == null reject (KP:202-203).
+                // acct_ok reads the accounts as they stand before this epoch's account records;
+                // k_route redoes it when the epoch has some (C_ACCT_OPS).
+                const int64_t sid = io.sid[i];
+                const int32_t grp = group_of(sid, S.G);
+                S.route_grp[i] = grp;
+                if (grp < 0) {
+                    write_out(io, i, a, false, size, false, 0);
                 } else {
-                    const int64_t aid = io.aid[i];
-                    if (aid >= 0 && aid < S.A) {
-                        const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
-                        atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
-                    }
+                    const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
+                    const int32_t w0 = (a & 0xFF) | ((price & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((sid < 0 ? 1 : 0) << 17);
+                    KG int4* p = &S.prec[2 * (size_t)i];
+                    p[0] = make_int4(w0, size, (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
+                    p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), placed ? (int32_t)h : -1, 0);
                 }
             }
         } else if (funded && (a == CREATE_BALANCE || a == TRANSFER)) {
@@ -368,13 +390,6 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
         if (na) atomicAdd(&S.ctr[ci(C_ACCT_OPS)], (unsigned long long)na);
         if (ni) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)ni);
     }
-}
-
-KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int32_t size, bool has_prev, int64_t prev) {
-    io.out_action[i] = ok ? action : (int32_t)REJECT;
-    io.out_size[i] = size;
-    io.out_prev[i] = has_prev ? prev : 0;
-    io.out_flags[i] = has_prev ? (uint8_t)KME_OUT_HAS_PREV : (uint8_t)0;
 }
 
 // FUNDED account records in arrival order (one wavefront; skipped when the epoch has none).
@@ -476,6 +491,18 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     int64_t ptgt = 0;             // PRec word 6 when it differs from tgt (a same-epoch cancel target)
     S.rest_slot[i] = -1;
     io.n_trades[i] = 0;
+    if (funded && (a == BUY || a == SELL)) {   // routed by k_emap
+        if (S.fallback) S.cancel_tgt[i] = -1;
+        if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
+        // the epoch has account records (k_ledger_funded has applied them): acct_ok again
+        const int32_t g = S.route_grp[i];
+        if (g < 0) return;
+        const int64_t aid = io.aid[i];
+        const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
+        KG int32_t* w0 = reinterpret_cast<KG int32_t*>(&S.prec[2 * (size_t)i]);
+        *w0 = (*w0 & ~(1 << 16)) | ((acct_ok ? 1 : 0) << 16);
+        return;
+    }
     bool direct = false, ok = false, acct_ok = false;
     switch (a) {
     case ADD_SYMBOL:
@@ -536,11 +563,10 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
     if (grp >= 0) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
-        // a BUY/SELL's word 6 is its oid-table entry's position (k_emap), which the matching kernel
-        // finalises (otab_final); a cancel's is its target
-        // (a same-epoch cancel target: -(its entry's position + 2), the slot read from the entry)
-        if (a == BUY || a == SELL) { const uint32_t h = S.epos[i]; tgt = h == OT_DEAD ? -1 : (int64_t)h; }
-        else if (ptgt <= -2) tgt = ptgt;
+        // word 6: a cancel's target (a same-epoch order: -(its entry's position + 2), the slot read
+        // from the entry the matcher finalised); a FUNDED BUY/SELL's packed record is k_emap's, with
+        // its own entry's position there
+        if (ptgt <= -2) tgt = ptgt;
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
