@@ -73,3 +73,45 @@ def test_two_epochs_in_flight(oracle_mod, tmp_path, light_max):
         assert got == o.tape_text(), f"epoch {k}"
         o.clear_tape()
     assert eng.snapshot_books() == o.dump_books()
+
+
+@pytest.mark.parametrize("light_max", [0, -1])
+def test_device_epoch_with_account_records(oracle_mod, light_max):
+    """A device epoch is not split at account records (kme_submit_epoch splits host epochs): orders
+    of an account created earlier in the same epoch pass the balance gate (KP:170), orders before
+    its CREATE_BALANCE do not -- k_emap routes the orders against the accounts as they stood, k_route
+    redoes acct_ok after k_ledger_funded.  Zero-risk orders (BUY at 0, SELL at 100, size 0) keep the
+    epoch inside the funded proof."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    B, S, C = W.BUY, W.SELL, W.CANCEL
+    setup = W.funded_setup(8, range(1, 5))
+    rows = [(B, 100, 50, 2, 0, 5),           # account 50 not created yet: REJECT
+            (100, 0, 50, 0, 0, 0),           # CREATE_BALANCE 50
+            (B, 101, 50, 2, 0, 5),           # risk 0: accepted, rests at 0
+            (S, 102, 50, 3, 100, 7),         # risk 0: accepted, rests at 100
+            (B, 103, 1, 2, 40, 3),           # a funded account's order
+            (C, 101, 50, 0, 0, 0),           # cancel of the order of the new account
+            (100, 0, 51, 0, 0, 0), (S, 104, 51, 3, 100, 0), (B, 105, 51, 3, 0, 2)]
+    part = W.Orders.from_rows(rows)
+    E = 64
+    cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=8, max_epoch=E, max_resting=1 << 12,
+                             max_accounts=64, light_max=light_max, max_trades=4 * E)
+    eng = kme.Engine(cfg)
+    eng.process(setup)
+    cols = {c: torch.from_numpy(np.ascontiguousarray(getattr(part, c))).to(dev)
+            for c in ("action", "oid", "aid", "sid", "price", "size")}
+    out = _dev_out(torch, dev, E, 4 * E)
+    ptrs = {c: t.data_ptr() for c, t in cols.items()}
+    optrs = {k: t.data_ptr() for k, t in out.items()}
+    optrs["trades_cap"] = 4 * E
+    eng.submit_device(ptrs, len(part), out=optrs)
+    st = eng.wait()
+    assert st.status == 0
+    o = oracle_mod.Oracle()
+    o.process(setup)
+    o.clear_tape()
+    o.process(part)
+    assert _result(out, len(part), st).tape_json(part) == o.tape_text()
+    assert eng.snapshot_books() == o.dump_books()
