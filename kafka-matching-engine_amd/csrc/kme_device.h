@@ -100,6 +100,7 @@ enum Ctr : int {
     C_FALLBACK,        // FUNDED + KME_FLAG_SERIAL_FALLBACK: nonzero = this epoch runs serially
     C_BUSY,            // FUNDED: groups k_match took this epoch (the host's stream choice for the next)
     C_REBUILD_FAIL,    // oid-table rebuild: entries that found no slot (persistent, zeroed by the rebuild)
+    C_LIGHT,           // FUNDED: k_match_lanes wavefronts that had a group this epoch (the next one's launch)
     C_NCTR = 16
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
@@ -108,7 +109,7 @@ constexpr int ci(int k) { return k * CTR_STRIDE; }
 // in its own region [s * tshard_cap, (s + 1) * tshard_cap) through its own counter line; a shard
 // that runs full spills to the overflow region behind them (counter C_TTMP).
 constexpr int TSHARDS = 256;
-enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2 };
+enum TShardWord : int { TS_USED = 0, TS_RESTS = 1, TS_CANCELS = 2, TS_LIGHT = 3 };
 
 
 struct DevState {

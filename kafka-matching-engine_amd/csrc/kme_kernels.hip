@@ -1962,16 +1962,19 @@ struct GroupWave {
 };
 
 // (2) FUNDED: one wavefront per symbol group, the group's records in arrival order.
-__global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
+// all: k_match_lanes is not launched this epoch (its last launch found no light group), so the
+// light groups are k_match's too.
+__global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf,
+                                              int all) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
     const int32_t g = blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
-    if (b >= e || e - b <= (uint32_t)S.light_max) return;   // empty, or a light group (k_match_lanes)
+    if (b >= e || (!all && e - b <= (uint32_t)S.light_max)) return;   // empty, or a light group (k_match_lanes)
     if (S.ctr[ci(C_FALLBACK)]) return;
     const uint32_t lim = err_limit(S.ctr, iop->n);          // records from a fault on do not take effect
-    if (threadIdx.x == 0) atomicAdd(&S.ctr[ci(C_BUSY)], 1ull);
+    if (threadIdx.x == 0 && e - b > (uint32_t)S.light_max) atomicAdd(&S.ctr[ci(C_BUSY)], 1ull);
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
     w.load_group();
@@ -2087,6 +2090,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     if (lane == 0) {
         if (n_rest) atomicAdd(&tsh[TS_RESTS], (unsigned long long)n_rest);
         if (n_cancel) atomicAdd(&tsh[TS_CANCELS], (unsigned long long)n_cancel);
+        if (e - b <= (uint32_t)S.light_max) atomicAdd(&tsh[TS_LIGHT], 1ull);   // a light group (all): lanes next epoch
     }
 #ifdef KME_STAMPS
     const unsigned long long tk1 = stamp();
@@ -2428,6 +2432,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
     uint32_t b = 0, e = 0;
     if (lane_id() < LANE_GROUPS && g < S.G) { b = S.seg[g]; e = S.seg[g + 1]; }
     if (e - b > (uint32_t)S.light_max) e = b;                // a heavy group: k_match's
+    const bool has_group = __ballot(b < e) != 0;             // (C_LIGHT: the next epoch's launch choice)
     uint32_t n_rest = 0, n_cancel = 0;
     if (b < e) {
         GroupLane w(S, io, fs, g);
@@ -2583,6 +2588,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
         KG unsigned long long* tsh = S.tsh + (size_t)(blockIdx.x & (TSHARDS - 1)) * CTR_STRIDE;
         if (n_rest) atomicAdd(&tsh[TS_RESTS], (unsigned long long)n_rest);
         if (n_cancel) atomicAdd(&tsh[TS_CANCELS], (unsigned long long)n_cancel);
+        if (has_group) atomicAdd(&tsh[TS_LIGHT], 1ull);
     }
 }
 
@@ -2823,12 +2829,14 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
 __global__ void __launch_bounds__(256) k_tsh_fold(DevState S) {
     __shared__ uint32_t red[4];
     KG unsigned long long* line = S.tsh + (size_t)threadIdx.x * CTR_STRIDE;   // TSHARDS == 256 threads
-    const unsigned long long rests = line[TS_RESTS], cancels = line[TS_CANCELS];
-    line[TS_USED] = 0; line[TS_RESTS] = 0; line[TS_CANCELS] = 0;
+    const unsigned long long rests = line[TS_RESTS], cancels = line[TS_CANCELS], light = line[TS_LIGHT];
+    line[TS_USED] = 0; line[TS_RESTS] = 0; line[TS_CANCELS] = 0; line[TS_LIGHT] = 0;
     const uint32_t r = block_sum_256((uint32_t)rests, red), c = block_sum_256((uint32_t)cancels, red);
+    const uint32_t l = block_sum_256((uint32_t)light, red);
     if (threadIdx.x == 0) {
         if (r) atomicAdd(&S.ctr[ci(C_RESTS)], (unsigned long long)r);
         if (c) atomicAdd(&S.ctr[ci(C_CANCEL_OK)], (unsigned long long)c);
+        if (l) atomicAdd(&S.ctr[ci(C_LIGHT)], (unsigned long long)l);
     }
 }
 
@@ -2915,7 +2923,8 @@ __global__ void k_init_state(DevState S) {
 __global__ void k_epoch_reset(DevState S) {
     const int k = threadIdx.x;
     if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
-    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY) S.ctr[ci(k)] = 0ull;
+    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY || k == C_LIGHT)
+        S.ctr[ci(k)] = 0ull;
 }
 
 // ------------------------------------------------------------------ launchers
@@ -2969,8 +2978,8 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src);
     return src;
 }
-void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
-    hipLaunchKernelGGL(k_match, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf);
+void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all) {
+    hipLaunchKernelGGL(k_match, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

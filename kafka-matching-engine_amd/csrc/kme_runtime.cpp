@@ -41,6 +41,7 @@ struct kme_engine {
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint64_t last_busy = 1;              // groups k_match took in the last epoch (C_BUSY)
+    uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
     DevState S{};
     DevState* d_S = nullptr;
@@ -384,16 +385,19 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         // light groups one lane each, concurrently with k_match's busy ones (a second stream).  When
         // the last epoch had no busy group both go on the engine stream: the fork / join costs
         // ~30 us per epoch (measured), k_match then only finds empty work (~16 us at C3).
-        const bool fork = S.light_max > 0 && e->last_busy != 0;
+        // Likewise, when the last epoch had no light group (every group busy: the N = 8 shard shape,
+        // C2, C5), k_match_lanes is not launched and k_match takes any light group itself.
+        const bool lanes = S.light_max > 0 && e->last_light != 0;
+        const bool fork = lanes && e->last_busy != 0;
         if (fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, st));
             HIP_TRY(hipStreamWaitEvent(e->lane_stream, e->ev_fork, 0));
             launch_match_lanes(S, e->d_S, e->d_io, buf, e->lane_stream);
             HIP_TRY(hipEventRecord(e->ev_join, e->lane_stream));
-        } else if (S.light_max > 0) {
+        } else if (lanes) {
             launch_match_lanes(S, e->d_S, e->d_io, buf, st);
         }
-        launch_match(S, e->d_S, e->d_io, buf, st);
+        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);
@@ -459,6 +463,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.serial_fallback = c[ci(C_FALLBACK)] ? 1u : 0u;
     s.n_effective = last_n;
     e->last_busy = c[ci(C_BUSY)];
+    e->last_light = c[ci(C_LIGHT)];
     if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
