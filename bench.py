@@ -169,71 +169,38 @@ def reduce_stats(dist, torch, elapsed: float, n_orders: int, n_trades: int, ok: 
     return float(t.item()), float(sums[0].item()), float(sums[1].item()), bool(flag.item())
 
 
-def measure_host_path(eng, stream, first, n_epochs, E, dev, max_trades):
-    """The product path of a host caller at rate: epochs in pinned host memory,
-    H2D of epoch k+1 on one stream and D2H of epoch k's results on another while epoch k+1's kernels
-    run (double-buffered device inputs and results).  Timed from the first H2D to the last D2H;
-    PCIe-inclusive, so it is a secondary field, never the headline value."""
-    import torch
+def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
+    """The Java processor's path at rate, timed by the committed C harness
+    (integration/host_harness.c): GpuMatchingEngine.java's schedule -- records written into two
+    slots of registered host columns, kme_submit_epoch_host (H2D, kernels, D2H queued), kme_wait +
+    kme_expand_rows into the slot's row buffer and a pass over the rows -- over exactly the C ABI
+    calls kme_jni.c makes.  PCIe- and host-inclusive: a secondary field, never the headline value."""
+    import ctypes as C
 
-    cols = ("action", "oid", "aid", "sid", "price", "size")
-    n_rec = n_epochs * E
-    a0 = first * E
-    host_in = {c: torch.from_numpy(np.ascontiguousarray(getattr(stream, c)[a0:a0 + n_rec])).pin_memory() for c in cols}
-    dev_in = [{c: torch.empty(E, dtype=host_in[c].dtype, device=dev) for c in cols} for _ in range(2)]
-    shapes = {"out_action": (E, torch.int32), "out_size": (E, torch.int32), "out_prev": (E, torch.int64),
-              "out_flags": (E, torch.uint8), "trade_off": (E + 1, torch.int32), "trades": (4 * max_trades, torch.int64)}
-    dev_out = [{k: torch.empty(n, dtype=t, device=dev) for k, (n, t) in shapes.items()} for _ in range(2)]
-    host_out = [{k: torch.empty(n, dtype=t).pin_memory() for k, (n, t) in shapes.items()} for _ in range(2)]
-    work = torch.cuda.current_stream(dev)
-    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    ev_in = [torch.cuda.Event() for _ in range(2)]
-    ev_done = [torch.cuda.Event() for _ in range(2)]
-    ev_out = [torch.cuda.Event() for _ in range(2)]
-    n_trades = []
+    import kme
 
-    def h2d_copy(k):
-        b = k % 2
-        with torch.cuda.stream(h2d):
-            for c in cols:
-                dev_in[b][c].copy_(host_in[c][k * E:(k + 1) * E], non_blocking=True)
-            ev_in[b].record(h2d)
-
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    h2d_copy(0)
-    for k in range(n_epochs):
-        b = k % 2
-        work.wait_event(ev_in[b])
-        out = {key: t.data_ptr() for key, t in dev_out[b].items()}
-        out["trades_cap"] = max_trades
-        eng.submit_device({c: t.data_ptr() for c, t in dev_in[b].items()}, E, out=out)
-        ev_done[b].record(work)
-        if k + 1 < n_epochs:
-            h2d_copy(k + 1)          # dev_in[(k+1) % 2] was read by epoch k-1, finished at its wait()
-        with torch.cuda.stream(d2h):
-            d2h.wait_event(ev_done[b])
-            for key, t in dev_out[b].items():
-                if key != "trades":
-                    host_out[b][key].copy_(t, non_blocking=True)
-            ev_out[b].record(d2h)
-        st = eng.wait()
-        nt = int(st.n_trades)
-        n_trades.append(nt)
-        if nt:                       # this epoch's trades (count known now), behind its other results
-            with torch.cuda.stream(d2h):
-                host_out[b]["trades"][:4 * nt].copy_(dev_out[b]["trades"][:4 * nt], non_blocking=True)
-                ev_out[b].record(d2h)
-        ev_out[(k + 1) % 2].synchronize()   # host_out[(k+1) % 2] free for the next epoch
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
+    lib = C.CDLL(os.path.join(ROOT, "integration", "libkme_host_harness.so"))
+    lib.kme_host_path_run.argtypes = [C.c_void_p, C.POINTER(kme.kme_orders), C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_double)]
+    lib.kme_host_path_run.restype = C.c_int
+    a0, n_rec = first * E, n_epochs * E
+    cols = {c: np.ascontiguousarray(getattr(stream, c)[a0:a0 + n_rec]) for c in ("action", "oid", "aid", "sid", "price", "size")}
+    ko = kme.kme_orders(*[C.c_void_p(cols[c].ctypes.data) for c in ("action", "oid", "aid", "sid", "price", "size")])
+    stats = (C.c_double * 7)()
+    rc = lib.kme_host_path_run(eng.handle, C.byref(ko), E, n_epochs, max_trades, stats)
+    if rc:
+        raise kme.KmeError(rc, "kme_host_path_run")
+    dt = stats[0]
     h2d_b = 36 * E
-    d2h_b = 21 * E + 4 + 32 * (sum(n_trades) / n_epochs)
+    d2h_b = 21 * E + 4 + 32 * (stats[5] / n_epochs)
     return {"value": n_rec / dt, "unit": "records/s", "epochs": n_epochs, "epoch_records": E,
-            "h2d_bytes_per_epoch": h2d_b, "d2h_bytes_per_epoch": int(d2h_b),
+            "rows": int(stats[1]), "trades": int(stats[5]), "rows_per_s": stats[1] / dt, "h2d_bytes_per_epoch": h2d_b, "d2h_bytes_per_epoch": int(d2h_b),
             "pcie_GBps_each_way": round(max(h2d_b, d2h_b) * n_epochs / dt / 1e9, 2),
-            "path": "pinned host SoA -> H2D (stream 1) | kernels (engine stream) | results D2H (stream 2), "
-                    "double-buffered; PCIe-inclusive, not the headline value"}
+            "host_s": {"fill": round(stats[2], 4), "wait": round(stats[3], 4), "rows": round(stats[4], 4),
+                       "total": round(dt, 4)},
+            "path": "integration/host_harness.c: GpuMatchingEngine.java's schedule over kme_jni.c's C ABI calls "
+                    "(registered host columns -> kme_submit_epoch_host -> kme_wait + kme_expand_rows -> rows read), "
+                    "two epochs in flight; PCIe- and host-inclusive, not the headline value"}
 
 
 def parse_args(argv=None):
@@ -419,7 +386,7 @@ def main():
         print(f"rank {rank}: market data check failed (own snapshot vs full-range: {md_local}, "
               f"all-gathered block: {md_gather})", file=sys.stderr, flush=True)
     # the host-buffer path (after the market-data check: its epochs move the books on)
-    host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, dev, cfg.max_trades) \
+    host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, cfg.max_trades) \
         if host_epochs else None
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 4
+#define KME_ABI_VERSION 5
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -62,7 +62,10 @@ enum kme_domain {
     KME_D_FUNDED_RANGE = 9,  /* FUNDED mode: BUY/SELL price outside 0..100 or size < 0 */
     KME_D_SENTINEL_OID = 10, /* reserved (no longer raised: the oid tables have no sentinel oids) */
     KME_D_CAP_POOL = 11, KME_D_CAP_OIDTAB = 12, KME_D_CAP_TRADES = 13, KME_D_CAP_SYMBOL = 14,
-    KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17
+    KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17,
+    KME_D_UNPROVEN = 18      /* KME_E_UNFUNDED of the epoch as a whole: the funded proof failed, so
+                                none of its records took effect (error_index -1, n_effective 0),
+                                whatever other fault the epoch holds further on */
 };
 
 /* Engine modes.
@@ -201,6 +204,50 @@ kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in_dev, uint
 kme_status kme_wait(kme_engine* e, kme_epoch_status* st);
 /* Engine-owned device result buffers of the last device epoch. */
 kme_status kme_device_results(kme_engine* e, kme_epoch_result* out_dev);
+
+/* ---- Host epochs at device rate: the Java processor's path ----
+ * kme_submit_epoch above copies pageable arrays and waits; a JVM feeding the engine at rate keeps two
+ * epochs of records in caller-owned host memory that the engine's copy engines reach directly (JVM
+ * direct ByteBuffers), and overlaps the PCIe transfers of one epoch with the kernels of the other.
+ *
+ * kme_host_register: make `bytes` of caller host memory at `host` DMA-able and device-mapped
+ * (hipHostRegister); kme_host_unregister undoes it (no epoch using it may be in flight). */
+kme_status kme_host_register(kme_engine* e, void* host, size_t bytes);
+kme_status kme_host_unregister(kme_engine* e, void* host);
+/* MatchingEngine.process (KP:96-126) for n records whose inputs and results live in host memory
+ * registered with kme_host_register.  Asynchronous: the H2D of the six input columns (copy stream),
+ * the epoch's kernels (engine stream) and the D2H of the results -- out_action / out_size / out_prev /
+ * out_flags [n], trade_off [n + 1] and trades [0, trade_off[n]) (copy stream; the trades by a copy
+ * kernel that reads their count on the device) -- are queued and the call returns.  kme_poll tells
+ * when the oldest epoch is done, kme_wait completes it; the results are valid after kme_wait.  Up to
+ * two epochs in flight (as kme_submit_epoch_device): the inputs of epoch k + 1 cross PCIe while
+ * epoch k's kernels run.  As on the device path the epoch is not split at account records. */
+kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in_host, uint32_t n,
+                                 const kme_epoch_result* out_host);
+/* Non-blocking: *done = 1 when the oldest epoch in flight has completed (kme_wait will not block) or
+ * none is in flight, 0 while it runs.  The processor's wall-clock punctuator polls with it, so the
+ * stream thread never blocks on the GPU (the reference's process() never waits either, KP:96). */
+kme_status kme_poll(kme_engine* e, int* done);
+
+/* One MatchOut record as the processor forwards it (KP:97, 124, 272-273): key "IN" (kind 0) or "OUT"
+ * (kind 1 = a maker / taker fill, kind 2 = the OUT echo), value = an Order (KP:449-458). */
+typedef struct kme_row {
+    int64_t oid, aid, sid;
+    int64_t prev;          /* Order.prev when has_prev (the OUT echo of an append, KP:217), else null */
+    int32_t action, price, size;
+    uint8_t kind, has_prev;
+    uint8_t _pad[2];
+} kme_row; /* 48 bytes */
+/* Expands the results of records [0, n) of an epoch into its MatchOut rows, in order: IN, the maker
+ * and taker fill of each trade (executeTrade, KP:265-274), OUT.  *n_rows = rows needed; nothing is
+ * written past cap (KME_E_CAPACITY when they do not fit).  Host buffers; the JNI glue and the host-path
+ * harness both use it. */
+kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_result* res, kme_row* rows,
+                           size_t cap, size_t* n_rows);
+
+/* Identifies the sources libkme was built from (a hash of csrc/ and include/): the test session
+ * rebuilds the library when it differs from the tree's. */
+const char* kme_build_id(void);
 
 /* Persistence (SURVEY §8 row f next-3; the reference keeps its state in RocksDB stores with
  * changelogs, KP:30-49, and commits after every record, KP:125).  kme_checkpoint writes the

@@ -1,16 +1,26 @@
 /* kme_jni.c -- JNI glue for GpuMatchingEngine.java, the processor that replaces the reference's
  * MatchingEngine at its topology (KProcessor.java:52, `.addProcessor("MatchingEngine", ...)`).
  *
- * The Java side buffers input Orders into an epoch (structure of arrays), calls submit(), and
- * forwards the rows this file expands from the epoch result, in the reference's order: for input i
- * the IN echo (KP:97), then the maker fill and the taker fill of each trade (executeTrade,
- * KP:265-274), then the OUT echo (KP:124).  On an error the rows of the records that took effect
- * ([0, n_effective), kme.h kme_epoch_status) are still produced: the reference forwards and commits
- * every record before the one that throws (KP:97, 124-125).
+ * The product path at rate (include/kme.h, "Host epochs at device rate"): the Java side owns two
+ * slots of JVM direct ByteBuffers -- the six Order columns of an epoch (structure of arrays, native
+ * byte order) and the MatchOut rows that come back -- and this file registers them with the engine
+ * once (kme_host_register), so an epoch crosses PCIe straight from and to them: no array pinning, no
+ * copies through the JNI boundary, and the garbage collector is never blocked on the GPU.
+ *
+ *   bind(h, slot, action, oid, aid, sid, price, size, rows)   the slot's buffers (checked, registered)
+ *   submit(h, slot, n)        kme_submit_epoch_host: H2D, kernels, D2H queued; returns at once
+ *   poll(h)                   kme_poll: 1 when the oldest epoch in flight is done (punctuator)
+ *   complete(h, slot, st)     kme_wait + kme_expand_rows into the slot's row buffer, in the
+ *                             reference's order: IN (KP:97), maker / taker fill per trade
+ *                             (executeTrade, KP:265-274), OUT (KP:124); st[0..3] = status, domain
+ *                             detail, error index, records that took effect (kme_epoch_status)
+ *
+ * On an error the rows of the records that took effect ([0, n_effective)) are still produced: the
+ * reference forwards and commits every record before the one that throws (KP:97, 124-125).
  *
  * Build (JDK present): integration/jni/build.sh.  This container has no JDK; the CPU test suite
- * compiles this file with -fsyntax-only against tests/jni_stub/jni.h (a declaration subset) so that
- * it stays in step with include/kme.h.
+ * compiles this file with -fsyntax-only against tests/jni_stub/jni.h (a declaration subset) and the GPU
+ * suite drives it through a JNIEnv made with ctypes (tests/test_jni_glue.py).
  */
 #include <jni.h>
 #include <stdint.h>
@@ -19,13 +29,19 @@
 
 #include "kme.h"
 
-/* Fill record actions (KP:265-274). */
-enum { JKME_BOUGHT = 5, JKME_SOLD = 6, JKME_BUY = 2 };
+typedef struct jslot {
+    kme_orders in;                 /* the slot's direct ByteBuffers (Java writes the records) */
+    kme_row* rows;                 /* direct ByteBuffer of MatchOut rows (Java reads them) */
+    size_t rows_cap;
+    void* regs[7];                 /* what bind() registered */
+    kme_epoch_result res;          /* native host results, registered at create() */
+    uint32_t n;                    /* records of the epoch in flight (0 = none) */
+} jslot;
 
 typedef struct jkme {
     kme_engine* e;
     uint32_t max_epoch, max_trades;
-    kme_epoch_result res;          /* host result buffers, reused by every submit */
+    jslot slot[2];
 } jkme;
 
 static void throw_state(JNIEnv* env, const char* msg) {
@@ -33,15 +49,25 @@ static void throw_state(JNIEnv* env, const char* msg) {
     if (c) (*env)->ThrowNew(env, c, msg);
 }
 
+static void* aligned(size_t bytes) {
+    void* p = NULL;
+    return posix_memalign(&p, 4096, bytes ? bytes : 1) == 0 ? p : NULL;
+}
+
 static void free_handle(jkme* h) {
     if (!h) return;
+    for (int s = 0; s < 2; ++s) {
+        jslot* sl = &h->slot[s];
+        for (int k = 0; k < 7; ++k)
+            if (sl->regs[k] && h->e) kme_host_unregister(h->e, sl->regs[k]);
+        void* res[6] = {sl->res.out_action, sl->res.out_size, sl->res.out_prev, sl->res.out_flags, sl->res.trade_off,
+                        sl->res.trades};
+        for (int k = 0; k < 6; ++k) {
+            if (res[k] && h->e) kme_host_unregister(h->e, res[k]);
+            free(res[k]);
+        }
+    }
     if (h->e) kme_destroy(h->e);
-    free(h->res.out_action);
-    free(h->res.out_size);
-    free(h->res.out_prev);
-    free(h->res.out_flags);
-    free(h->res.trade_off);
-    free(h->res.trades);
     free(h);
 }
 
@@ -69,25 +95,32 @@ JNIEXPORT jlong JNICALL Java_GpuMatchingEngine_create(JNIEnv* env, jclass cls, j
     if (!h) { throw_state(env, "kme: out of host memory"); return 0; }
     h->max_epoch = (uint32_t)maxEpoch;
     h->max_trades = (uint32_t)maxTrades;
-    h->res.out_action = (int32_t*)malloc(sizeof(int32_t) * (size_t)maxEpoch);
-    h->res.out_size = (int32_t*)malloc(sizeof(int32_t) * (size_t)maxEpoch);
-    h->res.out_prev = (int64_t*)malloc(sizeof(int64_t) * (size_t)maxEpoch);
-    h->res.out_flags = (uint8_t*)malloc((size_t)maxEpoch);
-    h->res.trade_off = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)maxEpoch + 1));
-    h->res.trades = (kme_trade*)malloc(sizeof(kme_trade) * (size_t)maxTrades);
-    h->res.trades_cap = (uint32_t)maxTrades;
-    if (!h->res.out_action || !h->res.out_size || !h->res.out_prev || !h->res.out_flags || !h->res.trade_off ||
-        !h->res.trades) {
-        free_handle(h);
-        throw_state(env, "kme: out of host memory");
-        return 0;
-    }
     const kme_status s = kme_create(&cfg, &h->e);
     if (s != KME_OK) {
         h->e = NULL;
         free_handle(h);
         throw_state(env, kme_strerror(s));
         return 0;
+    }
+    const size_t E = (size_t)maxEpoch;
+    for (int k = 0; k < 2; ++k) {
+        kme_epoch_result* r = &h->slot[k].res;
+        r->out_action = (int32_t*)aligned(sizeof(int32_t) * E);
+        r->out_size = (int32_t*)aligned(sizeof(int32_t) * E);
+        r->out_prev = (int64_t*)aligned(sizeof(int64_t) * E);
+        r->out_flags = (uint8_t*)aligned(E);
+        r->trade_off = (uint32_t*)aligned(sizeof(uint32_t) * (E + 1));
+        r->trades = (kme_trade*)aligned(sizeof(kme_trade) * (size_t)maxTrades);
+        r->trades_cap = (uint32_t)maxTrades;
+        const size_t bytes[6] = {4 * E, 4 * E, 8 * E, E, 4 * (E + 1), sizeof(kme_trade) * (size_t)maxTrades};
+        void* p[6] = {r->out_action, r->out_size, r->out_prev, r->out_flags, r->trade_off, r->trades};
+        for (int q = 0; q < 6; ++q) {
+            if (!p[q] || kme_host_register(h->e, p[q], bytes[q]) != KME_OK) {
+                free_handle(h);
+                throw_state(env, "kme: cannot allocate or register the result buffers");
+                return 0;
+            }
+        }
     }
     return (jlong)(intptr_t)h;
 }
@@ -98,97 +131,96 @@ JNIEXPORT void JNICALL Java_GpuMatchingEngine_destroy(JNIEnv* env, jclass cls, j
     free_handle((jkme*)(intptr_t)handle);
 }
 
-/* static native int submit(long h, int n, int[] action, long[] oid, long[] aid, long[] sid,
- *                          int[] price, int[] size,
- *                          byte[] kind, int[] oAction, long[] oOid, long[] oAid, long[] oSid,
- *                          int[] oPrice, int[] oSize, long[] oPrev, byte[] oHasPrev, long[] status)
- * Runs the n buffered records as one epoch and writes the MatchOut rows (kind 0 = "IN", 1 = fill,
- * 2 = "OUT") of the records that took effect.  Returns the row count; status[0..2] = kme_status,
- * domain detail, error index.  The output arrays need 2 n + 2 maxTrades rows. */
-JNIEXPORT jint JNICALL Java_GpuMatchingEngine_submit(JNIEnv* env, jclass cls, jlong handle, jint n,
-        jintArray action, jlongArray oid, jlongArray aid, jlongArray sid, jintArray price, jintArray size,
-        jbyteArray kind, jintArray oAction, jlongArray oOid, jlongArray oAid, jlongArray oSid,
-        jintArray oPrice, jintArray oSize, jlongArray oPrev, jbyteArray oHasPrev, jlongArray status) {
+/* static native int bind(long h, int slot, ByteBuffer action, ByteBuffer oid, ByteBuffer aid,
+ *                        ByteBuffer sid, ByteBuffer price, ByteBuffer size, ByteBuffer rows)
+ * Direct buffers of at least maxEpoch elements each (int / long columns) and rows for
+ * 2 maxEpoch + 2 maxTrades MatchOut rows of 48 bytes; returns a kme_status. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_bind(JNIEnv* env, jclass cls, jlong handle, jint slot, jobject action,
+                                                     jobject oid, jobject aid, jobject sid, jobject price, jobject size,
+                                                     jobject rows) {
     (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || n < 0 || (uint32_t)n > h->max_epoch) { throw_state(env, "kme: bad handle or epoch size"); return -1; }
-    const jsize rows_cap = (*env)->GetArrayLength(env, kind);
-    if ((int64_t)rows_cap < 2 * (int64_t)n) { throw_state(env, "kme: output arrays too small"); return -1; }
+    if (!h || slot < 0 || slot > 1 || h->slot[slot].n) return KME_E_INVALID;
+    jslot* sl = &h->slot[slot];
+    const size_t E = h->max_epoch;
+    jobject bufs[7] = {action, oid, aid, sid, price, size, rows};
+    const size_t need[7] = {4 * E, 8 * E, 8 * E, 8 * E, 4 * E, 4 * E,
+                            sizeof(kme_row) * (2 * E + 2 * (size_t)h->max_trades)};
+    void* addr[7];
+    for (int k = 0; k < 7; ++k) {
+        if (!bufs[k]) return KME_E_INVALID;
+        addr[k] = (*env)->GetDirectBufferAddress(env, bufs[k]);
+        const jlong cap = (*env)->GetDirectBufferCapacity(env, bufs[k]);
+        if (!addr[k] || cap < 0 || (size_t)cap < need[k] || ((uintptr_t)addr[k] & 7u)) return KME_E_INVALID;
+    }
+    for (int k = 0; k < 7; ++k) {
+        if (sl->regs[k]) { kme_host_unregister(h->e, sl->regs[k]); sl->regs[k] = NULL; }
+        const kme_status s = kme_host_register(h->e, addr[k], need[k]);
+        if (s != KME_OK) return s;
+        sl->regs[k] = addr[k];
+    }
+    sl->in.action = (const int32_t*)addr[0];
+    sl->in.oid = (const int64_t*)addr[1];
+    sl->in.aid = (const int64_t*)addr[2];
+    sl->in.sid = (const int64_t*)addr[3];
+    sl->in.price = (const int32_t*)addr[4];
+    sl->in.size = (const int32_t*)addr[5];
+    sl->rows = (kme_row*)addr[6];
+    sl->rows_cap = need[6] / sizeof(kme_row);
+    return KME_OK;
+}
 
-    /* inputs: pinned for the duration of the (synchronous) submission */
-    kme_orders in;
-    int32_t* a = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, action, NULL);
-    int64_t* o = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, oid, NULL);
-    int64_t* ac = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, aid, NULL);
-    int64_t* sd = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, sid, NULL);
-    int32_t* pr = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, price, NULL);
-    int32_t* sz = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, size, NULL);
-    in.action = a; in.oid = o; in.aid = ac; in.sid = sd; in.price = pr; in.size = sz;
+/* static native int submit(long h, int slot, int n): the slot's n buffered records as one epoch,
+ * asynchronously (at most two epochs in flight); returns a kme_status. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_submit(JNIEnv* env, jclass cls, jlong handle, jint slot, jint n) {
+    (void)env; (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h || slot < 0 || slot > 1 || n <= 0 || (uint32_t)n > h->max_epoch) return KME_E_INVALID;
+    jslot* sl = &h->slot[slot];
+    if (sl->n || !sl->rows) return KME_E_INVALID;   /* in flight already, or never bound */
+    const kme_status s = kme_submit_epoch_host(h->e, &sl->in, (uint32_t)n, &sl->res);
+    if (s == KME_OK) sl->n = (uint32_t)n;
+    return s;
+}
+
+/* static native int poll(long h): 1 when the oldest epoch in flight is done (complete() will not
+ * block) or none is in flight, 0 while it runs, -status on an error. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_poll(JNIEnv* env, jclass cls, jlong handle) {
+    (void)env; (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h) return -KME_E_INVALID;
+    int done = 0;
+    const kme_status s = kme_poll(h->e, &done);
+    return s == KME_OK ? (jint)done : -(jint)s;
+}
+
+/* static native int complete(long h, int slot, long[] status): waits for the slot's epoch (the oldest
+ * in flight) and writes the MatchOut rows of the records that took effect into the slot's row buffer.
+ * Returns the row count; status[0..3] = kme_status, domain detail, error index, records that took
+ * effect. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, jlong handle, jint slot,
+                                                         jlongArray status) {
+    (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h || slot < 0 || slot > 1 || !h->slot[slot].n) { throw_state(env, "kme: no epoch in flight on this slot"); return -1; }
+    if (!status || (*env)->GetArrayLength(env, status) < 4) { throw_state(env, "kme: status needs 4 entries"); return -1; }
+    jslot* sl = &h->slot[slot];
     kme_epoch_status st;
     memset(&st, 0, sizeof st);
-    const kme_status s = kme_submit_epoch(h->e, &in, (uint32_t)n, &h->res, &st);
-
-    /* rows of the records that took effect */
-    const uint32_t ne = s == KME_OK ? (uint32_t)n : st.n_effective;
-    jint rows = 0;
-    jbyte* k = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, kind, NULL);
-    int32_t* ra = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, oAction, NULL);
-    int64_t* ro = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, oOid, NULL);
-    int64_t* rc = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, oAid, NULL);
-    int64_t* rs = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, oSid, NULL);
-    int32_t* rp = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, oPrice, NULL);
-    int32_t* rz = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, oSize, NULL);
-    int64_t* rv = (int64_t*)(*env)->GetPrimitiveArrayCritical(env, oPrev, NULL);
-    jbyte* rh = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, oHasPrev, NULL);
-    int overflow = 0;
-    for (uint32_t i = 0; i < ne && !overflow; ++i) {
-        const uint32_t t0 = h->res.trade_off[i], t1 = h->res.trade_off[i + 1];
-        if ((int64_t)rows + 2 + 2 * (int64_t)(t1 - t0) > (int64_t)rows_cap) { overflow = 1; break; }
-        /* IN: the input unchanged (KP:97) */
-        k[rows] = 0; ra[rows] = a[i]; ro[rows] = o[i]; rc[rows] = ac[i]; rs[rows] = sd[i];
-        rp[rows] = pr[i]; rz[rows] = sz[i]; rv[rows] = 0; rh[rows] = 0; ++rows;
-        const int taker_buy = a[i] == JKME_BUY;
-        for (uint32_t t = t0; t < t1; ++t) {
-            const kme_trade* tr = &h->res.trades[t];
-            /* maker fill: {SOLD|BOUGHT, maker oid/aid/sid, 0, size} */
-            k[rows] = 1; ra[rows] = taker_buy ? JKME_SOLD : JKME_BOUGHT; ro[rows] = tr->maker_oid;
-            rc[rows] = tr->maker_aid; rs[rows] = tr->maker_sid; rp[rows] = 0; rz[rows] = tr->size;
-            rv[rows] = 0; rh[rows] = 0; ++rows;
-            /* taker fill: {BOUGHT|SOLD, taker oid/aid/sid, taker.price - maker.price, size} */
-            k[rows] = 1; ra[rows] = taker_buy ? JKME_BOUGHT : JKME_SOLD; ro[rows] = o[i]; rc[rows] = ac[i];
-            rs[rows] = sd[i]; rp[rows] = (int32_t)((uint32_t)pr[i] - (uint32_t)tr->maker_price);
-            rz[rows] = tr->size; rv[rows] = 0; rh[rows] = 0; ++rows;
-        }
-        /* OUT: the mutated order (KP:124; prev set by addOrder, KP:218) */
-        k[rows] = 2; ra[rows] = h->res.out_action[i]; ro[rows] = o[i]; rc[rows] = ac[i]; rs[rows] = sd[i];
-        rp[rows] = pr[i]; rz[rows] = h->res.out_size[i];
-        rh[rows] = (h->res.out_flags[i] & KME_OUT_HAS_PREV) ? 1 : 0;
-        rv[rows] = rh[rows] ? h->res.out_prev[i] : 0;
-        ++rows;
-    }
-    (*env)->ReleasePrimitiveArrayCritical(env, oHasPrev, rh, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oPrev, rv, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oSize, rz, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oPrice, rp, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oSid, rs, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oAid, rc, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oOid, ro, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, oAction, ra, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, kind, k, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, size, sz, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, price, pr, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, sid, sd, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, aid, ac, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, oid, o, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, action, a, JNI_ABORT);
-
-    jlong stv[3];
-    stv[0] = (jlong)s;
-    stv[1] = (jlong)st.detail;
-    stv[2] = (jlong)st.error_index;
-    (*env)->SetLongArrayRegion(env, status, 0, 3, stv);
-    if (overflow) { throw_state(env, "kme: output arrays too small for the epoch's trades"); return -1; }
-    return rows;
+    const kme_status s = kme_wait(h->e, &st);
+    const uint32_t n = sl->n;
+    sl->n = 0;
+    const uint32_t ne = s == KME_OK ? n : (st.n_effective < n ? st.n_effective : n);
+    size_t rows = 0;
+    const kme_status x = ne ? kme_expand_rows(&sl->in, ne, &sl->res, sl->rows, sl->rows_cap, &rows) : KME_OK;
+    jlong stv[4];
+    stv[0] = (jlong)(s != KME_OK ? s : x);
+    stv[1] = (jlong)(s != KME_OK ? st.detail : (x != KME_OK ? KME_D_CAP_TRADES : 0));
+    stv[2] = (jlong)(s != KME_OK ? st.error_index : -1);
+    stv[3] = (jlong)(x == KME_OK ? ne : 0);
+    (*env)->SetLongArrayRegion(env, status, 0, 4, stv);
+    if (x != KME_OK) return 0;   /* (cannot happen: the row buffer holds 2 maxEpoch + 2 maxTrades rows) */
+    return (jint)rows;
 }
 
 /* static native String statusText(int status) */
@@ -198,10 +230,10 @@ JNIEXPORT jstring JNICALL Java_GpuMatchingEngine_statusText(JNIEnv* env, jclass 
 }
 
 /* static native int checkpoint(long h, String path) / restore(long h, String path): persistence
- * in place of the RocksDB changelogs (KP:30-49); call checkpoint after a flush, before commit. */
+ * in place of the RocksDB changelogs (KP:30-49); between epochs (nothing in flight), before commit. */
 static jint ckpt(JNIEnv* env, jlong handle, jstring path, int restore) {
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h) return KME_E_INVALID;
+    if (!h || !path) return KME_E_INVALID;
     const char* p = (*env)->GetStringUTFChars(env, path, NULL);
     if (!p) return KME_E_INVALID;
     const kme_status s = restore ? kme_restore(h->e, p) : kme_checkpoint(h->e, p);

@@ -60,6 +60,45 @@ struct Out {
 
 extern "C" {
 
+// The processor's MatchOut rows for records [0, n): IN (KP:97), per trade the maker fill then the
+// taker fill (executeTrade, KP:265-274), OUT (KP:124).  Same order and values as kme_tape_json, as
+// binary rows the JNI glue hands to Java (one Order per row) instead of text.
+kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
+                           size_t* n_rows) {
+    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
+    const size_t need = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
+    *n_rows = need;
+    if (need > cap) return KME_E_CAPACITY;
+    kme_row* w = rows;
+    for (uint32_t i = 0; i < n; ++i) {
+        const int32_t a = in->action[i], price = in->price[i];
+        const int64_t oid = in->oid[i], aid = in->aid[i], sid = in->sid[i];
+        kme_row x;
+        std::memset(&x, 0, sizeof x);
+        x.oid = oid; x.aid = aid; x.sid = sid; x.action = a; x.price = price; x.size = in->size[i]; x.kind = 0;
+        *w++ = x;
+        const bool taker_buy = a == KME_BUY;
+        for (uint32_t t = r->trade_off[i]; t < r->trade_off[i + 1]; ++t) {
+            const kme_trade& tr = r->trades[t];
+            x.kind = 1; x.prev = 0; x.has_prev = 0;
+            x.action = taker_buy ? KME_SOLD : KME_BOUGHT;          // maker fill {oid, aid, sid, 0, size}
+            x.oid = tr.maker_oid; x.aid = tr.maker_aid; x.sid = tr.maker_sid; x.price = 0; x.size = tr.size;
+            *w++ = x;
+            x.action = taker_buy ? KME_BOUGHT : KME_SOLD;          // taker fill {.., price - maker price, size}
+            x.oid = oid; x.aid = aid; x.sid = sid;
+            x.price = (int32_t)((uint32_t)price - (uint32_t)tr.maker_price);
+            *w++ = x;
+        }
+        x.kind = 2;                                                // OUT: the mutated order
+        x.oid = oid; x.aid = aid; x.sid = sid; x.price = price;
+        x.action = r->out_action[i]; x.size = r->out_size[i];
+        x.has_prev = (r->out_flags[i] & KME_OUT_HAS_PREV) ? 1 : 0;
+        x.prev = x.has_prev ? r->out_prev[i] : 0;
+        *w++ = x;
+    }
+    return KME_OK;
+}
+
 kme_status kme_tape_json(const kme_orders* in, uint32_t n, const kme_epoch_result* r, char* buf, size_t cap, size_t* len) {
     if (!in || !r || !len) return KME_E_INVALID;
     Out o{buf, buf ? cap : 0, 0, {}};

@@ -452,7 +452,9 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
 
 // FUNDED per-account proof: balance >= lb_start - need - debits >= 0 >= any single risk remaining,
 // i.e. every checkBalance (KP:177) of this epoch passes.  Otherwise the epoch runs serially
-// (KME_FLAG_SERIAL_FALLBACK) or is refused as a whole (KME_E_UNFUNDED, no index).
+// (KME_FLAG_SERIAL_FALLBACK) or is refused as a whole: KME_E_UNFUNDED / KME_D_UNPROVEN raised at
+// index 0, the smallest error code there is, so no indexed fault raised elsewhere in the epoch can
+// replace it and err_limit lets no record of the epoch take effect.
 __global__ void k_check_funded(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
@@ -461,19 +463,25 @@ __global__ void k_check_funded(DevState S, EpochIO io) {
     const int64_t lbs = S.acct_since[a] < io.seq_base ? S.acct_lb[a] : 0;
     if (lbs - need - S.acct_negx[a] < 0) {
         if (S.fallback) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull);   // k_serial takes the epoch
-        else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_NONE, -1);
+        else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_UNPROVEN, 0);
     }
 }
 // The bounds roll forward once the whole proof is in (a kernel boundary after k_check_funded):
-// lb = lb_start - need + transfers.  An epoch refused as a whole by the proof changes no bound
-// (nothing of it takes effect, so the caller can resubmit it: KME_E_UNFUNDED is not fatal).
+// lb = lb_start - need + transfers.  An epoch none of whose records takes effect (refused by the
+// proof, or faulting at its first record) changes no bound, and the accounts its CREATE_BALANCE
+// records created (k_ledger_funded, for the acct_ok of the epoch's later orders) are absent again:
+// nothing of it took effect, so the caller can resubmit it (KME_E_UNFUNDED is not fatal).
 __global__ void k_commit_funded(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
+    const unsigned long long c = S.ctr[ci(C_ERR)];
+    const bool refused = c != ~0ull && (c >> 16) == 0;
+    if (refused && S.ctr[ci(C_ACCT_OPS)] != 0) {
+        const int64_t since = S.acct_since[a];
+        if (since >= io.seq_base && since < io.seq_base + (int64_t)io.n) { S.acct_since[a] = INT64_MAX; S.acct_lb[a] = 0; }
+    }
     const int64_t need = S.acct_need[a], negx = S.acct_negx[a], xfer = S.acct_xfer[a];
     if (need == 0 && negx == 0 && xfer == 0) return;
-    const unsigned long long c = S.ctr[ci(C_ERR)];
-    const bool refused = c != ~0ull && (c & 0xFF) == KME_E_UNFUNDED && (c >> 16) == 0xFFFFFFFFFFFFull;
     const int64_t since = S.acct_since[a];
     if (!refused && since < io.seq_base + (int64_t)io.n) S.acct_lb[a] = (since < io.seq_base ? S.acct_lb[a] : 0) - need + xfer;
     S.acct_need[a] = 0; S.acct_negx[a] = 0; S.acct_xfer[a] = 0;
@@ -2927,6 +2935,15 @@ __global__ void k_epoch_reset(DevState S) {
         S.ctr[ci(k)] = 0ull;
 }
 
+// ------------------------------------------------------------------ host epochs: trades to the host
+// kme_submit_epoch_host: the epoch's trades, whose count only the device knows (trade_off[n]), copied
+// into the caller's registered host buffer through its device mapping (16-B stores, coalesced, each
+// lane one half of a 32-B record), on the copy stream beside the next epoch's kernels.
+__global__ void __launch_bounds__(256) k_export_trades(const int4* src, const uint32_t* count, uint32_t cap, int4* dst) {
+    const uint32_t n = *count < cap ? *count : cap;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < 2 * n; k += gridDim.x * blockDim.x) dst[k] = src[k];
+}
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
@@ -3023,6 +3040,10 @@ void launch_tob(const DevState& S, void* out, hipStream_t st) {
 void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_tob_groups, dim3(cdiv(n, 256)), dim3(256), 0, st, S, groups, n, (kme_tob*)out);
+}
+void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st) {
+    hipLaunchKernelGGL(k_export_trades, dim3(128), dim3(256), 0, st, reinterpret_cast<const int4*>(src), count, cap,
+                       reinterpret_cast<int4*>(dst_mapped));
 }
 void launch_init_state(const DevState& S, hipStream_t st) {
     const uint32_t n = (uint32_t)(S.G > S.A ? S.G : S.A);

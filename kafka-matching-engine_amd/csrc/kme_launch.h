@@ -48,5 +48,7 @@ void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st)
 void launch_tob(const DevState& S, void* out, hipStream_t st);
 void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st);
 void launch_init_state(const DevState& S, hipStream_t st);
+// host epochs (kme_submit_epoch_host): trades[0, min(trade_off[n], cap)) into device-mapped host memory
+void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st);
 
 }  // namespace kme

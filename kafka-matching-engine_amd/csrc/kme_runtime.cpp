@@ -76,6 +76,24 @@ struct kme_engine {
     bool ev_used[2][PH_N] = {};
     float phase_ms[KME_MAX_PHASES] = {};
     uint64_t otab_cap = 0;
+    // host epochs (kme_submit_epoch_host): two slots of device-side inputs and results, a copy stream
+    // each way (allocated at the first host epoch)
+    struct HostSlot {
+        int32_t *action, *price, *size;
+        int64_t *oid, *aid, *sid;
+        int32_t *out_action, *out_size;
+        int64_t* out_prev;
+        uint8_t* out_flags;
+        uint32_t* trade_off;
+        TradeRec* trades;
+    };
+    HostSlot hs[2] = {};
+    bool hs_ready = false;
+    hipStream_t in_stream = nullptr, out_stream = nullptr;
+    hipEvent_t ev_in[2] = {};
+    bool host_epoch[2] = {};              // the epoch of this slot is a host epoch
+    bool host_mapped[2] = {};             // its trades go out through the device mapping (k_export_trades)
+    kme_epoch_result host_out[2] = {};    // the caller's result buffers of that epoch
 };
 
 #define HIP_TRY(x)                                                                          \
@@ -140,7 +158,8 @@ const char* kme_domain_str(int d) {
                                   "resting price outside 0..126", "duplicate live oid", "FUNDED price/size range",
                                   "sentinel oid", "order pool full", "oid table full", "trade buffer full",
                                   "symbol id >= max_symbols", "account id >= max_accounts", "ledger table full",
-                                  "epoch larger than max_epoch"};
+                                  "epoch larger than max_epoch",
+                                  "funded proof failed: the epoch as a whole was refused"};
     if (d < 0 || d >= (int)(sizeof(names) / sizeof(names[0]))) return "unknown";
     return names[d];
 }
@@ -316,6 +335,11 @@ kme_status kme_destroy(kme_engine* e) {
     for (auto& evs : e->ev)
         for (auto& ev : evs) if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : e->ev_end) if (ev) (void)hipEventDestroy(ev);
+    if (e->in_stream) (void)hipStreamSynchronize(e->in_stream);
+    if (e->out_stream) (void)hipStreamSynchronize(e->out_stream);
+    for (auto& ev : e->ev_in) if (ev) (void)hipEventDestroy(ev);
+    if (e->in_stream) (void)hipStreamDestroy(e->in_stream);
+    if (e->out_stream) (void)hipStreamDestroy(e->out_stream);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->lane_stream) (void)hipStreamDestroy(e->lane_stream);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -453,6 +477,15 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     HIP_TRY(hipEventSynchronize(e->ev_end[slot]));
     --e->inflight;
     const uint32_t last_n = e->fl_n[slot];
+    bool host_overflow = false;
+    if (e->host_epoch[slot]) {   // kme_submit_epoch_host: its results have landed in the caller's buffers
+        e->host_epoch[slot] = false;
+        const kme_epoch_result& ho = e->host_out[slot];
+        const uint32_t nt = ho.trade_off[last_n];
+        host_overflow = nt > ho.trades_cap;
+        if (!e->host_mapped[slot] && nt && !host_overflow)   // trades buffer not registered: copy them now
+            HIP_TRY(hipMemcpy(ho.trades, e->hs[slot].trades, (size_t)nt * sizeof(kme_trade), hipMemcpyDeviceToHost));
+    }
     const unsigned long long* c = e->h_ctr + slot * (size_t)C_NCTR * CTR_STRIDE;
     s.n_inputs = last_n;
     s.n_trades = (uint32_t)c[ci(C_TRADES)];
@@ -464,13 +497,19 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_effective = last_n;
     e->last_busy = c[ci(C_BUSY)];
     e->last_light = c[ci(C_LIGHT)];
-    if (c[ci(C_ERR)] != ~0ull) {
+    if (host_overflow && c[ci(C_ERR)] == ~0ull) {   // the caller's trades buffer is too small for the epoch
+        s.status = KME_E_CAPACITY; s.detail = KME_D_CAP_TRADES; s.n_effective = 0;
+        e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_TRADES;
+    } else if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
         const uint64_t ix = c[ci(C_ERR)] >> 16;
-        s.error_index = ix == 0xFFFFFFFFFFFFull ? -1 : (int64_t)ix;
+        // (KME_D_UNPROVEN: the funded proof refused the epoch as a whole, raised at index 0 so that
+        // no indexed fault replaces it; reported without an index)
+        s.error_index = (ix == 0xFFFFFFFFFFFFull || s.detail == KME_D_UNPROVEN) ? -1 : (int64_t)ix;
         // the records before the fault took effect (their results are valid), none after it
         s.n_effective = s.error_index < 0 ? 0u : (uint32_t)std::min<int64_t>(s.error_index, last_n);
+        if (s.detail == KME_D_UNPROVEN) s.n_effective = 0;
         if (s.status == KME_E_UNFUNDED && e->inflight == 0) {
             // not fatal: the refused records changed nothing, so their sequence numbers are
             // handed out again when they are resubmitted
@@ -509,6 +548,104 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     if (st) *st = s;
     return (kme_status)s.status;
 }
+
+kme_status kme_poll(kme_engine* e, int* done) {
+    if (!e || !done) return KME_E_INVALID;
+    if (e->inflight == 0) { *done = 1; return KME_OK; }
+    const int slot = (int)((e->sub_count - (uint32_t)e->inflight) & 1);   // the older epoch in flight
+    const hipError_t q = hipEventQuery(e->ev_end[slot]);
+    if (q == hipSuccess) { *done = 1; return KME_OK; }
+    if (q == hipErrorNotReady) { (void)hipGetLastError(); *done = 0; return KME_OK; }
+    return KME_E_HIP;
+}
+
+kme_status kme_host_register(kme_engine* e, void* host, size_t bytes) {
+    if (!e || !host || !bytes) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    const hipError_t r = hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (r == hipErrorHostMemoryAlreadyRegistered) { (void)hipGetLastError(); return KME_OK; }
+    HIP_TRY(r);
+    return KME_OK;
+}
+
+kme_status kme_host_unregister(kme_engine* e, void* host) {
+    if (!e || !host) return KME_E_INVALID;
+    if (e->inflight) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipHostUnregister(host));
+    return KME_OK;
+}
+
+static kme_status host_slots(kme_engine* e) {
+    if (e->hs_ready) return KME_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&e->in_stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->out_stream, hipStreamNonBlocking));
+    for (auto& ev : e->ev_in) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const size_t E = e->cfg.max_epoch;
+    for (auto& h : e->hs) {
+        kme_status r = KME_OK;
+        if ((r = dalloc(e, &h.action, E)) || (r = dalloc(e, &h.price, E)) || (r = dalloc(e, &h.size, E)) ||
+            (r = dalloc(e, &h.oid, E)) || (r = dalloc(e, &h.aid, E)) || (r = dalloc(e, &h.sid, E)) ||
+            (r = dalloc(e, &h.out_action, E)) || (r = dalloc(e, &h.out_size, E)) || (r = dalloc(e, &h.out_prev, E)) ||
+            (r = dalloc(e, &h.out_flags, E)) || (r = dalloc(e, &h.trade_off, E + 1)) ||
+            (r = dalloc(e, &h.trades, (size_t)e->cfg.max_trades)))
+            return r;
+    }
+    e->hs_ready = true;
+    return KME_OK;
+}
+
+kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
+    if (!e || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
+        (!out->trades && out->trades_cap))
+        return KME_E_INVALID;
+    if (e->failed) return KME_E_FAILED;
+    if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
+    if (e->inflight == 2) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    if (kme_status r = host_slots(e)) return r;
+    const int slot = (int)(e->sub_count & 1);   // = submit()'s slot
+    const auto& h = e->hs[slot];
+    hipStream_t si = e->in_stream, so = e->out_stream;
+    // inputs: PCIe while the engine stream still runs the previous epoch's kernels
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(h.action, in->action, n * sizeof(int32_t), hipMemcpyHostToDevice, si));
+        HIP_TRY(hipMemcpyAsync(h.oid, in->oid, n * sizeof(int64_t), hipMemcpyHostToDevice, si));
+        HIP_TRY(hipMemcpyAsync(h.aid, in->aid, n * sizeof(int64_t), hipMemcpyHostToDevice, si));
+        HIP_TRY(hipMemcpyAsync(h.sid, in->sid, n * sizeof(int64_t), hipMemcpyHostToDevice, si));
+        HIP_TRY(hipMemcpyAsync(h.price, in->price, n * sizeof(int32_t), hipMemcpyHostToDevice, si));
+        HIP_TRY(hipMemcpyAsync(h.size, in->size, n * sizeof(int32_t), hipMemcpyHostToDevice, si));
+    }
+    HIP_TRY(hipEventRecord(e->ev_in[slot], si));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_in[slot], 0));
+    const kme_orders din{h.action, h.oid, h.aid, h.sid, h.price, h.size};
+    const kme_epoch_result dres{h.out_action, h.out_size, h.out_prev, h.out_flags, h.trade_off,
+                                reinterpret_cast<kme_trade*>(h.trades), e->cfg.max_trades};
+    if (kme_status r = submit(e, &din, n, &dres)) return r;
+    // results: behind the kernels (ev_end of this slot), on the other copy stream
+    HIP_TRY(hipStreamWaitEvent(so, e->ev_end[slot], 0));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(out->out_action, h.out_action, n * sizeof(int32_t), hipMemcpyDeviceToHost, so));
+        HIP_TRY(hipMemcpyAsync(out->out_size, h.out_size, n * sizeof(int32_t), hipMemcpyDeviceToHost, so));
+        HIP_TRY(hipMemcpyAsync(out->out_prev, h.out_prev, n * sizeof(int64_t), hipMemcpyDeviceToHost, so));
+        HIP_TRY(hipMemcpyAsync(out->out_flags, h.out_flags, n * sizeof(uint8_t), hipMemcpyDeviceToHost, so));
+    }
+    HIP_TRY(hipMemcpyAsync(out->trade_off, h.trade_off, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, so));
+    void* mapped = nullptr;
+    e->host_mapped[slot] = out->trades_cap && hipHostGetDevicePointer(&mapped, out->trades, 0) == hipSuccess && mapped;
+    if (!e->host_mapped[slot]) (void)hipGetLastError();
+    else launch_export_trades(h.trades, h.trade_off + n, out->trades_cap, reinterpret_cast<TradeRec*>(mapped), so);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_end[slot], so));   // kme_poll / kme_wait: the results have landed
+    e->host_epoch[slot] = true;
+    e->host_out[slot] = *out;
+    return KME_OK;
+}
+
+#ifndef KME_SRC_HASH
+#define KME_SRC_HASH "unknown"
+#endif
+const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
 namespace {
@@ -554,7 +691,9 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    if (ctr[ci(C_ERR)] != ~0ull) return KME_E_FAILED;   // the last epoch faulted: its state is not a checkpoint
+    // the last epoch faulted: its state is not a checkpoint (an epoch refused with KME_E_UNFUNDED
+    // changed nothing: the engine's state is the one before it)
+    if (ctr[ci(C_ERR)] != ~0ull && (ctr[ci(C_ERR)] & 0xFF) != KME_E_UNFUNDED) return KME_E_FAILED;
     CkptHeader h{};
     std::memcpy(h.magic, kCkptMagic, sizeof h.magic);
     h.cfg = e->cfg;

@@ -26,7 +26,7 @@ MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
           7: "FAILED"}
-ABI_VERSION = 4
+ABI_VERSION = 5
 FLAG_EXACT_LEDGER = 1
 FLAG_SERIAL_FALLBACK = 2   # FUNDED: an epoch whose funded proof fails runs serially (needs FLAG_EXACT_LEDGER)
 
@@ -72,6 +72,7 @@ EXPORTS = [
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
+    "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_build_id",
 ]
 
 _lib = None
@@ -134,6 +135,13 @@ def lib():
         "kme_router_route": (st, [vp, C.POINTER(kme_orders), u32, vp]),
         "kme_router_split": (st, [vp, C.POINTER(kme_orders), u32, vp, vp, vp, vp]),
         "kme_router_directory_size": (C.c_uint64, [vp]),
+        "kme_host_register": (st, [vp, vp, C.c_size_t]),
+        "kme_host_unregister": (st, [vp, vp]),
+        "kme_submit_epoch_host": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result)]),
+        "kme_poll": (st, [vp, C.POINTER(C.c_int)]),
+        "kme_expand_rows": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
+                                 C.POINTER(C.c_size_t)]),
+        "kme_build_id": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -157,6 +165,7 @@ class KmeError(RuntimeError):
         super().__init__(msg)
         self.status, self.detail = status, detail
         self.index = st.error_index if st is not None else -1
+        self.n_effective = int(st.n_effective) if st is not None else 0
 
 
 def _np_ptr(a: np.ndarray):
@@ -271,6 +280,34 @@ class Engine:
         rc = self._L.kme_submit_epoch_device(self._h, C.byref(s), n, C.byref(r) if r is not None else None)
         if rc:
             raise KmeError(rc, "kme_submit_epoch_device")
+
+    # ---- host epochs at rate (kme_submit_epoch_host / kme_poll): numpy arrays registered once
+    def host_register(self, arr: np.ndarray):
+        rc = self._L.kme_host_register(self._h, C.c_void_p(arr.ctypes.data), arr.nbytes)
+        if rc:
+            raise KmeError(rc, "kme_host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        rc = self._L.kme_host_unregister(self._h, C.c_void_p(arr.ctypes.data))
+        if rc:
+            raise KmeError(rc, "kme_host_unregister")
+
+    def submit_host(self, cols: dict, n: int, out: "EpochResult"):
+        """cols: the six input columns (numpy, registered); out: an EpochResult whose arrays receive the
+        results at wait()."""
+        s = kme_orders(*[C.c_void_p(cols[k].ctypes.data) for k in ("action", "oid", "aid", "sid", "price", "size")])
+        r = kme_epoch_result(_np_ptr(out.out_action), _np_ptr(out.out_size), _np_ptr(out.out_prev),
+                             _np_ptr(out.out_flags), _np_ptr(out.trade_off), _np_ptr(out.trades), len(out.trades))
+        rc = self._L.kme_submit_epoch_host(self._h, C.byref(s), n, C.byref(r))
+        if rc:
+            raise KmeError(rc, "kme_submit_epoch_host")
+
+    def poll(self) -> bool:
+        done = C.c_int(0)
+        rc = self._L.kme_poll(self._h, C.byref(done))
+        if rc:
+            raise KmeError(rc, "kme_poll")
+        return bool(done.value)
 
     def wait(self) -> kme_epoch_status:
         st = kme_epoch_status()
@@ -426,6 +463,39 @@ def order_from_json(value: str):
     if rc:
         raise KmeError(rc, "kme_order_from_json")
     return (a.value, o.value, ai.value, s.value, p.value, z.value)
+
+
+ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
+                      ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
+assert ROW_DTYPE.itemsize == 48   # kme_row
+
+
+def new_result(n: int, trades_cap: int) -> EpochResult:
+    """Result arrays of an n-record epoch (page-aligned, so that kme_host_register pins only them)."""
+    def arr(count, dt):
+        dt = np.dtype(dt)
+        raw = np.zeros(count * dt.itemsize + 4096, np.uint8)
+        off = (-raw.ctypes.data) % 4096
+        return raw[off:off + count * dt.itemsize].view(dt)
+    return EpochResult(arr(n, np.int32), arr(n, np.int32), arr(n, np.int64), arr(n, np.uint8), arr(n + 1, np.uint32),
+                       arr(trades_cap, TRADE_DTYPE), kme_epoch_status())
+
+
+def expand_rows(orders: Orders, res: EpochResult, n: int | None = None) -> np.ndarray:
+    """kme_expand_rows: the MatchOut rows (ROW_DTYPE) of records [0, n) -- IN, fills, OUT."""
+    L = lib()
+    n = len(orders) if n is None else n
+    s, keep = _soa(orders)
+    r = kme_epoch_result(_np_ptr(res.out_action), _np_ptr(res.out_size), _np_ptr(res.out_prev),
+                         _np_ptr(res.out_flags), _np_ptr(res.trade_off), _np_ptr(res.trades), len(res.trades))
+    need = C.c_size_t(0)
+    L.kme_expand_rows(C.byref(s), n, C.byref(r), None, 0, C.byref(need))
+    rows = np.zeros(need.value, ROW_DTYPE)
+    rc = L.kme_expand_rows(C.byref(s), n, C.byref(r), C.c_void_p(rows.ctypes.data), len(rows), C.byref(need))
+    if rc:
+        raise KmeError(rc, "kme_expand_rows")
+    del keep
+    return rows
 
 
 def tape_json_from(orders: Orders, res: EpochResult) -> str:

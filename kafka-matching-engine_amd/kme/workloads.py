@@ -263,11 +263,14 @@ def shard_symbols(n_symbols: int, n_shards: int, shard: int, sid_base: int = 1) 
 
 def uniform(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: int = 1,
             sid_base: int = 1, aid_base: int = 0, oid_base: int = 1, price_lo: int = 30,
-            price_hi: int = 75, mix=(0.34, 0.33, 0.33), symbols: np.ndarray | None = None) -> Orders:
+            price_hi: int = 75, mix=(0.34, 0.33, 0.33), symbols: np.ndarray | None = None,
+            cancels: str = "uniform") -> Orders:
     """C2/C3: 34/33/33 BUY/SELL/CANCEL, sid uniform, price uniform [30,75] (the
     H5-safe band), size floor(N(50,10)) clamped to [1,100], cancels of an earlier oid of the same
     account.  ``symbols``: draw sids uniformly from this set instead of sid_base + [0, n_symbols)
-    (a murmur2 shard of a larger universe, ``shard_symbols``); the same draws otherwise."""
+    (a murmur2 shard of a larger universe, ``shard_symbols``); the same draws otherwise.
+    ``cancels="live"``: each cancel instead takes its account's most recent order that still rests
+    (``live_cancels``), so cancels hit the book the way a trader's do."""
     rng = np.random.Generator(np.random.PCG64(seed))
     u = rng.random(n_orders)
     action = np.where(u < mix[0], BUY, np.where(u < mix[0] + mix[1], SELL, CANCEL)).astype(np.int32)
@@ -285,7 +288,12 @@ def uniform(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: 
     sid = np.where(is_can, 0, sid)
     price = np.where(is_can, 0, price).astype(np.int32)
     size = np.where(is_can, 0, size).astype(np.int32)
-    return Orders(action, oid, aid, sid, price, size, np.zeros(n_orders, bool))
+    o = Orders(action, oid, aid, sid, price, size, np.zeros(n_orders, bool))
+    if cancels == "live":
+        live_cancels(o, aid_base + n_accounts)
+    elif cancels != "uniform":
+        raise ValueError(cancels)
+    return o
 
 
 def zipf(n_orders: int, n_symbols: int = 65536, n_accounts: int = 65536, s: float = 1.1,
@@ -312,47 +320,94 @@ def zipf(n_orders: int, n_symbols: int = 65536, n_accounts: int = 65536, s: floa
     return o
 
 
+_GEN = None
+
+
+def _gen():
+    """libkme_workload.so (csrc/kme_workload.c, built with libkme): the book replay that picks cancel
+    targets that still rest.  Workload generation only."""
+    global _GEN
+    if _GEN is None:
+        import ctypes as C
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkme_workload.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not built (make -C kafka-matching-engine_amd/csrc)")
+        L = C.CDLL(path)
+        P = C.c_void_p
+        L.kme_gen_live_cancels.argtypes = [C.c_uint32, P, P, P, P, P, P, C.c_uint32, C.c_uint32]
+        L.kme_gen_live_cancels.restype = C.c_int
+        L.kme_gen_cancel_replace.argtypes = [C.c_uint32] + [P] * 8 + [C.c_uint32] * 3 + [C.c_double] + [P] * 6
+        L.kme_gen_cancel_replace.restype = C.c_int64
+        _GEN = L
+    return _GEN
+
+
+def live_cancels(o: Orders, n_accounts: int) -> Orders:
+    """Every CANCEL row of `o` re-targeted at its account's most recent order that still rests when
+    the cancel arrives (0 when the account has none), by replaying the stream through a plain
+    price-time book (kme_workload.c).  In place; returns `o`."""
+    import ctypes as C
+
+    L = _gen()
+    a = np.ascontiguousarray(o.action, np.int32)
+    ai = np.ascontiguousarray(o.aid, np.int64)
+    si = np.ascontiguousarray(o.sid, np.int64)
+    pr = np.ascontiguousarray(o.price, np.int32)
+    sz = np.ascontiguousarray(o.size, np.int32)
+    oid = np.array(o.oid, np.int64, copy=True)
+    max_sid = int(np.abs(si).max()) if len(si) else 0
+    ptr = lambda x: C.c_void_p(x.ctypes.data)
+    rc = L.kme_gen_live_cancels(len(o), ptr(a), ptr(ai), ptr(si), ptr(pr), ptr(sz), ptr(oid), n_accounts, max_sid)
+    if rc:
+        raise RuntimeError("kme_gen_live_cancels failed")
+    o.oid = oid
+    return o
+
+
 def cancel_replace(n_orders: int, n_symbols: int = 1024, n_accounts: int = 4096, seed: int = 1,
-                   sid_base: int = 1, aid_base: int = 0, oid_base: int = 1) -> Orders:
-    """C5: 45% (CANCEL, new order of the same account) pairs = 90% of records, and 10% large
-    marketable orders (BUY@75 / SELL@30, size 5,000-50,000) that sweep many levels."""
+                   sid_base: int = 1, aid_base: int = 0, oid_base: int = 1, quotes: int = 4,
+                   sweep_frac: float = 0.4) -> Orders:
+    """C5: 45% (CANCEL, new order of the same account) pairs = 90% of records, and 10%
+    large marketable orders (BUY at 75 / SELL at 30) that sweep many levels.
+
+    Cancel/replace as a quoting account does it: every account keeps ``quotes`` quotes and replaces
+    them in turn -- the CANCEL takes the quote being replaced (a live order unless a sweep filled
+    it), and the new quote goes in at a passive price near the touch (BUY up to 10 ticks under
+    min(best ask - 1, mid), SELL likewise over max(best bid + 1, mid); clamped to [30, 75]; size
+    floor(N(50, 10)) in [1, 100]), so the books hold ~quotes x accounts / symbols orders.  A
+    sweep's size is drawn from 5,000-50,000 and capped at ``sweep_frac`` of the opposite side's
+    quantity within its limit, so it clears the best levels without resting a remainder that would
+    pin the book.  Flow balance bounds the sweeps: 45% of the records add a quote and 10% sweep, so a
+    sweep takes ~(1 - cancel success) x 4.5 quotes on average; the defaults give ~55-60% successful
+    cancels (SURVEY §8d C5's churn) and a steady book.  The book replay that places them is
+    kme_workload.c (workload generation only)."""
+    import ctypes as C
+
     rng = np.random.Generator(np.random.PCG64(seed))
     n_pairs = int(n_orders * 0.45)
-    n_big = n_orders - 2 * n_pairs
-    # background book: build with plain limit orders first, then the churn
+    n_big = max(0, n_orders - 2 * n_pairs)
     n_units = n_pairs + n_big
-    kind = rng.permutation(np.r_[np.zeros(n_pairs, np.int8), np.ones(n_big, np.int8)])
-    n = n_pairs * 2 + n_big
-    action = np.empty(n, np.int32)
-    aid = np.empty(n, np.int64)
-    sid = np.zeros(n, np.int64)
-    price = np.zeros(n, np.int32)
-    size = np.zeros(n, np.int32)
-    unit_len = np.where(kind == 0, 2, 1)
-    start = np.r_[0, np.cumsum(unit_len)[:-1]]
-    ua = rng.integers(0, n_accounts, n_units).astype(np.int64) + aid_base
-    us = rng.integers(0, n_symbols, n_units).astype(np.int64) + sid_base
-    side = np.where(rng.random(n_units) < 0.5, BUY, SELL).astype(np.int32)
-    pp = start[kind == 0]
-    # cancel/replace pair: CANCEL then a fresh limit order from the same account
-    action[pp] = CANCEL
-    aid[pp] = ua[kind == 0]
-    action[pp + 1] = side[kind == 0]
-    aid[pp + 1] = ua[kind == 0]
-    sid[pp + 1] = us[kind == 0]
-    price[pp + 1] = rng.integers(30, 76, n_pairs)
-    size[pp + 1] = np.clip(np.floor(rng.normal(50, 10, n_pairs)), 1, 100)
-    bp = start[kind == 1]
-    bs = side[kind == 1]
-    action[bp] = bs
-    aid[bp] = ua[kind == 1]
-    sid[bp] = us[kind == 1]
-    price[bp] = np.where(bs == BUY, 75, 30)
-    size[bp] = rng.integers(5000, 50001, n_big)
-    oid = _unique_oids(n, oid_base)
-    is_can = action == CANCEL
-    oid = np.where(is_can, _cancel_targets(action, aid, oid, rng), oid)
-    return Orders(action, oid, aid, sid, price.astype(np.int32), size.astype(np.int32), np.zeros(n, bool))
+    kind = rng.permutation(np.r_[np.zeros(n_pairs, np.uint8), np.ones(n_big, np.uint8)])
+    acct = rng.integers(0, n_accounts, n_units).astype(np.int64) + aid_base
+    sym = rng.integers(0, n_symbols, n_units).astype(np.int64) + sid_base
+    is_sell = (rng.random(n_units) >= 0.5).astype(np.uint8)
+    u_price = rng.random(n_units)
+    qsize = np.clip(np.floor(rng.normal(50, 10, n_units)), 1, 100).astype(np.int32)
+    bsize = rng.integers(5000, 50001, n_units).astype(np.int32)
+    n = 2 * n_pairs + n_big
+    new_oid = _unique_oids(n_units, oid_base)
+    cols = Orders.empty(n)
+    L = _gen()
+    ptr = lambda x: C.c_void_p(x.ctypes.data)
+    rows = L.kme_gen_cancel_replace(n_units, ptr(kind), ptr(acct), ptr(sym), ptr(is_sell), ptr(u_price), ptr(qsize),
+                                    ptr(bsize), ptr(new_oid), aid_base + n_accounts, sid_base + n_symbols, quotes, sweep_frac,
+                                    ptr(cols.action), ptr(cols.aid), ptr(cols.sid), ptr(cols.price), ptr(cols.size),
+                                    ptr(cols.oid))
+    if rows != n:
+        raise RuntimeError(f"kme_gen_cancel_replace: {rows} rows, expected {n}")
+    return cols
 
 
 def funded_transfers_needed(n_orders: int, n_accounts: int, big: bool = False) -> int:

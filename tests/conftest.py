@@ -30,11 +30,43 @@ def oracle_mod():
     return oracle
 
 
+# the sources kme_build_id() hashes (kafka-matching-engine_amd/csrc/Makefile SRCS, same order)
+LIB_SOURCES = ["kme_kernels.hip", "kme_serialize.hip", "kme_runtime.cpp", "kme_host.cpp", "kme_processor.cpp",
+               "kme_router.cpp", "kme_device.h", "kme_launch.h", "kme_processor.hpp", "../../include/kme.h",
+               "../../include/kme_processor.h"]
+
+
+def source_hash() -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in LIB_SOURCES:
+        with open(os.path.join(PKG, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def built_id(path) -> str:
+    """kme_build_id() of a built libkme.so, read from the file (loading it here would pin that copy
+    in the process before a rebuild)."""
+    import re
+
+    with open(path, "rb") as fh:
+        data = fh.read()
+    want = source_hash().encode()
+    return want.decode() if want in data else (re.findall(rb"[0-9a-f]{16}", data) or [b"?"])[0].decode()
+
+
 @pytest.fixture(scope="session")
 def kme_mod():
-    if not os.path.exists(os.path.join(PKG, "kme", "libkme.so")):
+    """libkme.so built from THIS tree: rebuilt (make is incremental) when missing or when its
+    kme_build_id() differs from the sources' hash, so a test run never uses a stale library."""
+    so = os.path.join(PKG, "kme", "libkme.so")
+    if not os.path.exists(so) or built_id(so) != source_hash():
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(PKG, "csrc")], check=True)
     import kme
 
-    kme.lib()
+    L = kme.lib()
+    got = L.kme_build_id().decode()
+    assert got == source_hash(), f"libkme.so was built from other sources ({got} != {source_hash()})"
     return kme

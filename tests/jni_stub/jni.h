@@ -36,5 +36,7 @@ struct JNINativeInterface_ {
     jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
     const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
     void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
+    void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
+    jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
 };
 #endif

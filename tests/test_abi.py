@@ -153,3 +153,38 @@ def test_funded_capacity_bound_on_the_oid_table(kme_mod):
     with pytest.raises(kme_mod.KmeError) as e:
         kme_mod.Engine(cfg)
     assert e.value.status == 1                                   # KME_E_INVALID, before any device call
+
+
+def test_expand_rows_order_and_values(kme_mod):
+    """kme_expand_rows (the JNI glue's row expansion, host only): IN, per trade the maker fill then the
+    taker fill (executeTrade, KP:265-274), OUT with prev when set (KP:217)."""
+    import numpy as np
+
+    from kme import workloads as W
+
+    orders = W.Orders.from_rows([(W.SELL, 11, 1, 5, 40, 10), (W.BUY, 12, 2, 5, 45, 4), (W.BUY, 13, 3, 5, 30, 7)])
+    res = kme_mod.new_result(3, 4)
+    res.out_action[:] = [W.SELL, W.BUY, W.BUY]
+    res.out_size[:] = [10, 0, 7]
+    res.out_flags[:] = [0, 0, 1]
+    res.out_prev[:] = [0, 0, 99]
+    res.trade_off[:] = [0, 0, 1, 1]
+    res.trades[0] = (11, 1, -5, 40, 4)
+    rows = kme_mod.expand_rows(orders, res)
+    assert list(rows["kind"]) == [0, 2, 0, 1, 1, 2, 0, 2]
+    assert list(rows["action"]) == [W.SELL, W.SELL, W.BUY, W.SOLD, W.BOUGHT, W.BUY, W.BUY, W.BUY]
+    maker, taker = rows[3], rows[4]
+    assert (maker["oid"], maker["aid"], maker["sid"], maker["price"], maker["size"]) == (11, 1, -5, 0, 4)
+    assert (taker["oid"], taker["aid"], taker["sid"], taker["price"], taker["size"]) == (12, 2, 5, 5, 4)
+    assert rows[7]["has_prev"] == 1 and rows[7]["prev"] == 99 and rows[5]["has_prev"] == 0
+    # too small a buffer: nothing written, the count returned
+    import ctypes as C
+
+    L = kme_mod.lib()
+    s, keep = kme_mod._soa(orders)
+    r = kme_mod.kme_epoch_result(*[C.c_void_p(a.ctypes.data) for a in (res.out_action, res.out_size, res.out_prev,
+                                                                        res.out_flags, res.trade_off, res.trades)], 4)
+    need = C.c_size_t(0)
+    small = np.zeros(3, kme_mod.ROW_DTYPE)
+    assert L.kme_expand_rows(C.byref(s), 3, C.byref(r), C.c_void_p(small.ctypes.data), 3, C.byref(need)) == 2
+    assert need.value == 8 and not small["oid"].any()

@@ -234,3 +234,101 @@ def test_checkpoint_refuses_failed_or_pending_epochs(kme_mod, tmp_path):
     assert kme_mod.STATUS[ke.value.status] == "INVALID"
     eng.wait()
     eng.checkpoint(tmp_path / "ok.ckpt")
+
+
+def _device_cols(orders):
+    import torch
+
+    cols = {k: torch.from_numpy(np.ascontiguousarray(getattr(orders, k))).cuda()
+            for k in ("action", "oid", "aid", "sid", "price", "size")}
+    return cols, {k: t.data_ptr() for k, t in cols.items()}
+
+
+def _unprovable(n_sym=16, n_acc=8):
+    """Setup funded with 200,000 per account, then an order stream of ~375 orders per account that
+    the per-account proof cannot hold, and the top-up that makes it provable."""
+    setup = W.Orders.from_rows([r for a in range(n_acc) for r in ((W.CREATE_BALANCE, 0, a, 0, 0, 0),
+                                                                  (W.TRANSFER, 0, a, 0, 0, 200_000))]
+                               + [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)])
+    big = W.uniform(3000, n_symbols=n_sym, n_accounts=n_acc, seed=2, oid_base=10_000)
+    topup = W.Orders.from_rows([(W.TRANSFER, 0, a, 0, 0, 2_000_000_000) for a in range(n_acc)])
+    return setup, big, topup
+
+
+@pytest.mark.parametrize("light_max", [0, 1 << 30])
+def test_unproven_epoch_outranks_an_indexed_fault(kme_mod, oracle_mod, light_max):
+    """Advisor (round 2): an epoch whose funded proof fails AND that holds an indexed fault further
+    on (here FUNDED_RANGE) is refused as a whole -- no record of it is matched on an unproven
+    ledger.  After the top-up the same records run up to the fault, as the reference would."""
+    n_sym, n_acc = 16, 8
+    setup, big, topup = _unprovable(n_sym, n_acc)
+    i = 1700
+    bad = _inject(big, i, (W.BUY, 99_999_999, 3, 5, 101, 3))
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=n_acc, light_max=light_max))
+    got = eng.process(setup).tape_json(setup)
+    books = eng.snapshot_books()
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(bad)
+    assert kme_mod.STATUS[ke.value.status] == "UNFUNDED" and ke.value.detail == 18   # KME_D_UNPROVEN
+    assert ke.value.index == -1 and ke.value.n_effective == 0
+    assert eng.snapshot_books() == books
+    got += eng.process(topup).tape_json(topup)
+    with pytest.raises(kme_mod.KmeError) as ke2:
+        eng.process(bad)
+    assert kme_mod.STATUS[ke2.value.status] == "DOMAIN" and ke2.value.detail == 9 and ke2.value.index == i
+    got += ke2.value.result.tape_json(bad.slice(0, i))
+    o = oracle_mod.Oracle()
+    for part in (setup, topup, bad.slice(0, i)):
+        o.process(part)
+    assert got == o.tape_text()
+
+
+def test_refused_mixed_device_epoch_leaves_no_account(kme_mod, oracle_mod):
+    """Advisor (round 2): a device epoch mixing account records with orders (not split like host
+    epochs) that the proof refuses must not leave its CREATE_BALANCE behind: after the documented
+    top-up the resubmitted epoch creates the account, as the reference does."""
+    import torch
+
+    n_sym = 16
+    setup, big, topup = _unprovable(n_sym, 7)                 # accounts 0..6; account 7 absent
+    new_acct = W.Orders.from_rows([(W.CREATE_BALANCE, 0, 7, 0, 0, 0), (W.TRANSFER, 0, 7, 0, 0, 5000)])
+    mixed = W.Orders.concat([new_acct, big])
+    topup = W.Orders.concat([topup, W.Orders.from_rows([(W.TRANSFER, 0, 7, 0, 0, 1000)])])
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=8))
+    got = eng.process(setup).tape_json(setup)
+    cols, ptrs = _device_cols(mixed)
+    eng.submit_device(ptrs, len(mixed))
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.wait()
+    assert kme_mod.STATUS[ke.value.status] == "UNFUNDED" and ke.value.n_effective == 0
+    got += eng.process(topup).tape_json(topup)     # account 7 does not exist: its TRANSFER is rejected
+    eng.submit_device(ptrs, len(mixed))
+    eng.wait()
+    got += eng.tape_json_device(ptrs, len(mixed)).decode()
+    torch.cuda.synchronize()
+    o = oracle_mod.Oracle()
+    for part in (setup, topup, mixed):
+        o.process(part)
+    assert got == o.tape_text()
+    assert eng.snapshot_books() == o.dump_books()
+
+
+def test_checkpoint_after_an_unfunded_refusal(kme_mod, oracle_mod, tmp_path):
+    """Advisor (round 2): KME_E_UNFUNDED is not fatal, so the engine can be checkpointed right after
+    the refusal; a restored engine takes the top-up and the refused records like the original."""
+    n_sym, n_acc = 16, 8
+    setup, big, topup = _unprovable(n_sym, n_acc)
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=n_acc))
+    got = eng.process(setup).tape_json(setup)
+    with pytest.raises(kme_mod.KmeError):
+        eng.process(big)
+    ck = tmp_path / "after_refusal.ckpt"
+    eng.checkpoint(ck)
+    b = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=n_acc))
+    b.restore(ck)
+    got += b.process(topup).tape_json(topup) + b.process(big).tape_json(big)
+    o = oracle_mod.Oracle()
+    for part in (setup, topup, big):
+        o.process(part)
+    assert got == o.tape_text()
+    assert b.snapshot_books() == o.dump_books()

@@ -1,0 +1,199 @@
+"""The KP:52 drop-in's Java side (integration/jni/GpuMatchingEngine.java) against the reference's
+declarations.  There is no JDK in this image, so the file cannot be compiled here; instead every
+reference type and constructor it uses is checked against KProcessor.java's own declarations
+(tests/golden/kprocessor_api.json, extracted by tools/gen_kprocessor_api.py; re-extracted from
+/root/reference when it is present), and every native method against the JNI glue's exports.
+
+Round 2's file named `KProcessor.Order`, a class that does not exist: the reference's Order is a
+package-private top-level class (KP:449-475) and KProcessor nests only MatchingEngine (KP:63).
+"""
+import json
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JAVA = os.path.join(ROOT, "integration", "jni", "GpuMatchingEngine.java")
+JNI_C = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
+API = os.path.join(ROOT, "tests", "golden", "kprocessor_api.json")
+REF = "/root/reference/src/main/java/KProcessor.java"
+
+
+def _strip(src: str) -> str:
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", " ", src)
+    return re.sub(r'"(?:\\.|[^"\\])*"', '""', src)
+
+
+def _java():
+    with open(JAVA) as f:
+        return _strip(f.read())
+
+
+def _api():
+    with open(API) as f:
+        return json.load(f)
+
+
+def _call_args(src: str, start: int) -> list[str]:
+    """Top-level comma-separated arguments of the call whose '(' is at src[start]."""
+    depth, cur, out = 0, "", []
+    for ch in src[start:]:
+        if ch == "(":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch == ")":
+            depth -= 1
+            if depth == 0:
+                out.append(cur.strip())
+                return [a for a in out if a]
+        if ch == "," and depth == 1:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    raise AssertionError("unbalanced call")
+
+
+def test_fixture_matches_the_reference_source():
+    if not os.path.exists(REF):
+        pytest.skip("reference source not present (the committed fixture is used)")
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_kprocessor_api
+
+    with open(REF) as f:
+        assert gen_kprocessor_api.extract(f.read()) == _api()
+
+
+def test_order_is_the_reference_top_level_class():
+    api, src = _api(), _java()
+    o = api["order"]
+    assert o["top_level"] and not o["nested"]
+    assert "KProcessor.Order" not in src and "KProcessor." not in src
+    # Order is package-private in the reference's package: the processor must live in that package
+    pkg = re.search(r"^\s*package\s+([\w.]+)\s*;", src, flags=re.M)
+    assert (pkg.group(1) if pkg else "") == api["package"]
+    assert not o["public"]
+    # no import can bring in another Order
+    assert not re.search(r"import\s+[\w.]*\.Order\s*;", src)
+
+
+def test_processor_type_arguments_are_the_reference_ones():
+    api, src = _api(), _java()
+    p = api["processor"]
+    m = re.search(r"class\s+GpuMatchingEngine\s+implements\s+Processor\s*<\s*(\w+)\s*,\s*(\w+)\s*>", src)
+    assert m, "GpuMatchingEngine must implement Processor<K, V>"
+    assert (m.group(1), m.group(2)) == (p["key"], p["value"]) == ("String", "Order")
+    assert re.search(r"import\s+" + re.escape(p["interface"]) + r"\s*;", src)
+    # the Processor methods of kafka-streams 2.3 that MatchingEngine overrides (KP:86, 96, 129)
+    assert re.search(r"public\s+void\s+init\s*\(\s*ProcessorContext\s+\w+\s*\)", src)
+    assert re.search(r"public\s+void\s+process\s*\(\s*String\s+\w+\s*,\s*Order\s+\w+\s*\)", src)
+    assert re.search(r"public\s+void\s+close\s*\(\s*\)", src)
+
+
+def _expr_type(expr: str, locals_: dict) -> str:
+    """Java type of the simple expressions the processor passes to Order's constructor."""
+    expr = expr.strip()
+    m = re.fullmatch(r"\w+\.get(Int|Long)\(.*\)", expr)
+    if m:
+        return {"Int": "int", "Long": "long"}[m.group(1)]
+    m = re.fullmatch(r"\(\s*(int|long)\s*\).*", expr)
+    if m:
+        return m.group(1)
+    if expr in locals_:
+        return locals_[expr]
+    raise AssertionError(f"cannot type {expr!r}")
+
+
+def test_every_order_construction_matches_a_reference_constructor():
+    api, src = _api(), _java()
+    ctors = [tuple(c) for c in api["order"]["constructors"]]
+    calls = [m.end() - 1 for m in re.finditer(r"\bnew\s+Order\s*\(", src)]
+    assert calls, "the processor builds the forwarded Orders"
+    widen = {("int", "long"), ("int", "int"), ("long", "long")}
+    for at in calls:
+        args = _call_args(src, at)
+        types = [_expr_type(a, {}) for a in args]
+        ok = [c for c in ctors if len(c) == len(types) and all((t, p) in widen for t, p in zip(types, c))]
+        assert ok, f"new Order({', '.join(args)}): argument types {types} match no constructor {ctors}"
+
+
+def test_order_fields_used_exist_with_compatible_types():
+    api, src = _api(), _java()
+    fields = api["order"]["fields"]
+    # variables of type Order in the processor
+    names = set(re.findall(r"\bOrder\s+(\w+)\s*[=,)]", src))
+    assert names
+    used = re.findall(r"\b(" + "|".join(sorted(names)) + r")\.(\w+)\b", src)
+    assert used
+    for var, f in used:
+        assert f in fields, f"{var}.{f}: Order has no public field {f} (fields: {sorted(fields)})"
+    # reads of the six columns go to puts of the right width (KP:451-456)
+    for f, put in (("action", "putInt"), ("oid", "putLong"), ("aid", "putLong"), ("sid", "putLong"),
+                   ("price", "putInt"), ("size", "putInt")):
+        m = re.search(r"\.(put\w+)\([^;]*\b\w+\." + f + r"\)", src)
+        assert m and m.group(1) == put and fields[f] == {"putInt": "int", "putLong": "long"}[put], f
+    # the only field written is prev (Long, KP:458), from a long: boxing conversion
+    for var, f in re.findall(r"\b(\w+)\.(\w+)\s*=[^=]", src):
+        if var in names:
+            assert f == "prev" and fields[f] == "Long"
+
+
+_JNI_TYPES = {"int": "jint", "long": "jlong", "String": "jstring", "ByteBuffer": "jobject", "long[]": "jlongArray",
+              "void": "void"}
+
+
+def test_native_methods_match_the_jni_glue():
+    src = _java()
+    with open(JNI_C) as f:
+        c = f.read()
+    natives = re.findall(r"\bstatic\s+native\s+([\w\[\]]+)\s+(\w+)\s*\(([^)]*)\)\s*;", src)
+    assert {n for _, n, _ in natives} >= {"create", "destroy", "bind", "submit", "poll", "complete", "statusText",
+                                          "checkpoint", "restore"}
+    for ret, name, params in natives:
+        m = re.search(r"JNIEXPORT\s+(\w+)\s+JNICALL\s+Java_GpuMatchingEngine_" + name + r"\s*\(([^)]*)\)", c)
+        assert m, f"native {name} has no Java_GpuMatchingEngine_{name} in kme_jni.c"
+        jret, jparams = m.group(1), [p.strip() for p in m.group(2).split(",")]
+        assert jret == _JNI_TYPES[ret.replace("String", "String")] or (ret == "String" and jret == "jstring"), name
+        assert jparams[0].startswith("JNIEnv") and jparams[1].startswith("jclass"), name
+        jtypes = [p.split()[0] for p in jparams[2:]]
+        jtypes_java = [_JNI_TYPES[p.split()[0]] for p in params.split(",") if p.strip()]
+        assert jtypes == jtypes_java, f"{name}: Java {jtypes_java} vs C {jtypes}"
+
+
+def test_row_layout_matches_kme_row():
+    """GpuMatchingEngine reads kme_row (include/kme.h) at fixed offsets: oid 0, aid 8, sid 16, prev 24,
+    action 32, price 36, size 40, kind 44, has_prev 45, 48 bytes a row."""
+    import ctypes as C
+
+    class Row(C.Structure):
+        _fields_ = [("oid", C.c_int64), ("aid", C.c_int64), ("sid", C.c_int64), ("prev", C.c_int64),
+                    ("action", C.c_int32), ("price", C.c_int32), ("size", C.c_int32), ("kind", C.c_uint8),
+                    ("has_prev", C.c_uint8), ("_pad", C.c_uint8 * 2)]
+
+    assert C.sizeof(Row) == 48
+    with open(os.path.join(ROOT, "include", "kme.h")) as f:
+        h = f.read()
+    body = re.search(r"typedef struct kme_row \{(.*?)\} kme_row;", h, flags=re.S).group(1)
+    assert re.sub(r"/\*.*?\*/|\s+", "", body, flags=re.S) == \
+        "int64_toid,aid,sid;int64_tprev;int32_taction,price,size;uint8_tkind,has_prev;uint8_t_pad[2];"
+    src = _java()
+    assert "ROW_BYTES = 48" in src
+    m = re.search(r"new\s+Order\(r\.getInt\(b \+ 32\), r\.getLong\(b\), r\.getLong\(b \+ 8\), r\.getLong\(b \+ 16\),\s*"
+                  r"r\.getInt\(b \+ 36\), r\.getInt\(b \+ 40\)\)", src)
+    assert m, "Order(action, oid, aid, sid, price, size) from the row's offsets"
+    assert "r.get(b + 44)" in src and "r.get(b + 45)" in src and "r.getLong(b + 24)" in src
+
+
+def test_java_source_is_balanced():
+    src = _java()
+    for o, c in ("{}", "()", "[]"):
+        depth = 0
+        for ch in src:
+            depth += (ch == o) - (ch == c)
+            assert depth >= 0
+        assert depth == 0, o + c

@@ -2,10 +2,11 @@
 
 There is no JDK in this image, so libkme_jni_check.so is kme_jni.c built against
 tests/jni_stub/jni.h, and the JNIEnv it receives is a function table made here with ctypes: Java
-arrays are numpy arrays, exceptions are recorded.  The GPU tests run whole epochs through
-Java_GpuMatchingEngine_submit and compare the MatchOut rows it expands with the oracle's tape,
-record by record ("IN", maker fill, taker fill ..., "OUT"; KP:97, 265-274, 124), including the
-rows of the records before a fault.
+arrays and direct ByteBuffers are numpy arrays, exceptions are recorded.  The GPU tests drive the
+processor's own protocol -- bind two slots of direct buffers, submit an epoch per slot, poll,
+complete the oldest (kme_submit_epoch_host / kme_poll / kme_wait / kme_expand_rows) -- and compare
+the MatchOut rows with the oracle's tape record by record ("IN", maker fill, taker fill ..., "OUT";
+KP:97, 265-274, 124), including the rows of the records before a fault.
 """
 import ctypes as C
 import os
@@ -19,7 +20,10 @@ from kme import workloads as W
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
 CHECK_LIB = os.path.join(ROOT, "integration", "jni", "libkme_jni_check.so")
-SYMBOLS = ["create", "destroy", "submit", "statusText", "checkpoint", "restore"]
+SYMBOLS = ["create", "destroy", "bind", "submit", "poll", "complete", "statusText", "checkpoint", "restore"]
+ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
+                      ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
+assert ROW_DTYPE.itemsize == 48
 
 
 class FakeJni:
@@ -40,6 +44,8 @@ class FakeJni:
             ("NewStringUTF", C.CFUNCTYPE(P, P, C.c_char_p), lambda env, s: self._new(s.decode())),
             ("GetStringUTFChars", C.CFUNCTYPE(P, P, P, P), self._utf),
             ("ReleaseStringUTFChars", C.CFUNCTYPE(V, P, P, P), lambda env, s, p: None),
+            ("GetDirectBufferAddress", C.CFUNCTYPE(P, P, P), lambda env, b: self.objs[b].ctypes.data),
+            ("GetDirectBufferCapacity", C.CFUNCTYPE(L, P, P), lambda env, b: self.objs[b].nbytes),
         ]
 
         class Table(C.Structure):
@@ -69,6 +75,14 @@ class FakeJni:
     def arr(self, a):
         return self._new(np.ascontiguousarray(a))
 
+    def direct(self, nbytes, dtype):
+        """A direct ByteBuffer: page-aligned native memory, as ByteBuffer.allocateDirect gives."""
+        raw = np.zeros(nbytes + 4096, np.uint8)
+        off = (-raw.ctypes.data) % 4096
+        view = raw[off:off + nbytes].view(dtype)
+        self._keep.append(raw)
+        return self._new(view), view
+
 
 def _lib():
     if not os.path.exists(CHECK_LIB):
@@ -78,8 +92,14 @@ def _lib():
     lib.Java_GpuMatchingEngine_create.argtypes = [P, P, I, I, I, L, I, I, I, I]
     lib.Java_GpuMatchingEngine_create.restype = L
     lib.Java_GpuMatchingEngine_destroy.argtypes = [P, P, L]
-    lib.Java_GpuMatchingEngine_submit.argtypes = [P, P, L, I] + [P] * 16
+    lib.Java_GpuMatchingEngine_bind.argtypes = [P, P, L, I] + [P] * 7
+    lib.Java_GpuMatchingEngine_bind.restype = I
+    lib.Java_GpuMatchingEngine_submit.argtypes = [P, P, L, I, I]
     lib.Java_GpuMatchingEngine_submit.restype = I
+    lib.Java_GpuMatchingEngine_poll.argtypes = [P, P, L]
+    lib.Java_GpuMatchingEngine_poll.restype = I
+    lib.Java_GpuMatchingEngine_complete.argtypes = [P, P, L, I, P]
+    lib.Java_GpuMatchingEngine_complete.restype = I
     lib.Java_GpuMatchingEngine_statusText.argtypes = [P, P, I]
     lib.Java_GpuMatchingEngine_statusText.restype = P
     return lib
@@ -102,32 +122,47 @@ def test_jni_glue_exports_and_cpu_paths():
     assert j.thrown and "maxEpoch" in j.thrown[0]
 
 
-def _submit(lib, j, h, orders, max_trades):
-    n = len(orders)
-    rows = 2 * n + 2 * max_trades
-    outs = {"kind": np.zeros(rows, np.int8), "oAction": np.zeros(rows, np.int32), "oOid": np.zeros(rows, np.int64),
-            "oAid": np.zeros(rows, np.int64), "oSid": np.zeros(rows, np.int64), "oPrice": np.zeros(rows, np.int32),
-            "oSize": np.zeros(rows, np.int32), "oPrev": np.zeros(rows, np.int64), "oHasPrev": np.zeros(rows, np.int8),
-            "status": np.zeros(3, np.int64)}
-    ins = [j.arr(orders.action.astype(np.int32)), j.arr(orders.oid.astype(np.int64)), j.arr(orders.aid.astype(np.int64)),
-           j.arr(orders.sid.astype(np.int64)), j.arr(orders.price.astype(np.int32)), j.arr(orders.size.astype(np.int32))]
-    handles = {k: j.arr(v) for k, v in outs.items()}
-    outs = {k: j.objs[v] for k, v in handles.items()}
-    m = lib.Java_GpuMatchingEngine_submit(j.env, None, h, n, *ins, *[handles[k] for k in
-                                          ("kind", "oAction", "oOid", "oAid", "oSid", "oPrice", "oSize", "oPrev",
-                                           "oHasPrev", "status")])
-    assert not j.thrown, j.thrown
-    assert m >= 0
-    return m, outs
+class Proc:
+    """GpuMatchingEngine.java's protocol over the JNI glue: two slots of direct buffers, epochs
+    submitted asynchronously, the oldest completed first and its rows read back."""
+
+    def __init__(self, lib, j, h, epoch, max_trades):
+        self.lib, self.j, self.h, self.epoch = lib, j, h, epoch
+        self.cols, self.rows = [], []
+        for slot in range(2):
+            bufs, views = [], {}
+            for name, dt in (("action", np.int32), ("oid", np.int64), ("aid", np.int64), ("sid", np.int64),
+                             ("price", np.int32), ("size", np.int32)):
+                b, v = j.direct(epoch * np.dtype(dt).itemsize, dt)
+                bufs.append(b)
+                views[name] = v
+            rb, rv = j.direct(48 * (2 * epoch + 2 * max_trades), ROW_DTYPE)
+            assert lib.Java_GpuMatchingEngine_bind(j.env, None, h, slot, *bufs, rb) == 0
+            self.cols.append(views)
+            self.rows.append(rv)
+        self.status = j.arr(np.zeros(4, np.int64))
+        self.pending = []          # (slot, n) in submission order
+
+    def submit(self, slot, part):
+        for name, v in self.cols[slot].items():
+            v[:len(part)] = getattr(part, name)
+        rc = self.lib.Java_GpuMatchingEngine_submit(self.j.env, None, self.h, slot, len(part))
+        assert rc == 0, rc
+        self.pending.append(slot)
+
+    def complete(self):
+        slot = self.pending.pop(0)
+        m = self.lib.Java_GpuMatchingEngine_complete(self.j.env, None, self.h, slot, self.status)
+        assert not self.j.thrown, self.j.thrown
+        return self.rows[slot][:m].copy(), self.j.objs[self.status].copy()
 
 
-def _as_tape(m, o, rec_dtype):
-    t = np.zeros(m, rec_dtype)
-    t["key"] = (o["kind"][:m] != 0).astype(np.int32)
-    for f, k in (("action", "oAction"), ("oid", "oOid"), ("aid", "oAid"), ("sid", "oSid"), ("price", "oPrice"),
-                 ("size", "oSize"), ("prev", "oPrev")):
-        t[f] = o[k][:m]
-    t["has_prev"] = o["oHasPrev"][:m]
+def _as_tape(rows, rec_dtype):
+    t = np.zeros(len(rows), rec_dtype)
+    t["key"] = (rows["kind"] != 0).astype(np.int32)
+    for f in ("action", "oid", "aid", "sid", "price", "size", "prev"):
+        t[f] = rows[f]
+    t["has_prev"] = rows["has_prev"]
     return t
 
 
@@ -141,33 +176,52 @@ def _cmp_fields(got, want):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["funded", "exact"])
-def test_jni_submit_rows_equal_oracle_tape(oracle_mod, mode):
+def test_jni_epochs_in_flight_equal_oracle_tape(oracle_mod, mode):
+    """Two epochs in flight at a time (the processor fills one slot while the other runs), poll until
+    the oldest is done, complete it: the rows of every epoch in order equal the oracle's tape."""
+    import time
+
     lib = _lib()
     j = FakeJni()
     if mode == "funded":
-        orders = W.Orders.concat([W.funded_setup(256, range(1, 65)), W.uniform(20_000, n_symbols=64, n_accounts=256, seed=11)])
-        h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 1 << 15, 1 << 16, 1 << 16, 256, 0, 0)
+        setup = W.funded_setup(256, range(1, 65))
+        orders = W.Orders.concat([setup, W.uniform(40_000, n_symbols=64, n_accounts=256, seed=11)])
+        # default processor flags: the exact ledger, serial fallback where the proof fails
+        h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 1 << 13, 1 << 16, 1 << 15, 256, 3, 0)
+        epoch, max_trades = 1 << 13, 1 << 15
     else:
-        orders = W.exchange_test(3_000, seed=5)
-        h = lib.Java_GpuMatchingEngine_create(j.env, None, 0, 8, 1 << 13, 1 << 14, 1 << 15, 0, 0, 0)
+        orders = W.exchange_test(6_000, seed=5)
+        h = lib.Java_GpuMatchingEngine_create(j.env, None, 0, 8, 1 << 12, 1 << 14, 1 << 14, 0, 0, 0)
+        epoch, max_trades = 1 << 12, 1 << 14
     assert h and not j.thrown, j.thrown
+    p = Proc(lib, j, h, epoch, max_trades)
+    assert lib.Java_GpuMatchingEngine_poll(j.env, None, h) == 1      # nothing in flight
+    got, polls = [], 0
+    parts = [orders.slice(a, min(len(orders), a + epoch)) for a in range(0, len(orders), epoch)]
+    for k, part in enumerate(parts):
+        if len(p.pending) == 2:
+            t0 = time.time()
+            while lib.Java_GpuMatchingEngine_poll(j.env, None, h) == 0:   # the punctuator's poll
+                polls += 1
+                assert time.time() - t0 < 60
+            rows, st = p.complete()
+            assert st[0] == 0 and st[3] > 0
+            got.append(_as_tape(rows, oracle_mod.REC_DTYPE))
+        p.submit(k % 2, part)
+    while p.pending:
+        rows, st = p.complete()
+        assert st[0] == 0
+        got.append(_as_tape(rows, oracle_mod.REC_DTYPE))
+    lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
     o = oracle_mod.Oracle()
     o.process(orders)
-    want = o.tape()
-    got = []
-    for a in range(0, len(orders), 1 << 13):    # several flushes, as the processor would
-        part = orders.slice(a, min(len(orders), a + (1 << 13)))
-        m, outs = _submit(lib, j, h, part, 1 << 15 if mode == "funded" else 1 << 14)
-        assert outs["status"][0] == 0
-        got.append(_as_tape(m, outs, oracle_mod.REC_DTYPE))
-    lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
-    _cmp_fields(np.concatenate(got), want)
+    _cmp_fields(np.concatenate(got), o.tape())
 
 
 @pytest.mark.gpu
-def test_jni_submit_forwards_the_records_before_a_fault(oracle_mod):
+def test_jni_forwards_the_records_before_a_fault(oracle_mod):
     """A REMOVE_SYMBOL of a non-empty book never returns in the reference (KP:341-353): the rows of
-    the records before it are produced, status names the fault and its index."""
+    the records before it are produced, status names the fault, its index and n_effective."""
     lib = _lib()
     j = FakeJni()
     setup = W.funded_setup(16, range(1, 9))
@@ -176,13 +230,16 @@ def test_jni_submit_forwards_the_records_before_a_fault(oracle_mod):
     orders = W.Orders.concat([body.slice(0, 2000), bad, body.slice(2000, 3000)])
     h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 9, 1 << 13, 1 << 14, 1 << 14, 16, 0, 0)
     assert h
-    _submit(lib, j, h, setup, 1 << 14)
-    m, outs = _submit(lib, j, h, orders, 1 << 14)
-    st = outs["status"]
-    assert st[0] == 3 and st[2] == 2000          # KME_E_DOMAIN at the REMOVE_SYMBOL
+    p = Proc(lib, j, h, 1 << 13, 1 << 14)
+    p.submit(0, setup)
+    _, st0 = p.complete()
+    assert st0[0] == 0
+    p.submit(1, orders)
+    rows, st = p.complete()
+    assert st[0] == 3 and st[2] == 2000 and st[3] == 2000      # KME_E_DOMAIN at the REMOVE_SYMBOL
     o = oracle_mod.Oracle()
     o.process(setup)
     o.clear_tape()
     o.process(orders.slice(0, 2000))
-    _cmp_fields(_as_tape(m, outs, oracle_mod.REC_DTYPE), o.tape())
+    _cmp_fields(_as_tape(rows, oracle_mod.REC_DTYPE), o.tape())
     lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
