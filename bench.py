@@ -295,6 +295,7 @@ def main():
         "price": torch.from_numpy(stream.price).to(dev), "size": torch.from_numpy(stream.size).to(dev),
     }
     orders_per_epoch = [int(stream.slice(k * E, (k + 1) * E).n_orders()) for k in range(args.warmup + args.steps + 1)]
+    cancels_timed = int(np.count_nonzero(stream.action[args.warmup * E:(args.warmup + args.steps) * E] == W.CANCEL))
     # market data: this rank's symbols' top of book, all-gathered (16 B per symbol)
     rows, per_rank = market_data_layout(world, args.workload, args.symbols)
     groups = torch.from_numpy(sids.astype(np.int32)).to(dev)
@@ -467,6 +468,8 @@ def main():
             "host_path": host_path,
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
+            # cancels that removed a resting order (KP:289-323) / cancels in the timed epochs
+            "cancel_success_rank0": mix["cancels_ok"] / max(1, cancels_timed),
             "roofline": {"kernel": "k_match_lanes+k_match (match phase: light groups one lane each, heavy groups "
                                    "one wavefront each, concurrent)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

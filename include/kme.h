@@ -281,6 +281,34 @@ kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out);
  * bench.py all-gathers over RCCL. */
 kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uint32_t n, kme_tob* dev_out);
 
+/* ---- Multi-GPU: one engine per GPU, symbols keyed over them (kme_shard_of) ----
+ * An RCCL communicator over the node's engines.  kme_comm_unique_id (on one rank) fills 128 bytes
+ * that the caller hands to every rank over any channel (torch.distributed, a Kafka control topic);
+ * kme_comm_init joins rank `rank` of `n_ranks` on the engine's device (blocks until all joined).
+ * RCCL is loaded at the first call (env KME_RCCL_LIB, default librccl.so.1): libkme itself does not
+ * depend on it. */
+typedef struct kme_comm kme_comm;
+kme_status kme_comm_unique_id(void* id128);
+kme_status kme_comm_init(kme_engine* e, uint32_t n_ranks, uint32_t rank, const void* id128, kme_comm** out);
+kme_status kme_comm_destroy(kme_comm* c);
+/* Per-epoch market data, the only collective of the data path: this engine's top of book for its
+ * n_groups symbol groups (as kme_top_of_book_groups) into its own block of dev_all (rows_per_rank
+ * rows per rank, rank-major; rows past n_groups are -1 / 0), then an in-place ncclAllGather over
+ * xGMI on the engine stream, so every rank holds the node's snapshot (16 B per symbol). */
+kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t* dev_groups, uint32_t n_groups,
+                                     uint32_t rows_per_rank, kme_tob* dev_all);
+/* Credit between symbol shards (credit_shards = N > 1; between epochs, none in flight).  Each shard
+ * proves its orders against its own share of an account's cash and the funded bound only falls, so a
+ * share can run dry while the others hold cash.  kme_credit_state: this engine's
+ * funded bound and demand so far per account, two int64 device arrays of max_accounts
+ * (dev_out[0, A) and dev_out[A, 2A)); kme_credit_adjust: the re-split of the pooled bound from every
+ * shard's pair (dev_all = N such blocks, shard-major): every engine computes the same split and the
+ * shares sum to the pooled bound, so the account's cash still covers all of them;
+ * kme_credit_rebalance: state, all-gather over RCCL, adjust (collective: every rank calls it). */
+kme_status kme_credit_state(kme_engine* e, int64_t* dev_out);
+kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_shards, uint32_t my_shard);
+kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c);
+
 /* Wall-clock (HIP event) duration in ms of each kernel phase of the last epoch; index by name
  * (kme_phase_names).  Used by bench.py for the roofline of the dominant kernel. */
 #define KME_MAX_PHASES 16

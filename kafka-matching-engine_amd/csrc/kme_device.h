@@ -132,6 +132,7 @@ struct DevState {
     KG int64_t* acct_need;
     KG int64_t* acct_negx;
     KG int64_t* acct_xfer;
+    KG int64_t* acct_demand;          // sum of the epochs' need on this engine (credit re-splitting weights)
     // EXACT ledger
     KG uint32_t* bal_state;
     KG int64_t* bal_key;

@@ -483,8 +483,59 @@ __global__ void k_commit_funded(DevState S, EpochIO io) {
     const int64_t need = S.acct_need[a], negx = S.acct_negx[a], xfer = S.acct_xfer[a];
     if (need == 0 && negx == 0 && xfer == 0) return;
     const int64_t since = S.acct_since[a];
-    if (!refused && since < io.seq_base + (int64_t)io.n) S.acct_lb[a] = (since < io.seq_base ? S.acct_lb[a] : 0) - need + xfer;
+    if (!refused && since < io.seq_base + (int64_t)io.n) {
+        S.acct_lb[a] = (since < io.seq_base ? S.acct_lb[a] : 0) - need + xfer;
+        S.acct_demand[a] += need;
+    }
     S.acct_need[a] = 0; S.acct_negx[a] = 0; S.acct_xfer[a] = 0;
+}
+
+// ------------------------------------------------------------------ credit between symbol shards
+// With symbols keyed over N engines (credit_shards = N) each engine proves its orders against its
+// own share of an account's cash (k_ledger_funded / k_check_funded), and the funded bound only falls
+// inside the proof (refunds are not credited back, KP:269, 286, 331), so a share can run dry while
+// the account's other shares still hold most of its cash.  Between epochs the shares are pooled and
+// split again: every engine contributes (funded bound, demand so far), all-gathers them
+// (kme_credit_rebalance over RCCL, or any caller transport: kme_credit_state / kme_credit_adjust),
+// and takes floor(total * w_me / sum w) of the pooled bound, w_k = demand_k + mean demand + 1 (half
+// proportional to where the account trades, half equal), the rounding left-over going to shard
+// a mod N.  Every engine computes the same split from the same data, the shares sum to exactly the
+// pooled bound, so the invariant the proof rests on -- the account's cash is at least the sum of the
+// shards' bounds -- holds across the re-split.
+__global__ void __launch_bounds__(256) k_credit_state(DevState S, int64_t* out) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= S.A) return;
+    out[a] = S.acct_since[a] == INT64_MAX ? 0 : S.acct_lb[a];
+    out[S.A + a] = S.acct_demand[a];
+}
+__global__ void __launch_bounds__(256) k_credit_adjust(DevState S, const int64_t* all, uint32_t n, uint32_t me) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= S.A || S.acct_since[a] == INT64_MAX) return;
+    const size_t A = (size_t)S.A;
+    unsigned __int128 tot = 0, dsum = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int64_t lb = all[(size_t)k * 2 * A + a], d = all[(size_t)k * 2 * A + A + a];
+        tot += (unsigned __int128)(lb > 0 ? lb : 0);
+        dsum += (unsigned __int128)(d > 0 ? d : 0);
+    }
+    const unsigned __int128 mean = dsum / n;
+    unsigned __int128 wsum = 0, w_me = 0, given = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int64_t d = all[(size_t)k * 2 * A + A + a];
+        const unsigned __int128 w = (unsigned __int128)(d > 0 ? d : 0) + mean + 1;
+        wsum += w;
+        if (k == me) w_me = w;
+    }
+    unsigned __int128 mine = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int64_t d = all[(size_t)k * 2 * A + A + a];
+        const unsigned __int128 share = tot * ((unsigned __int128)(d > 0 ? d : 0) + mean + 1) / wsum;
+        given += share;
+        if (k == me) mine = share;
+    }
+    (void)w_me;
+    if ((uint32_t)(a % n) == me) mine += tot - given;   // the rounding left-over
+    S.acct_lb[a] = (int64_t)mine;
 }
 
 // Symbol group of each record and the node a CANCEL addresses.  The cancel carries no symbol
@@ -2908,10 +2959,10 @@ __global__ void k_tob(DevState S, kme_tob* out) {
     if (g < S.G) out[g] = tob_of(S, g);
 }
 // The snapshot of a list of groups (a shard's own symbols): out[k] = top of book of groups[k].
-__global__ void k_tob_groups(DevState S, const uint32_t* groups, uint32_t n, kme_tob* out) {
+__global__ void k_tob_groups(DevState S, const uint32_t* groups, uint32_t n, uint32_t rows, kme_tob* out) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const uint32_t g = groups[k];
+    if (k >= rows) return;
+    const uint32_t g = k < n ? groups[k] : 0xFFFFFFFFu;   // rows past n: padding (-1 / 0)
     out[k] = g < (uint32_t)S.G ? tob_of(S, (int32_t)g) : kme_tob{-1, -1, 0, 0};
 }
 
@@ -3037,9 +3088,16 @@ void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st)
 void launch_tob(const DevState& S, void* out, hipStream_t st) {
     hipLaunchKernelGGL(k_tob, dim3(cdiv((uint32_t)S.G, 256)), dim3(256), 0, st, S, (kme_tob*)out);
 }
-void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st) {
-    if (n == 0) return;
-    hipLaunchKernelGGL(k_tob_groups, dim3(cdiv(n, 256)), dim3(256), 0, st, S, groups, n, (kme_tob*)out);
+void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st, uint32_t rows) {
+    if (rows < n) rows = n;
+    if (rows == 0) return;
+    hipLaunchKernelGGL(k_tob_groups, dim3(cdiv(rows, 256)), dim3(256), 0, st, S, groups, n, rows, (kme_tob*)out);
+}
+void launch_credit_state(const DevState& S, int64_t* out, hipStream_t st) {
+    if (S.A) hipLaunchKernelGGL(k_credit_state, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, out);
+}
+void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, hipStream_t st) {
+    if (S.A) hipLaunchKernelGGL(k_credit_adjust, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, all, n, me);
 }
 void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st) {
     hipLaunchKernelGGL(k_export_trades, dim3(128), dim3(256), 0, st, reinterpret_cast<const int4*>(src), count, cap,

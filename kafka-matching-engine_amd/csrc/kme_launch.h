@@ -46,8 +46,12 @@ void launch_ser_write(const kme_orders& in, const kme_epoch_result& r, uint32_t 
 // maintenance
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st);   // pool slots [0, used) hold every node
 void launch_tob(const DevState& S, void* out, hipStream_t st);
-void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st);
+// rows >= n: rows past n are padding (-1 / 0)
+void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st, uint32_t rows = 0);
 void launch_init_state(const DevState& S, hipStream_t st);
+// credit between symbol shards: (funded bound, demand) per account out; the re-split from all shards' pairs
+void launch_credit_state(const DevState& S, int64_t* out, hipStream_t st);
+void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, hipStream_t st);
 // host epochs (kme_submit_epoch_host): trades[0, min(trade_off[n], cap)) into device-mapped host memory
 void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st);
 

@@ -6,7 +6,9 @@
 //   kme_submit_epoch[_device]  MatchingEngine.process KP:96-126, for a whole epoch of records
 //   kme_destroy           MatchingEngine.close KP:129
 //   kme_snapshot_*        the contents of Books/Buckets/Orders and Balances/Positions
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -252,6 +254,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.acct_need, cfg->max_accounts);
         ALLOC(S.acct_negx, cfg->max_accounts);
         ALLOC(S.acct_xfer, cfg->max_accounts);
+        ALLOC(S.acct_demand, cfg->max_accounts);
         if (S.ledger_replay) ALLOC(S.vic, E);
     }
     if (exact_ledger) {
@@ -311,6 +314,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         HIP_TRY(hipMemsetAsync(S.acct_need, 0, cfg->max_accounts * sizeof(int64_t), st));
         HIP_TRY(hipMemsetAsync(S.acct_negx, 0, cfg->max_accounts * sizeof(int64_t), st));
         HIP_TRY(hipMemsetAsync(S.acct_xfer, 0, cfg->max_accounts * sizeof(int64_t), st));
+        HIP_TRY(hipMemsetAsync(S.acct_demand, 0, cfg->max_accounts * sizeof(int64_t), st));
     }
     if (exact_ledger) {
         const size_t lc = (size_t)S.bal_mask + 1;
@@ -642,6 +646,138 @@ kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in, uint32_t n
     return KME_OK;
 }
 
+// ------------------------------------------------------------------ multi-GPU: RCCL
+namespace {
+// RCCL through dlopen: libkme has no link-time dependency on it, and a process that already loaded
+// an RCCL (torch's) can point KME_RCCL_LIB at that copy so that one RCCL serves both.
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) allgather = nullptr;
+};
+Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        const char* path = std::getenv("KME_RCCL_LIB");
+        r.h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (r.h) {
+            r.get_id = (decltype(r.get_id))dlsym(r.h, "ncclGetUniqueId");
+            r.init = (decltype(r.init))dlsym(r.h, "ncclCommInitRank");
+            r.destroy = (decltype(r.destroy))dlsym(r.h, "ncclCommDestroy");
+            r.allgather = (decltype(r.allgather))dlsym(r.h, "ncclAllGather");
+        }
+        if (!r.get_id || !r.init || !r.destroy || !r.allgather) {
+            std::fprintf(stderr, "kme: RCCL not available (%s)\n", r.h ? "missing symbols" : dlerror());
+            r.h = nullptr;
+        }
+    }
+    return r.h ? &r : nullptr;
+}
+}  // namespace
+
+struct kme_comm {
+    ncclComm_t comm = nullptr;
+    uint32_t n = 0, rank = 0;
+    int device = 0;
+    int64_t* d_credit = nullptr;     // kme_credit_rebalance: n x (bound, demand) x accounts
+    size_t credit_accounts = 0;
+};
+
+kme_status kme_comm_unique_id(void* id128) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId");
+    if (!id128) return KME_E_INVALID;
+    Rccl* r = rccl();
+    if (!r) return KME_E_UNSUPPORTED;
+    ncclUniqueId id;
+    if (r->get_id(&id) != ncclSuccess) return KME_E_HIP;
+    std::memcpy(id128, &id, sizeof id);
+    return KME_OK;
+}
+
+kme_status kme_comm_init(kme_engine* e, uint32_t n_ranks, uint32_t rank, const void* id128, kme_comm** out) {
+    if (!e || !id128 || !out || n_ranks == 0 || rank >= n_ranks) return KME_E_INVALID;
+    Rccl* r = rccl();
+    if (!r) return KME_E_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof id);
+    kme_comm* c = new kme_comm();
+    c->n = n_ranks; c->rank = rank; c->device = e->device;
+    if (r->init(&c->comm, (int)n_ranks, id, (int)rank) != ncclSuccess) { delete c; return KME_E_HIP; }
+    *out = c;
+    return KME_OK;
+}
+
+kme_status kme_comm_destroy(kme_comm* c) {
+    if (!c) return KME_E_INVALID;
+    Rccl* r = rccl();
+    (void)hipSetDevice(c->device);
+    if (c->d_credit) (void)hipFree(c->d_credit);
+    if (r && c->comm) r->destroy(c->comm);
+    delete c;
+    return KME_OK;
+}
+
+kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t* dev_groups, uint32_t n_groups,
+                                     uint32_t rows_per_rank, kme_tob* dev_all) {
+    if (!e || !c || !dev_all || n_groups > rows_per_rank || (n_groups && !dev_groups)) return KME_E_INVALID;
+    Rccl* r = rccl();
+    if (!r) return KME_E_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(e->device));
+    kme_tob* mine = dev_all + (size_t)c->rank * rows_per_rank;
+    launch_tob_groups(e->S, dev_groups, n_groups, mine, e->stream, rows_per_rank);
+    HIP_TRY(hipGetLastError());
+    if (r->allgather(mine, dev_all, (size_t)rows_per_rank * sizeof(kme_tob), ncclUint8, c->comm, e->stream) != ncclSuccess)
+        return KME_E_HIP;
+    return KME_OK;
+}
+
+kme_status kme_credit_state(kme_engine* e, int64_t* dev_out) {
+    if (!e || !dev_out || e->cfg.mode != KME_MODE_FUNDED) return KME_E_INVALID;
+    if (e->inflight) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    launch_credit_state(e->S, dev_out, e->stream);
+    HIP_TRY(hipGetLastError());
+    return KME_OK;
+}
+
+kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_shards, uint32_t my_shard) {
+    if (!e || !dev_all || e->cfg.mode != KME_MODE_FUNDED || n_shards == 0 || my_shard >= n_shards) return KME_E_INVALID;
+    if (e->inflight) return KME_E_INVALID;
+    if (e->failed) return KME_E_FAILED;
+    HIP_TRY(hipSetDevice(e->device));
+    launch_credit_adjust(e->S, dev_all, n_shards, my_shard, e->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return KME_OK;
+}
+
+kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c) {
+    if (!e || !c || e->cfg.mode != KME_MODE_FUNDED) return KME_E_INVALID;
+    if (e->inflight) return KME_E_INVALID;
+    if (e->failed) return KME_E_FAILED;
+    Rccl* r = rccl();
+    if (!r) return KME_E_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t A = e->cfg.max_accounts;
+    if (!c->d_credit || c->credit_accounts != A) {
+        if (c->d_credit) HIP_TRY(hipFree(c->d_credit));
+        c->d_credit = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_credit, (size_t)c->n * 2 * A * sizeof(int64_t)));
+        c->credit_accounts = A;
+    }
+    int64_t* mine = c->d_credit + (size_t)c->rank * 2 * A;
+    launch_credit_state(e->S, mine, e->stream);
+    HIP_TRY(hipGetLastError());
+    if (r->allgather(mine, c->d_credit, 2 * A * sizeof(int64_t), ncclUint8, c->comm, e->stream) != ncclSuccess)
+        return KME_E_HIP;
+    return kme_credit_adjust(e, c->d_credit, c->n, c->rank);
+}
+
 #ifndef KME_SRC_HASH
 #define KME_SRC_HASH "unknown"
 #endif
@@ -670,6 +806,7 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
     if (e->cfg.mode == KME_MODE_FUNDED) {
         b.push_back({S.acct_since, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
         b.push_back({S.acct_lb, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
+        b.push_back({S.acct_demand, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
     }
     if (e->cfg.mode == KME_MODE_EXACT || S.ledger_replay) {
         const size_t lc = (size_t)S.bal_mask + 1;

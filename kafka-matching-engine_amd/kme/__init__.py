@@ -73,6 +73,8 @@ EXPORTS = [
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
     "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_build_id",
+    "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
+    "kme_credit_adjust", "kme_credit_rebalance",
 ]
 
 _lib = None
@@ -142,6 +144,13 @@ def lib():
         "kme_expand_rows": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                  C.POINTER(C.c_size_t)]),
         "kme_build_id": (C.c_char_p, []),
+        "kme_comm_unique_id": (st, [vp]),
+        "kme_comm_init": (st, [vp, u32, u32, vp, C.POINTER(vp)]),
+        "kme_comm_destroy": (st, [vp]),
+        "kme_market_data_allgather": (st, [vp, vp, vp, u32, u32, vp]),
+        "kme_credit_state": (st, [vp, vp]),
+        "kme_credit_adjust": (st, [vp, vp, u32, u32]),
+        "kme_credit_rebalance": (st, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -309,6 +318,20 @@ class Engine:
             raise KmeError(rc, "kme_poll")
         return bool(done.value)
 
+    # ---- multi-GPU: RCCL communicator, market data, credit between shards
+    def comm_init(self, n_ranks: int, rank: int, uid: bytes) -> "Comm":
+        return Comm(self, n_ranks, rank, uid)
+
+    def credit_state(self, dev_ptr: int):
+        rc = self._L.kme_credit_state(self._h, C.c_void_p(int(dev_ptr)))
+        if rc:
+            raise KmeError(rc, "kme_credit_state")
+
+    def credit_adjust(self, dev_all_ptr: int, n_shards: int, my_shard: int):
+        rc = self._L.kme_credit_adjust(self._h, C.c_void_p(int(dev_all_ptr)), n_shards, my_shard)
+        if rc:
+            raise KmeError(rc, "kme_credit_adjust")
+
     def wait(self) -> kme_epoch_status:
         st = kme_epoch_status()
         rc = self._L.kme_wait(self._h, C.byref(st))
@@ -404,6 +427,50 @@ class Engine:
 
     def snapshot_ledger(self) -> str:
         return self._text(self._L.kme_snapshot_ledger)
+
+
+def comm_unique_id() -> bytes:
+    """kme_comm_unique_id: 128 bytes for kme_comm_init, made on one rank and sent to all."""
+    buf = C.create_string_buffer(128)
+    rc = lib().kme_comm_unique_id(buf)
+    if rc:
+        raise KmeError(rc, "kme_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """kme_comm: this engine's rank of an RCCL communicator over the node's engines."""
+
+    def __init__(self, eng: "Engine", n_ranks: int, rank: int, uid: bytes):
+        self._L, self.eng, self.n, self.rank = lib(), eng, n_ranks, rank
+        h = C.c_void_p()
+        b = C.create_string_buffer(bytes(uid), 128)
+        rc = self._L.kme_comm_init(eng.handle, n_ranks, rank, b, C.byref(h))
+        if rc:
+            raise KmeError(rc, "kme_comm_init")
+        self._h = h
+
+    def market_data_allgather(self, groups_ptr: int, n_groups: int, rows_per_rank: int, dev_all_ptr: int):
+        rc = self._L.kme_market_data_allgather(self.eng.handle, self._h, C.c_void_p(int(groups_ptr)), n_groups,
+                                               rows_per_rank, C.c_void_p(int(dev_all_ptr)))
+        if rc:
+            raise KmeError(rc, "kme_market_data_allgather")
+
+    def credit_rebalance(self):
+        rc = self._L.kme_credit_rebalance(self.eng.handle, self._h)
+        if rc:
+            raise KmeError(rc, "kme_credit_rebalance")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.kme_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Processor:
