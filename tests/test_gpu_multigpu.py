@@ -91,7 +91,7 @@ def test_credit_resplit_keeps_every_epoch_parallel(kme_mod, oracle_mod, rebalanc
                 refused = ep
                 break
             text = sharding.partition_tape(r.tape_json(parts[k]), echo[k])
-            chunks.update(zip((seqs[k][echo[k]] + a).tolist(), sharding._chunks(text)))
+            chunks.update(zip(seqs[k][echo[k]].tolist(), sharding._chunks(text)))   # (global indices)
         if refused is not None:
             break
         if rebalance and ep > 0:
