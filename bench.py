@@ -407,7 +407,8 @@ def main():
         d = rows_[hot] if os.environ.get("KME_STAMPS_HOT") else rows_.sum(axis=0)
         names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",
                  "n_trade_rec", "n_rest_rec", "n_cancel_rec", "maker_wait", "n_maker", "victim_wait", "n_victim",
-                 "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre"]
+                 "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre",
+                 "fast", "n_fast_rec", "n_fast_seg", "fast_pass"]
         v = dict(zip(names, d))
         per = {"share_of_kernel": {n: v[n] / v["kernel"] for n in ("group_in", "batch", "trade_rec", "rest_rec",
                                                                      "cancel_rec", "other_rec", "group_out", "flush")},
@@ -421,7 +422,12 @@ def main():
                "rest_parts_per_rest": {n: v[n] / max(1, v["n_rest_rec"]) for n in ("rest_alloc", "rest_level", "rest_node", "tm_pre_norest")},
                "rec_pick_per_rec": v["rec_pick"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
                "rec_total_per_rec": v["rec_out"] / max(1, v["n_trade_rec"] + v["n_rest_rec"] + v["n_cancel_rec"]),
-               "counts": {n: v[n] for n in ("n_trade_rec", "n_rest_rec", "n_cancel_rec", "n_maker", "n_victim")}}
+               "counts": {n: v[n] for n in ("n_trade_rec", "n_rest_rec", "n_cancel_rec", "n_maker", "n_victim")},
+               "fast": {"records": v["n_fast_rec"], "segments": v["n_fast_seg"],
+                        "share_of_kernel": v["fast"] / v["kernel"],
+                        "cycles_per_fast_rec": v["fast"] / max(1, v["n_fast_rec"]),
+                        "pass_cycles_per_fast_rec": v["fast_pass"] / max(1, v["n_fast_rec"]),
+                        "records_per_segment": v["n_fast_rec"] / max(1, v["n_fast_seg"])}}
         per["group"] = hot if os.environ.get("KME_STAMPS_HOT") else "all"
         print(json.dumps({"stamps": per}), flush=True)
         return

@@ -101,7 +101,10 @@ enum Ctr : int {
     C_BUSY,            // FUNDED: groups k_match took this epoch (the host's stream choice for the next)
     C_REBUILD_FAIL,    // oid-table rebuild: entries that found no slot (persistent, zeroed by the rebuild)
     C_LIGHT,           // FUNDED: k_match_lanes wavefronts that had a group this epoch (the next one's launch)
-    C_NCTR = 16
+    C_SIZE0,           // persistent: nonzero once a BUY/SELL of size 0 was submitted (a book may then hold
+                       // size-0 makers, and k_match's fast segments -- which read a level's emptiness off
+                       // its quantity -- stay off)
+    C_NCTR = 20
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
 constexpr int ci(int k) { return k * CTR_STRIDE; }
@@ -118,7 +121,7 @@ struct DevState {
     int32_t light_max;                // FUNDED: groups with at most this many records in the epoch
                                       // run in k_match_lanes (one lane each); 0 = none
     int32_t fallback;                 // KME_FLAG_SERIAL_FALLBACK
-    int32_t os_lanes;                 // reserved (0): the OUT echo is stored at the input index
+    int32_t fast;                     // k_match fast segments on (env KME_FAST=0: off, for A/B runs)
     uint32_t pool_cap, otab_mask, credit_div, ttmp_cap;     // ttmp_cap: overflow region records
     uint32_t bal_mask, pos_mask, trades_cap, tshard_cap;
     uint32_t os_base, _pad1;          // osort records (= max_epoch)

@@ -319,6 +319,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     for (uint32_t i = t0; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
         n_orders += (a == BUY || a == SELL || a == CANCEL) ? 1u : 0u;
+        if ((a == BUY || a == SELL) && io.size[i] == 0 && !S.ctr[ci(C_SIZE0)]) atomicOr(&S.ctr[ci(C_SIZE0)], 1ull);
         if (a == BUY || a == SELL) {
             // the order's oid-table entry (pending until k_table); on the way, the duplicate-oid
             // guard: another BUY/SELL of this epoch, or a live resting order, with this oid
@@ -1421,7 +1422,10 @@ struct GroupLds {
     uint32_t dirty[DIRTY_WORDS];
     uint64_t bmap[4];             // level bitmaps: book +g (lsb, msb), book -g (lsb, msb)
     int32_t gs[8];                // exists, free-list head block, bump chunk next / end, free-stack top, staged trades
-    int4 trd[2 * TRD];            // trade k: (maker oid, maker aid), (price | sid < 0 << 8, size, seq, ord)
+    int4 trd[2 * TRD];            // trade k: (maker oid, maker aid), (price | sid < 0 << 8, size, seq, ord);
+                                  // during a fast segment (emptied first): record k's (oid, aid) at trd[k]
+    int4 fr[64];                  // fast segment: record k's (input index, PRec w0 | kind << 24, size, slot),
+                                  // then its results (trades, has_prev, prev)
 };
 
 KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1507,6 +1511,7 @@ enum Stamp : int {
     ST_GROUP_IN = 0, ST_BATCH, ST_TRADE_REC, ST_REST_REC, ST_CANCEL_REC, ST_OTHER_REC, ST_GROUP_OUT, ST_KERNEL,
     ST_N_TRADE_REC, ST_N_REST_REC, ST_N_CANCEL_REC, ST_MAKER_WAIT, ST_N_MAKER, ST_VICTIM_WAIT, ST_N_VICTIM, ST_FLUSH,
     ST_REST_ALLOC, ST_REST_LEVEL, ST_REST_NODE, ST_REC_PICK, ST_REC_OUT, ST_TM_PRE, ST_REST_PRE,
+    ST_FAST, ST_N_FAST_REC, ST_N_FAST_SEG, ST_FAST_PASS,
     ST_N = 32
 };
 
@@ -1969,6 +1974,348 @@ struct GroupWave {
         return !dead;
     }
 
+    // ---------------- fast segments: parallelism inside one book
+    // A hot book's records cost ~1.3 us each on the serial path above, mostly issue latency and the
+    // dependent loads of one record's chain.  A fast segment takes a run of the batch's records in
+    // two steps:
+    //   1. the aggregate pass (scalar, one record at a time, no node access): what each record does
+    //      to the book's LEVELS -- the level bitmaps (Books, KP:38-41) and each level's resting
+    //      quantity -- decides its outcome: a BUY/SELL that crosses takes its whole size from the
+    //      best opposite level (KP:225-263) or rests at its price (KP:200-223), a cancel removes its
+    //      prefetched victim's quantity (KP:289-323);
+    //   2. the level step (vector): every level the segment touched is replayed by one lane, its
+    //      records in arrival order -- appends at the tail, takes walking the FIFO from the head
+    //      maker by maker exactly as KP:237-261 does (H3 zero-size trades included), unlinks -- so
+    //      the touched levels' node work runs side by side instead of record after record.
+    // Levels are independent once step 1 fixed every record's level and amount, so the result is
+    // the reference's.  The pass stops (the record goes to the serial path) where that does not
+    // hold: a take that would empty its level (the sweep continues at the next level, or its end
+    // decides a zero-size trade against another level's head), a cancel whose level was already
+    // taken from in the segment or whose victim is not prefetched (an order of this batch, or a node
+    // written since), a price scan that would fault (H5), any other action; and the fast path is off
+    // for group 0 (H4: one shared book) and once a size-0 order was ever submitted (C_SIZE0: a level's
+    // emptiness is then not its quantity being 0).
+    enum { FK_NONE = 0, FK_TAKE = 1, FK_REST = 2, FK_CANCEL = 3 };
+
+    // fstack holds at least n slots (n <= 64): free-list blocks, then the bump chunk
+    KDEV void fast_refill(int n) {
+        int fsp = gsv(GS_FSP);
+        while (fsp < n) {
+            const int32_t blk = gsv(GS_FREE_HEAD);
+            if (blk >= 0) {
+                const int32_t w = lane < 2 + FBLK - 1 ? reinterpret_cast<const KG int32_t*>(&pool[blk])[lane] : 0;
+                const int32_t nxt = rl32(w, 0), cnt = rl32(w, 1);
+                if (lane >= 2 && lane < 2 + cnt) L.fstack[fsp + lane - 2] = w;
+                L.fstack[fsp + cnt] = blk;                   // the block's own slot
+                fsp += cnt + 1;
+                set_gs(GS_FREE_HEAD, nxt);
+            } else {
+                int32_t cn = gsv(GS_CHUNK_NEXT);
+                int32_t ce = gsv(GS_CHUNK_END);
+                if (cn >= ce) {
+                    unsigned long long c = 0;
+                    KG unsigned long long* bump = &ctr()[ci(C_POOL_BUMP)];
+                    if (lane == 0) c = atomicAdd(bump, (unsigned long long)POOL_CHUNK);
+                    c = bcast64(c);
+                    if (c + POOL_CHUNK > cold().pool_cap) { die(KME_E_CAPACITY, KME_D_CAP_POOL); return; }
+                    cn = (int32_t)c;
+                    ce = (int32_t)(c + POOL_CHUNK);
+                    set_gs(GS_CHUNK_END, ce);
+                }
+                const int k = imin(n - fsp, ce - cn);
+                if (lane < k) L.fstack[fsp + lane] = cn + lane;
+                fsp += k;
+                set_gs(GS_CHUNK_NEXT, cn + k);
+            }
+            sync_lds();
+        }
+        set_gs(GS_FSP, fsp);
+        sync_lds();
+    }
+
+    // per-lane trade scratch (the level step's takes): LANE_TCH slots reserved at a time on the
+    // group's shard line, unused ones left as holes (seq = -1) that k_scatter skips
+    KDEV void lane_emit(uint32_t& tpos, uint32_t& tlim, uint32_t seq, uint32_t ord, int4 maker, int32_t msneg,
+                        int32_t mprice, int32_t ts, int& err) {
+        if (tpos == tlim) {
+            const DevState& S = *Sp;
+            const uint32_t tcap = S.tshard_cap, tb = (uint32_t)(g & (TSHARDS - 1)) * tcap;
+            KG unsigned long long* used = &S.tsh[(size_t)(g & (TSHARDS - 1)) * CTR_STRIDE + TS_USED];
+            const unsigned long long need = __ballot(1);
+            const int leader = __ffsll((long long)need) - 1;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1));
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(used, (unsigned long long)kLaneTradeChunk * __popcll(need));
+            base = (unsigned long long)__shfl((long long)base, leader) + (unsigned long long)rank * kLaneTradeChunk;
+            if (base + kLaneTradeChunk <= tcap) {
+                tpos = tb + (uint32_t)base;
+            } else {
+                for (unsigned long long q = base; q < tcap; ++q) S.ttmp[tb + q].seq = -1;   // straddles the end
+                const unsigned long long ob = atomicAdd(&S.ctr[ci(C_TTMP)], (unsigned long long)kLaneTradeChunk);
+                if (ob + kLaneTradeChunk > S.ttmp_cap) {
+                    for (unsigned long long q = ob; q < S.ttmp_cap; ++q) S.ttmp[(size_t)TSHARDS * tcap + q].seq = -1;
+                    raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_TRADES, (int64_t)seq);
+                    err = 1;
+                    return;
+                }
+                tpos = TSHARDS * tcap + (uint32_t)ob;
+            }
+            tlim = tpos + kLaneTradeChunk;
+        }
+        KG int4* r = reinterpret_cast<KG int4*>(&Sp->ttmp[tpos++]);
+        r[0] = maker;
+        r[1] = make_int4((int32_t)seq, (int32_t)tt_ordp(ord, mprice, msneg != 0), ts, g);
+    }
+    KDEV void lane_dirty(int32_t s) { atomicOr(&L.dirty[(s >> 5) & (DIRTY_WORDS - 1)], 1u << (s & 31)); }
+    // a freed node onto the group's free stack (LDS), or, with the stack full, as a one-slot block
+    // pushed on the group's free list
+    KDEV void lane_free(int32_t s) {
+        pool[s].live = 0;
+        lane_dirty(s);
+        const int pos = atomicAdd(&L.gs[GS_FSP], 1);
+        if (pos < FSTK) {
+            L.fstack[pos] = s;
+        } else {
+            const int32_t old = atomicExch(&L.gs[GS_FREE_HEAD], s);
+            KG int32_t* w = reinterpret_cast<KG int32_t*>(&pool[s]);
+            w[0] = old;
+            w[1] = 0;
+        }
+    }
+
+    // Records [j0, nb) of the batch: returns the first record the segment did not take (== j0: none).
+    // Per lane (= record) results go to the batch's OUT registers.
+    KDEV int fast_segment(const Lanes& B, int j0, int nb, int32_t& o_act, int32_t& o_size, int32_t& o_plo,
+                          int32_t& o_phi, int32_t& o_ntr, uint32_t& tpos, uint32_t& tlim) {
+        const bool inrange = lane >= j0 && lane < nb;
+        const int32_t b_act = B.w0 & 0xFF;
+        const int n_bs = (int)__popcll(__ballot(inrange && (b_act == BUY || b_act == SELL)));
+        if (gsv(GS_TCNT)) flush_trades();                     // trd is the segment's staging
+        fast_refill(n_bs);
+        if (dead) return j0;
+        const int fsp0 = gsv(GS_FSP);
+        const int32_t fslot = lane < n_bs ? L.fstack[fsp0 - 1 - lane] : -1;   // the k-th rest takes lane k's
+        // the level bitmaps as the segment starts (the level step's "was the level occupied")
+        const uint64_t s0l = bl(0), s0m = bm(0), s1l = bl(1), s1m = bm(1);
+        uint64_t b0l = s0l, b0m = s0m, b1l = s1l, b1m = s1m;
+        uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;         // levels taken from in the segment
+        const int exists = gsv(GS_EXISTS);
+        int32_t f_kind = FK_NONE, f_lev = 0, f_x = 0, f_slot = -1;
+        int nrest = 0;
+        int j = j0;
+        KST(const unsigned long long tp0 = stamp();)
+        // ---- 1. the aggregate pass
+#pragma nounroll
+        for (; j < nb; ++j) {
+            const int32_t w0 = rl32(B.w0, j);
+            const int32_t a = w0 & 0xFF, P = (w0 >> 8) & 0xFF;
+            const int32_t sz = rl32(B.size, j);
+            int kind = FK_NONE, lev = 0, x = 0, slot = -1, rested = 0;
+            int32_t oact = a, osize = sz;
+            if (a == BUY || a == SELL) {
+                if (exists && ((w0 >> 16) & 1)) {
+                    if (sz <= 0) break;
+                    const bool is_buy = a == BUY;
+                    const int side = (((w0 >> 17) & 1) != (is_buy ? 0 : 1)) ? 1 : 0;   // book_side, g != 0
+                    const int os = 1 - side;
+                    const uint64_t lo = os ? b1l : b0l, hi = os ? b1m : b0m;
+                    const int32_t pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+                    bool take = false;
+                    if (pb != -1) {
+                        if (!check_bit(lo, hi, pb)) break;    // the H5 NPE: the serial path raises it
+                        take = crosses(is_buy, sz, pb, P);
+                    }
+                    if (take) {
+                        const int li = os * LVP + pb;
+                        const int64_t q = U64(L.qty[li]);
+                        if ((int64_t)sz >= q) break;          // empties the level: the serial path
+                        L.qty[li] = q - sz;
+                        const uint64_t bit = 1ull << (pb & 63);
+                        if (os) { if (pb < 64) c1l |= bit; else c1m |= bit; }
+                        else { if (pb < 64) c0l |= bit; else c0m |= bit; }
+                        kind = FK_TAKE; lev = os * 128 + pb; x = sz; osize = 0;
+                    } else {
+                        const int li = side * LVP + P;
+                        uint64_t lo2 = side ? b1l : b0l, hi2 = side ? b1m : b0m;
+                        const int64_t q = check_bit(lo2, hi2, P) ? U64(L.qty[li]) : 0;
+                        L.qty[li] = q + sz;
+                        set_bit(lo2, hi2, P);
+                        if (side) { b1l = lo2; b1m = hi2; } else { b0l = lo2; b0m = hi2; }
+                        slot = rl32(fslot, nrest);
+                        ++nrest;
+                        kind = FK_REST; lev = side * 128 + P; x = sz; rested = 1;
+                    }
+                } else {
+                    oact = REJECT;                            // books.get == null / balances.get == null
+                }
+            } else if (a == CANCEL) {
+                const int32_t tgt = rl32(B.tgt, j);
+                if (tgt == -1) {
+                    oact = REJECT;                            // orders.get(oid) == null (KP:290)
+                } else {
+                    const int32_t pfs = rl32(B.pf_slot, j);
+                    if (pfs < 0 || is_dirty(pfs)) break;      // not prefetched, or written since: serial
+                    const int32_t meta = rl32(B.pf_meta, j);
+                    if (!((meta >> 11) & 1)) {
+                        oact = REJECT;                        // gone, or another account's (KP:290-291)
+                    } else if (__ballot(f_kind == FK_CANCEL && f_slot == pfs)) {
+                        oact = REJECT;                        // removed by an earlier cancel of the segment
+                    } else {
+                        if (!exists) break;                   // NPE (KP:294): the serial path raises it
+                        const int vp = meta & 0xFF, vs = (meta >> 8) & 1;
+                        const uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
+                        if ((cw >> (vp & 63)) & 1) break;     // its level was taken from: serial
+                        const int li = vs * LVP + vp;
+                        const int64_t q = U64(L.qty[li]) - rl32(B.pf_size, j);
+                        L.qty[li] = q;
+                        if (q == 0) {
+                            uint64_t lo2 = vs ? b1l : b0l, hi2 = vs ? b1m : b0m;
+                            unset_bit(lo2, hi2, vp);
+                            if (vs) { b1l = lo2; b1m = hi2; } else { b0l = lo2; b0m = hi2; }
+                        }
+                        kind = FK_CANCEL; lev = vs * 128 + vp; slot = pfs;
+                    }
+                }
+            } else {
+                break;                                        // symbol admin / unknown: serial
+            }
+            const bool me = lane == j;
+            f_kind = me ? kind : f_kind;
+            f_lev = me ? lev : f_lev;
+            f_x = me ? x : f_x;
+            f_slot = me ? slot : f_slot;
+            o_act = me ? ((oact & 0xFFFF) | (rested << 17)) : o_act;
+            o_size = me ? osize : o_size;
+            o_plo = me ? 0 : o_plo;
+            o_phi = me ? 0 : o_phi;
+            o_ntr = me ? 0 : o_ntr;
+        }
+        const int je = j;
+        KST(acc[ST_FAST_PASS] += stamp() - tp0;)
+        if (je == j0) return j0;
+        set_bm(0, b0l, b0m);
+        set_bm(1, b1l, b1m);
+        set_gs(GS_FSP, fsp0 - nrest);
+        // ---- 2. the level step
+        const bool inseg = lane >= j0 && lane < je;
+        const bool ev = inseg && f_kind != FK_NONE;
+        L.fr[lane] = make_int4((int32_t)B.i, B.w0 | (f_kind << 24), f_x, f_slot);
+        L.trd[lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
+        sync_lds();
+        unsigned long long peers = __ballot(ev);             // the segment's records of lane's level
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            const unsigned long long m = __ballot(ev && ((f_lev >> bb) & 1));
+            peers &= ((f_lev >> bb) & 1) ? m : ~m;
+        }
+        const bool leader = ev && __builtin_ctzll(peers) == lane;
+        int err = 0;
+        if (leader) {
+            const int side = f_lev >> 7, price = f_lev & 127, li = side * LVP + price;
+            const bool was = check_bit(side ? s1l : s0l, side ? s1m : s0m, price);
+            int32_t head = -1, tail = -1;
+            int64_t toid = 0;
+            if (was) { const int2 ht = L.ht[li]; head = ht.x; tail = ht.y; toid = L.toid[li]; }
+            unsigned long long m = peers;
+            while (m) {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1;
+                const int4 f = L.fr[k];
+                const int kind = (f.y >> 24) & 3;
+                if (kind == FK_TAKE) {                        // tryMatch at one level (KP:237-261)
+                    const bool is_buy = (f.y & 0xFF) == BUY;
+                    const int32_t P = (f.y >> 8) & 0xFF;
+                    int32_t x = f.z, ms = head;
+                    uint32_t ntr = 0;
+                    bool moved = false;
+                    for (;;) {
+                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[ms]);
+                        const int4 n0 = nd[0], n1 = nd[1];
+                        if (!((x > 0 && is_buy) ? price <= P : price >= P)) break;   // KP:237 (H3)
+                        const int32_t ts = imin(x, n1.z);
+                        x -= ts;
+                        lane_emit(tpos, tlim, (uint32_t)f.x, ntr++, n0, n1.y < 0, price, ts, err);
+                        if (n1.z - ts != 0) { pool[ms].size = n1.z - ts; lane_dirty(ms); break; }
+                        lane_free(ms);                        // orders.delete (KP:243)
+                        if (n1.w < 0) { err = 2; break; }     // (the pass left quantity at this level)
+                        ms = n1.w;
+                        moved = true;
+                    }
+                    if (moved && err == 0) { pool[ms].prev = -1; lane_dirty(ms); }
+                    head = ms;
+                    L.fr[k] = make_int4((int32_t)ntr, 0, 0, 0);
+                } else if (kind == FK_REST) {                 // addOrder's rest (KP:205-221)
+                    const int4 id = L.trd[k];
+                    const int32_t slot = f.w;
+                    int32_t nprev = -1, hp = 0;
+                    int64_t poid = 0;
+                    if (head < 0) {
+                        head = slot;
+                    } else {
+                        pool[tail].next = slot;
+                        lane_dirty(tail);
+                        nprev = tail; poid = toid; hp = 1;
+                    }
+                    tail = slot;
+                    toid = mk64(id.x, id.y);
+                    const int32_t sidl = ((f.y >> 17) & 1) ? -g : g;
+                    KG int4* nd = reinterpret_cast<KG int4*>(&pool[slot]);
+                    nd[0] = id;
+                    nd[1] = make_int4(sidl, sidl < 0 ? -1 : 0, f.z, -1);
+                    nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
+                    nd[3] = make_int4(price, f.y & 0xFF, 1, 0);
+                    lane_dirty(slot);
+                    L.fr[k] = make_int4(0, hp, lo32(poid), hi32(poid));
+                } else {                                      // removeOrder's unlink (KP:297-320)
+                    const int32_t vs = f.w;
+                    const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[vs]);
+                    const int4 n1 = nd[1], n2 = nd[2], n3 = nd[3];
+                    const int32_t next = n1.w, prev = n2.z;
+                    const int64_t prev_oid = mk64(n2.x, n2.y);
+                    if (prev < 0 && next < 0) {
+                        head = -1; tail = -1;
+                    } else if (prev < 0) {
+                        head = next;
+                        pool[next].prev = -1;
+                        lane_dirty(next);
+                    } else if (next < 0) {
+                        tail = prev; toid = prev_oid;
+                        pool[prev].next = -1;
+                        lane_dirty(prev);
+                    } else {
+                        pool[prev].next = next;
+                        pool[next].prev = prev;
+                        pool[next].prev_oid = prev_oid;
+                        lane_dirty(prev);
+                        lane_dirty(next);
+                    }
+                    lane_free(vs);
+                    if (Sp->ledger_replay)                    // the removed order, for postRemoveAdjustments
+                        Sp->vic[f.x] = make_int4(price | ((n3.y == SELL ? SELL : BUY) << 8), n1.z, n1.y < 0 ? -g : g,
+                                                 n1.y < 0 ? -1 : 0);
+                    L.fr[k] = make_int4(0, 0, 0, 0);
+                }
+            }
+            L.ht[li] = make_int2(head, tail);
+            L.toid[li] = toid;
+        }
+        sync_lds();
+        if (__ballot(err != 0)) { die(err == 1 ? KME_E_CAPACITY : KME_E_DOMAIN, err == 1 ? KME_D_CAP_TRADES : KME_D_NPE_ORDER); return je; }
+        {
+            const int fsp = U32(L.gs[GS_FSP]);
+            if (fsp > FSTK) set_gs(GS_FSP, FSTK);
+        }
+        // per record: its results, its oid-table entry (the rest slot, or dead: KP:221)
+        const int4 fo = L.fr[lane];
+        if (inseg) {
+            o_ntr = f_kind == FK_TAKE ? fo.x : 0;
+            if (f_kind == FK_REST && fo.y) { o_act |= KME_OUT_HAS_PREV << 16; o_plo = fo.z; o_phi = fo.w; }
+            if (b_act == BUY || b_act == SELL) otab_final(cold().otab, B.tgt, f_kind == FK_REST ? f_slot : -1);
+        }
+        sync_lds();
+        return je;
+    }
+
     // ---------------- one record (MatchingEngine.process, KP:96-126)
     KDEV Out process(const Rec& r, const Lanes& B) {
         cur = r.i;
@@ -2041,6 +2388,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
     bool stop = false;
+    // fast segments (GroupWave::fast_segment): not for group 0 (one shared book, H4) nor once a
+    // size-0 order was ever submitted (C_SIZE0)
+    const bool fast = g != 0 && S.fast && !S.ctr[ci(C_SIZE0)];
+    uint32_t ftpos = 0, ftlim = 0;                          // this lane's trade scratch (fast segments)
     for (uint32_t k0 = b; k0 < e && !w.dead && !stop; k0 += 64) {
         KST(const unsigned long long tb0 = stamp();)
         const uint32_t k = k0 + lane;
@@ -2095,6 +2446,13 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         KST(w.acc[ST_BATCH] += stamp() - tb0;)
 #pragma nounroll
         for (int j = 0; j < nb; ++j) {
+            if (fast) {
+                KST(const unsigned long long tf0 = stamp(); const int jf0 = j;)
+                j = w.fast_segment(B, j, nb, o_act, o_size, o_plo, o_phi, o_ntr, ftpos, ftlim);
+                KST(w.acc[ST_FAST] += stamp() - tf0; w.acc[ST_N_FAST_REC] += (unsigned long long)(j - jf0); w.acc[ST_N_FAST_SEG] += j > jf0;)
+                if (w.dead) { done = j; break; }
+                if (j >= nb) break;
+            }
             KST(const unsigned long long tr0 = stamp();)
             Rec r;
             r.i = (uint32_t)rl32((int32_t)B.i, j);
@@ -2143,6 +2501,7 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
     }
     KST(const unsigned long long to0 = stamp();)
     w.flush_trades();
+    for (uint32_t q = ftpos; q < ftlim; ++q) S.ttmp[q].seq = -1;   // the fast segments' unused reservations
     KST(w.acc[ST_FLUSH] += stamp() - to0;)
     w.store_group();
     KG unsigned long long* tsh = w.tsh();

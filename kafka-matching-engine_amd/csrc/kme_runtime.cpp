@@ -228,7 +228,10 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     // to 2 LANE_TCH - 1 unused per light group, at most min(G, E) of them), and a reservation that
     // straddles a shard region's end leaves the straddled part as holes (at most one per shard and
     // matcher)
-    const uint64_t lane_waste = (uint64_t)(2 * kLaneTradeChunk - 1) * std::min<uint64_t>(G, E);
+    // (k_match's fast segments reserve the same way per lane of a busy group: up to 64 partly used
+    // reservations per group)
+    const uint64_t lane_waste = (uint64_t)(2 * kLaneTradeChunk - 1) * std::min<uint64_t>(G, E) +
+                                (uint64_t)64 * (kLaneTradeChunk - 1) * std::min<uint64_t>(G, E);
     const uint64_t ttmp_ov = funded ? (uint64_t)cfg->max_trades + 64 + lane_waste + 64ull * TSHARDS : 1;
     const uint64_t tshard_cap = funded ? std::max<uint64_t>(256, (2 * (uint64_t)cfg->max_trades + TSHARDS - 1) / TSHARDS) : 0;
     const uint64_t ttmp_total = ttmp_ov + (uint64_t)TSHARDS * tshard_cap;
@@ -276,7 +279,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     // OUT echo: one 16-B record per input index, stored by the matching kernels where the record
     // arrived (k_unsort then reads it sequentially; no sorted-position map)
     S.os_base = E;
-    S.os_lanes = 0;
+    S.fast = 1;
+    if (const char* v = std::getenv("KME_FAST")) S.fast = std::atoi(v) != 0;   // A/B diagnostics
     if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
@@ -897,6 +901,12 @@ kme_status kme_restore(kme_engine* e, const char* path) {
     ctr[ci(C_OTAB_USED)] = h.otab_used;
     ctr[ci(C_BAL_USED)] = h.bal_used;
     ctr[ci(C_POS_USED)] = h.pos_used;
+    {   // a restored book may hold size-0 makers: then the fast segments stay off (C_SIZE0)
+        const Node* nodes = reinterpret_cast<const Node*>(host[2].data());
+        ctr[ci(C_SIZE0)] = 0;
+        for (uint64_t k = 0; k < h.pool_used; ++k)
+            if (nodes[k].live && nodes[k].size == 0) { ctr[ci(C_SIZE0)] = 1; break; }
+    }
     HIP_TRY(hipMemcpy(e->S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
     e->seq_base = h.seq_base;
     return KME_OK;
