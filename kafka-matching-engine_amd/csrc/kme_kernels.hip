@@ -901,8 +901,8 @@ struct Rec {
     int64_t oid, aid, sid, tgt;
     int32_t lane;                 // lane of the record in its batch
 };
-constexpr uint32_t OS_MAX_NTR = 1u << 23;   // trades of one record the packed OUT echo (osort) can count
-static_assert(OS_MAX_NTR == 1u << TT_ORD_BITS, "a trade's ordinal in TradeTmp::ordp");
+constexpr uint32_t OS_MAX_NTR = 1u << FAST_RANK_SHIFT;   // trades of one record: a plain ordinal in TradeTmp::ordp
+static_assert(FAST_RANK_SHIFT + 3 <= TT_ORD_BITS, "a fast segment's ordinal (index | event rank << 20) in TradeTmp::ordp");
 // What process() decided for one record (the OUT echo fields and its trade count).
 struct Out {
     int32_t action, size;
@@ -1413,6 +1413,7 @@ constexpr int LVP = 101;          // LDS level entries per book side: prices 0..
 constexpr int FSTK = 128;         // LDS free-slot stack
 constexpr int TRD = 32;           // trades staged in LDS between reservations (GroupWave::emit)
 constexpr int DIRTY_WORDS = 64;   // 2048-bit filter of node slots written since the batch prefetch
+constexpr int FAST_EVCAP = 128;   // events of one fast segment (GroupWave::fast_segment)
 
 struct GroupLds {
     int2 ht[2 * LVP];             // head / tail node slot of level (side, price)
@@ -1424,8 +1425,9 @@ struct GroupLds {
     int32_t gs[8];                // exists, free-list head block, bump chunk next / end, free-stack top, staged trades
     int4 trd[2 * TRD];            // trade k: (maker oid, maker aid), (price | sid < 0 << 8, size, seq, ord);
                                   // during a fast segment (emptied first): record k's (oid, aid) at trd[k]
-    int4 fr[64];                  // fast segment: record k's (input index, PRec w0 | kind << 24, size, slot),
-                                  // then its results (trades, has_prev, prev)
+    int4 rin[64];                 // fast segment: record k's (input index, PRec w0, rest size, -)
+    int4 ev[FAST_EVCAP];          // fast segment: its events in arrival order (GroupWave::fast_segment), then
+                                  // their results (trades; has_prev, prev oid)
 };
 
 KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1503,6 +1505,7 @@ struct Lanes {
     int32_t w0, size, tgt;        // PRec word 0 (action | price << 8 | acct_ok << 16 | sid < 0 << 17)
     int64_t oid, aid;
     int32_t pf_slot, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10 | ok << 11
+                                                           // (pf_slot < 0: the raw oid-table entry of this epoch's target)
     int64_t pf_poid;
 };
 
@@ -1511,7 +1514,7 @@ enum Stamp : int {
     ST_GROUP_IN = 0, ST_BATCH, ST_TRADE_REC, ST_REST_REC, ST_CANCEL_REC, ST_OTHER_REC, ST_GROUP_OUT, ST_KERNEL,
     ST_N_TRADE_REC, ST_N_REST_REC, ST_N_CANCEL_REC, ST_MAKER_WAIT, ST_N_MAKER, ST_VICTIM_WAIT, ST_N_VICTIM, ST_FLUSH,
     ST_REST_ALLOC, ST_REST_LEVEL, ST_REST_NODE, ST_REC_PICK, ST_REC_OUT, ST_TM_PRE, ST_REST_PRE,
-    ST_FAST, ST_N_FAST_REC, ST_N_FAST_SEG, ST_FAST_PASS,
+    ST_FAST, ST_N_FAST_REC, ST_N_FAST_SEG, ST_FAST_PASS, ST_FAST_DRAIN, ST_FAST_LEVEL, ST_FAST_EPI,
     ST_N = 32
 };
 
@@ -1980,22 +1983,62 @@ struct GroupWave {
     // two steps:
     //   1. the aggregate pass (scalar, one record at a time, no node access): what each record does
     //      to the book's LEVELS -- the level bitmaps (Books, KP:38-41) and each level's resting
-    //      quantity -- decides its outcome: a BUY/SELL that crosses takes its whole size from the
-    //      best opposite level (KP:225-263) or rests at its price (KP:200-223), a cancel removes its
-    //      prefetched victim's quantity (KP:289-323);
-    //   2. the level step (vector): every level the segment touched is replayed by one lane, its
-    //      records in arrival order -- appends at the tail, takes walking the FIFO from the head
-    //      maker by maker exactly as KP:237-261 does (H3 zero-size trades included), unlinks -- so
-    //      the touched levels' node work runs side by side instead of record after record.
-    // Levels are independent once step 1 fixed every record's level and amount, so the result is
-    // the reference's.  The pass stops (the record goes to the serial path) where that does not
-    // hold: a take that would empty its level (the sweep continues at the next level, or its end
-    // decides a zero-size trade against another level's head), a cancel whose level was already
-    // taken from in the segment or whose victim is not prefetched (an order of this batch, or a node
-    // written since), a price scan that would fault (H5), any other action; and the fast path is off
-    // for group 0 (H4: one shared book) and once a size-0 order was ever submitted (C_SIZE0: a level's
-    // emptiness is then not its quantity being 0).
-    enum { FK_NONE = 0, FK_TAKE = 1, FK_REST = 2, FK_CANCEL = 3 };
+    //      quantity -- decides its outcome.  A BUY/SELL sweeps the opposite levels best first
+    //      (KP:225-263), taking min(remaining, level quantity) from each while the level crosses;
+    //      a level taken whole is unset and the next best one is scanned exactly as KP:244-252 does
+    //      (with its H5 bit check); a sweep that ends exactly on an emptied level decides the
+    //      zero-size trade against the next level's head (KP:237's loop test with size 0, H3); the
+    //      remainder rests at its price (KP:200-223).  A cancel removes its victim's quantity
+    //      (KP:289-323): a victim prefetched with the batch, or an order that rested earlier in the
+    //      segment.  Each effect on one level is an EVENT (take, zero trade, rest, unlink);
+    //   2. the level step (vector): the segment's events grouped by level, one lane per level,
+    //      replayed in arrival order -- appends at the tail, takes walking the FIFO from the head
+    //      maker by maker as KP:237-261 does (H3 zero-size trades at a level's maker boundary
+    //      included), unlinks -- so the touched levels' node work runs side by side.
+    // Levels are independent once step 1 fixed every event's level and amount, so the result is the
+    // reference's.  A record's trades keep their reference order: the trades of its k-th event
+    // carry ordinal (index | k << 20) and the epilogue stores the record's per-event bases
+    // (DevState::lvbase) for k_scatter.  The pass stops (the record goes to the serial path) where a
+    // record's effect is not decided by levels alone: a sweep over more than FAST_RMAX levels, a
+    // price scan that faults (H5), a cancel whose level was already taken from in the segment or
+    // whose victim was written since the batch prefetch or decided before the segment, admin
+    // actions, a full event buffer; and the fast path is off for group 0 (H4: one shared book) and
+    // once a size-0 order was ever submitted (C_SIZE0: a level's emptiness is then not its quantity
+    // being 0).
+    enum { EK_TAKE = 0, EK_REST = 1, EK_CANCEL = 2, EK_ZERO = 3 };
+    static constexpr int FAST_RMAX = FAST_LVB;       // levels one sweep may take from in a segment (its
+                                                     // zero trade is event rank FAST_RMAX at most)
+    static constexpr int32_t RR_REMOVED = 1 << 24;   // rr flag: rested in the segment, then cancelled in it
+    // lane l of the result is v, the others old's (v_cmp + v_cndmask; v scalar)
+    KDEV static int32_t wlane(int32_t v, int l, int32_t old) { return lane_id() == l ? v : old; }
+    // The pass's level quantities: lane l of Ql<k> / Qh<k> (k = 2 * side + h) holds the low / high word
+    // of level (side, 64 * h + l) -- read and written with readlane / lane selects, no LDS round trip
+    // (the 8 words are locals of fast_segment: a struct behind a reference becomes a dynamically
+    // indexed stack array, scratch memory)
+#define KME_QGET(s, p) mk64(rl32((s) ? ((p) < 64 ? Ql2 : Ql3) : ((p) < 64 ? Ql0 : Ql1), (p) & 63), \
+                            rl32((s) ? ((p) < 64 ? Qh2 : Qh3) : ((p) < 64 ? Qh0 : Qh1), (p) & 63))
+#define KME_QSET(s, p, v)                                                                              \
+    do {                                                                                               \
+        const int _k = (s) * 2 + ((p) >= 64 ? 1 : 0), _l = (p) & 63;                                   \
+        const int64_t _v = (v);                                                                        \
+        const int32_t _lo = lo32(_v), _hi = hi32(_v);                                                  \
+        Ql0 = wlane(_lo, _k == 0 ? _l : -1, Ql0); Qh0 = wlane(_hi, _k == 0 ? _l : -1, Qh0);            \
+        Ql1 = wlane(_lo, _k == 1 ? _l : -1, Ql1); Qh1 = wlane(_hi, _k == 1 ? _l : -1, Qh1);            \
+        Ql2 = wlane(_lo, _k == 2 ? _l : -1, Ql2); Qh2 = wlane(_hi, _k == 2 ? _l : -1, Qh2);            \
+        Ql3 = wlane(_lo, _k == 3 ? _l : -1, Ql3); Qh3 = wlane(_hi, _k == 3 ? _l : -1, Qh3);            \
+    } while (0)
+    // events of the pass: event e in lane e & 63 of Ex0, Ev0 / Ex1, Ev1 (e >> 6): x = record lane |
+    // kind << 6 | rank << 8 | level (side * 128 + price) << 16 | P << 24, v = the amount taken (a take)
+    // or the node slot (a rest, an unlink)
+#define KME_PUT_EV(e, k, kind, rank, lev, P, v)                                                        \
+    do {                                                                                               \
+        const int32_t _x = (k) | ((kind) << 6) | ((rank) << 8) | ((lev) << 16) | ((P) << 24);          \
+        const int _e = (e), _l0 = _e < 64 ? _e : -1, _l1 = _e >= 64 ? _e - 64 : -1;                    \
+        const int32_t _v = (v);                                                                        \
+        Ex0 = wlane(_x, _l0, Ex0); Ev0 = wlane(_v, _l0, Ev0);                                          \
+        Ex1 = wlane(_x, _l1, Ex1); Ev1 = wlane(_v, _l1, Ev1);                                          \
+    } while (0)
+    enum { PC_TAKE_REST = 0, PC_REJECT = 1, PC_CANCEL_PF = 2, PC_CANCEL_BATCH = 3, PC_SERIAL = 4 };
 
     // fstack holds at least n slots (n <= 64): free-list blocks, then the bump chunk
     KDEV void fast_refill(int n) {
@@ -2037,6 +2080,7 @@ struct GroupWave {
     // group's shard line, unused ones left as holes (seq = -1) that k_scatter skips
     KDEV void lane_emit(uint32_t& tpos, uint32_t& tlim, uint32_t seq, uint32_t ord, int4 maker, int32_t msneg,
                         int32_t mprice, int32_t ts, int& err) {
+        if (err) return;
         if (tpos == tlim) {
             const DevState& S = *Sp;
             const uint32_t tcap = S.tshard_cap, tb = (uint32_t)(g & (TSHARDS - 1)) * tcap;
@@ -2089,106 +2133,196 @@ struct GroupWave {
                           int32_t& o_phi, int32_t& o_ntr, uint32_t& tpos, uint32_t& tlim) {
         const bool inrange = lane >= j0 && lane < nb;
         const int32_t b_act = B.w0 & 0xFF;
-        const int n_bs = (int)__popcll(__ballot(inrange && (b_act == BUY || b_act == SELL)));
+        const bool b_bs = b_act == BUY || b_act == SELL;
+        const int n_bs = (int)__popcll(__ballot(inrange && b_bs));
         if (gsv(GS_TCNT)) flush_trades();                     // trd is the segment's staging
         fast_refill(n_bs);
         if (dead) return j0;
         const int fsp0 = gsv(GS_FSP);
         const int32_t fslot = lane < n_bs ? L.fstack[fsp0 - 1 - lane] : -1;   // the k-th rest takes lane k's
-        // the level bitmaps as the segment starts (the level step's "was the level occupied")
-        const uint64_t s0l = bl(0), s0m = bm(0), s1l = bl(1), s1m = bm(1);
-        uint64_t b0l = s0l, b0m = s0m, b1l = s1l, b1m = s1m;
-        uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;         // levels taken from in the segment
+        uint64_t b0l = bl(0), b0m = bm(0), b1l = bl(1), b1m = bm(1);
+        // the level quantities into lanes; levels unoccupied as the segment starts read as empty in
+        // the level step
+        int64_t qv[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int sd = h >> 1, p = lane + 64 * (h & 1);
+            const bool occ = p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p);
+            qv[h] = occ ? L.qty[sd * LVP + p] : 0;
+            if (p <= 100 && !occ) L.ht[sd * LVP + p] = make_int2(-1, -1);
+        }
+        int32_t Ql0 = lo32(qv[0]), Ql1 = lo32(qv[1]), Ql2 = lo32(qv[2]), Ql3 = lo32(qv[3]);
+        int32_t Qh0 = hi32(qv[0]), Qh1 = hi32(qv[1]), Qh2 = hi32(qv[2]), Qh3 = hi32(qv[3]);
+        // each record's class, decided per lane before the serial pass: pk = class | BUY << 4 | P << 8 |
+        // action << 16 | victim level << 24 (a prefetched cancel's).  A BUY/SELL with a negative sid
+        // (its side is the other book, KP:201) takes the serial path.
         const int exists = gsv(GS_EXISTS);
-        int32_t f_kind = FK_NONE, f_lev = 0, f_x = 0, f_slot = -1;
-        int nrest = 0;
+        int32_t pk;
+        {
+            const int32_t P = (B.w0 >> 8) & 0xFF;
+            int cls = PC_SERIAL, vlev = 0;
+            if (b_bs) {
+                cls = !(exists && ((B.w0 >> 16) & 1)) ? PC_REJECT
+                      : (B.size <= 0 || ((B.w0 >> 17) & 1) ? PC_SERIAL : PC_TAKE_REST);
+            } else if (b_act == CANCEL) {
+                if (B.tgt == -1) {
+                    cls = PC_REJECT;                          // orders.get(oid) == null (KP:290)
+                } else if (B.pf_slot >= 0) {                  // a victim resting before the batch
+                    const bool dirty = (L.dirty[(B.pf_slot >> 5) & (DIRTY_WORDS - 1)] >> (B.pf_slot & 31)) & 1;
+                    if (!((B.pf_meta >> 11) & 1)) cls = PC_REJECT;   // gone / another account's (KP:290-291)
+                    else cls = dirty || !exists ? PC_SERIAL : PC_CANCEL_PF;   // written since the prefetch /
+                    vlev = ((B.pf_meta >> 8) & 1) * 128 + (B.pf_meta & 0xFF);  // KP:294's NPE: serial
+                } else {                                      // an order of this epoch not final at the prefetch
+                    cls = (uint32_t)B.pf_meta == OT_DEAD ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
+                }
+            }
+            pk = cls | (b_act == BUY ? 16 : 0) | (P << 8) | (b_act << 16) | (vlev << 24);
+        }
+        uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;         // levels taken from in the segment
+        int32_t f_vslot = -1;                                 // lane j: the prefetched victim record j removes
+        int32_t Ex0 = 0, Ex1 = 0, Ev0 = 0, Ev1 = 0;
+        int nrest = 0, nev = 0;
         int j = j0;
+        int32_t oact = 0, osize = 0, flags = 0, rslot = -1, rlev = 0;
+        // A BUY (IB) or SELL of sid +g: takes from book side 1 - SIDE, rests on SIDE (KP:201, 292).
+        // Returns false where the record goes to the serial path.
+        auto take_rest = [&](auto ib_tag) -> bool {
+            constexpr bool IB = decltype(ib_tag)::value;
+            constexpr int SIDE = IB ? 0 : 1, OS = 1 - SIDE;
+            uint64_t& olo = OS ? b1l : b0l;
+            uint64_t& ohi = OS ? b1m : b0m;
+            uint64_t& slo = SIDE ? b1l : b0l;
+            uint64_t& shi = SIDE ? b1m : b0m;
+            uint64_t& col = OS ? c1l : c0l;
+            uint64_t& coh = OS ? c1m : c0m;
+            const int32_t P = (rl32(pk, j) >> 8) & 0xFF;
+            int32_t rem = rl32(B.size, j);
+            int32_t pb = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
+            if (pb != -1 && !check_bit(olo, ohi, pb)) return false;   // the H5 NPE: the serial path raises it
+            if (pb != -1 && crosses(IB, rem, pb, P)) {
+                const int64_t q = KME_QGET(OS, pb);
+                if ((int64_t)rem < q) {                        // the best level absorbs it (KP:237-261)
+                    if (nev + 1 > FAST_EVCAP) return false;
+                    KME_QSET(OS, pb, q - rem);
+                    if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
+                    KME_PUT_EV(nev++, j, EK_TAKE, 0, OS * 128 + pb, P, rem);
+                    rem = 0;
+                } else {                                       // a sweep: dry run, then commit
+                    uint64_t lo = olo, hi = ohi;
+                    int32_t r = rem, p = pb, nt = 0, zl = -1;
+                    bool bad = false;
+#pragma nounroll
+                    for (;;) {                                 // KP:237-253
+                        if (nt == FAST_RMAX) { bad = true; break; }
+                        const int64_t qq = KME_QGET(OS, p);
+                        const int32_t x = qq < (int64_t)r ? (int32_t)qq : r;
+                        r -= x;
+                        ++nt;
+                        if ((int64_t)x < qq) break;            // stops inside the level
+                        unset_bit(lo, hi, p);                  // taken whole (KP:244-252)
+                        const int32_t np = IB ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
+                        if (np != -1 && !check_bit(lo, hi, np)) { bad = true; break; }   // H5
+                        if (r == 0) { if (np != -1 && np >= P) zl = np; break; }        // H3 zero trade
+                        if (np == -1 || !crosses(IB, r, np, P)) break;
+                        p = np;
+                    }
+                    if (bad || nev + nt + (zl >= 0) + (r > 0) > FAST_EVCAP) return false;
+#pragma nounroll
+                    for (int t = 0; t < nt; ++t) {
+                        const int64_t qq = KME_QGET(OS, pb);
+                        const int32_t x = qq < (int64_t)rem ? (int32_t)qq : rem;
+                        rem -= x;
+                        KME_QSET(OS, pb, qq - x);
+                        if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
+                        KME_PUT_EV(nev++, j, EK_TAKE, t, OS * 128 + pb, P, x);
+                        if ((int64_t)x == qq) {
+                            unset_bit(olo, ohi, pb);
+                            pb = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
+                        }
+                    }
+                    if (zl >= 0) KME_PUT_EV(nev++, j, EK_ZERO, nt, OS * 128 + zl, P, 0);
+                }
+            }
+            if (rem > 0) {                                     // addOrder (KP:200-223)
+                if (nev + 1 > FAST_EVCAP) return false;       // (only when nothing was taken: rem == size)
+                const int64_t q = check_bit(slo, shi, P) ? KME_QGET(SIDE, P) : 0;
+                KME_QSET(SIDE, P, q + rem);
+                set_bit(slo, shi, P);
+                rslot = rl32(fslot, nrest);
+                ++nrest;
+                rlev = SIDE * 128 + P;
+                KME_PUT_EV(nev++, j, EK_REST, 0, rlev, P, rslot);
+                flags = 2;
+            }
+            osize = rem;
+            return true;
+        };
+        // (stamps builds: the wait for this wavefront's outstanding vector memory operations, timed
+        // apart from the pass)
+        KST(const unsigned long long td0 = stamp(); __builtin_amdgcn_s_waitcnt(VMCNT0); acc[ST_FAST_DRAIN] += stamp() - td0;)
         KST(const unsigned long long tp0 = stamp();)
-        // ---- 1. the aggregate pass
+        // ---- 1. the aggregate pass.  Per record: its class and fields by readlane, its events and
+        // results by lane selects (results: o_act = action | flags << 16, o_size, o_plo = first event |
+        // events << 8 | rest level << 16, o_phi = rest slot; the epilogue replaces the last two).
 #pragma nounroll
         for (; j < nb; ++j) {
-            const int32_t w0 = rl32(B.w0, j);
-            const int32_t a = w0 & 0xFF, P = (w0 >> 8) & 0xFF;
-            const int32_t sz = rl32(B.size, j);
-            int kind = FK_NONE, lev = 0, x = 0, slot = -1, rested = 0;
-            int32_t oact = a, osize = sz;
-            if (a == BUY || a == SELL) {
-                if (exists && ((w0 >> 16) & 1)) {
-                    if (sz <= 0) break;
-                    const bool is_buy = a == BUY;
-                    const int side = (((w0 >> 17) & 1) != (is_buy ? 0 : 1)) ? 1 : 0;   // book_side, g != 0
-                    const int os = 1 - side;
-                    const uint64_t lo = os ? b1l : b0l, hi = os ? b1m : b0m;
-                    const int32_t pb = is_buy ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
-                    bool take = false;
-                    if (pb != -1) {
-                        if (!check_bit(lo, hi, pb)) break;    // the H5 NPE: the serial path raises it
-                        take = crosses(is_buy, sz, pb, P);
-                    }
-                    if (take) {
-                        const int li = os * LVP + pb;
-                        const int64_t q = U64(L.qty[li]);
-                        if ((int64_t)sz >= q) break;          // empties the level: the serial path
-                        L.qty[li] = q - sz;
-                        const uint64_t bit = 1ull << (pb & 63);
-                        if (os) { if (pb < 64) c1l |= bit; else c1m |= bit; }
-                        else { if (pb < 64) c0l |= bit; else c0m |= bit; }
-                        kind = FK_TAKE; lev = os * 128 + pb; x = sz; osize = 0;
-                    } else {
-                        const int li = side * LVP + P;
-                        uint64_t lo2 = side ? b1l : b0l, hi2 = side ? b1m : b0m;
-                        const int64_t q = check_bit(lo2, hi2, P) ? U64(L.qty[li]) : 0;
-                        L.qty[li] = q + sz;
-                        set_bit(lo2, hi2, P);
-                        if (side) { b1l = lo2; b1m = hi2; } else { b0l = lo2; b0m = hi2; }
-                        slot = rl32(fslot, nrest);
-                        ++nrest;
-                        kind = FK_REST; lev = side * 128 + P; x = sz; rested = 1;
-                    }
-                } else {
-                    oact = REJECT;                            // books.get == null / balances.get == null
-                }
-            } else if (a == CANCEL) {
-                const int32_t tgt = rl32(B.tgt, j);
-                if (tgt == -1) {
-                    oact = REJECT;                            // orders.get(oid) == null (KP:290)
-                } else {
+            const int32_t pj = rl32(pk, j);
+            const int cls = pj & 7;
+            if (cls == PC_SERIAL) break;
+            oact = (pj >> 16) & 0xFF; osize = 0; flags = 0; rslot = -1; rlev = 0;
+            const int evb = nev;
+            if (cls == PC_TAKE_REST) {
+                const bool ok = (pj >> 4) & 1 ? take_rest(std::true_type()) : take_rest(std::false_type());
+                if (!ok) break;
+            } else if (cls == PC_REJECT) {
+                oact = REJECT;                                // (KP:100-104, 290-291)
+                osize = rl32(B.size, j);
+            } else {                                          // removeOrder (KP:289-323)
+                int32_t vlev = -1, vsl = -1, vsz = 0, vrec = -1;
+                if (cls == PC_CANCEL_PF) {
                     const int32_t pfs = rl32(B.pf_slot, j);
-                    if (pfs < 0 || is_dirty(pfs)) break;      // not prefetched, or written since: serial
-                    const int32_t meta = rl32(B.pf_meta, j);
-                    if (!((meta >> 11) & 1)) {
-                        oact = REJECT;                        // gone, or another account's (KP:290-291)
-                    } else if (__ballot(f_kind == FK_CANCEL && f_slot == pfs)) {
+                    if (__ballot(f_vslot == pfs)) {
                         oact = REJECT;                        // removed by an earlier cancel of the segment
                     } else {
-                        if (!exists) break;                   // NPE (KP:294): the serial path raises it
-                        const int vp = meta & 0xFF, vs = (meta >> 8) & 1;
-                        const uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
-                        if ((cw >> (vp & 63)) & 1) break;     // its level was taken from: serial
-                        const int li = vs * LVP + vp;
-                        const int64_t q = U64(L.qty[li]) - rl32(B.pf_size, j);
-                        L.qty[li] = q;
-                        if (q == 0) {
-                            uint64_t lo2 = vs ? b1l : b0l, hi2 = vs ? b1m : b0m;
-                            unset_bit(lo2, hi2, vp);
-                            if (vs) { b1l = lo2; b1m = hi2; } else { b0l = lo2; b0m = hi2; }
-                        }
-                        kind = FK_CANCEL; lev = vs * 128 + vp; slot = pfs;
+                        vlev = (pj >> 24) & 0xFF;
+                        vsl = pfs;
+                        vsz = rl32(B.pf_size, j);
+                    }
+                } else {                                      // pending: a BUY/SELL of this batch
+                    const uint32_t ti = (uint32_t)rl32(B.pf_meta, j) & ~OT_PENDING;
+                    const uint64_t hit = __ballot(lane < nb && B.i == ti);
+                    if (!hit) break;
+                    const int jt = __builtin_ctzll(hit);
+                    if (jt < j0 || jt >= j) break;            // decided before the segment: serial
+                    const int32_t rx = rl32(o_act, jt);
+                    if (!((rx >> 16) & 2) || (rx & RR_REMOVED) || rl64(B.aid, jt) != rl64(B.aid, j)) {
+                        oact = REJECT;                        // traded away, removed, another account's
+                    } else {
+                        vlev = (rl32(o_plo, jt) >> 16) & 0xFF;
+                        vsl = rl32(o_phi, jt);
+                        vsz = rl32(o_size, jt);
+                        vrec = jt;
                     }
                 }
-            } else {
-                break;                                        // symbol admin / unknown: serial
+                if (vlev >= 0) {
+                    if (nev + 1 > FAST_EVCAP) break;
+                    const int vs = vlev >> 7, vp = vlev & 127;
+                    const uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
+                    if ((cw >> (vp & 63)) & 1) break;         // its level was taken from: serial
+                    const int64_t q = KME_QGET(vs, vp) - vsz;
+                    KME_QSET(vs, vp, q);
+                    if (q == 0) {
+                        if (vs) unset_bit(b1l, b1m, vp); else unset_bit(b0l, b0m, vp);
+                    }
+                    if (vrec >= 0) o_act = wlane(rl32(o_act, vrec) | RR_REMOVED, vrec, o_act);
+                    else f_vslot = wlane(vsl, j, f_vslot);
+                    KME_PUT_EV(nev++, j, EK_CANCEL, 0, vlev, 0, vsl);
+                }
             }
-            const bool me = lane == j;
-            f_kind = me ? kind : f_kind;
-            f_lev = me ? lev : f_lev;
-            f_x = me ? x : f_x;
-            f_slot = me ? slot : f_slot;
-            o_act = me ? ((oact & 0xFFFF) | (rested << 17)) : o_act;
-            o_size = me ? osize : o_size;
-            o_plo = me ? 0 : o_plo;
-            o_phi = me ? 0 : o_phi;
-            o_ntr = me ? 0 : o_ntr;
+            o_act = wlane((oact & 0xFFFF) | (flags << 16), j, o_act);
+            o_size = wlane(osize, j, o_size);
+            o_plo = wlane(evb | ((nev - evb) << 8) | (rlev << 16), j, o_plo);
+            o_phi = wlane(rslot, j, o_phi);
         }
         const int je = j;
         KST(acc[ST_FAST_PASS] += stamp() - tp0;)
@@ -2196,123 +2330,166 @@ struct GroupWave {
         set_bm(0, b0l, b0m);
         set_bm(1, b1l, b1m);
         set_gs(GS_FSP, fsp0 - nrest);
-        // ---- 2. the level step
-        const bool inseg = lane >= j0 && lane < je;
-        const bool ev = inseg && f_kind != FK_NONE;
-        L.fr[lane] = make_int4((int32_t)B.i, B.w0 | (f_kind << 24), f_x, f_slot);
-        L.trd[lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
-        sync_lds();
-        unsigned long long peers = __ballot(ev);             // the segment's records of lane's level
+        qv[0] = mk64(Ql0, Qh0); qv[1] = mk64(Ql1, Qh1); qv[2] = mk64(Ql2, Qh2); qv[3] = mk64(Ql3, Qh3);
 #pragma unroll
-        for (int bb = 0; bb < 8; ++bb) {
-            const unsigned long long m = __ballot(ev && ((f_lev >> bb) & 1));
-            peers &= ((f_lev >> bb) & 1) ? m : ~m;
+        for (int h = 0; h < 4; ++h) {                         // quantities back (occupied levels)
+            const int sd = h >> 1, p = lane + 64 * (h & 1);
+            if (p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = qv[h];
         }
-        const bool leader = ev && __builtin_ctzll(peers) == lane;
-        int err = 0;
-        if (leader) {
-            const int side = f_lev >> 7, price = f_lev & 127, li = side * LVP + price;
-            const bool was = check_bit(side ? s1l : s0l, side ? s1m : s0m, price);
-            int32_t head = -1, tail = -1;
-            int64_t toid = 0;
-            if (was) { const int2 ht = L.ht[li]; head = ht.x; tail = ht.y; toid = L.toid[li]; }
-            unsigned long long m = peers;
-            while (m) {
-                const int k = __builtin_ctzll(m);
-                m &= m - 1;
-                const int4 f = L.fr[k];
-                const int kind = (f.y >> 24) & 3;
-                if (kind == FK_TAKE) {                        // tryMatch at one level (KP:237-261)
-                    const bool is_buy = (f.y & 0xFF) == BUY;
-                    const int32_t P = (f.y >> 8) & 0xFF;
-                    int32_t x = f.z, ms = head;
-                    uint32_t ntr = 0;
-                    bool moved = false;
-                    for (;;) {
-                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[ms]);
-                        const int4 n0 = nd[0], n1 = nd[1];
-                        if (!((x > 0 && is_buy) ? price <= P : price >= P)) break;   // KP:237 (H3)
-                        const int32_t ts = imin(x, n1.z);
-                        x -= ts;
-                        lane_emit(tpos, tlim, (uint32_t)f.x, ntr++, n0, n1.y < 0, price, ts, err);
-                        if (n1.z - ts != 0) { pool[ms].size = n1.z - ts; lane_dirty(ms); break; }
-                        lane_free(ms);                        // orders.delete (KP:243)
-                        if (n1.w < 0) { err = 2; break; }     // (the pass left quantity at this level)
-                        ms = n1.w;
-                        moved = true;
-                    }
-                    if (moved && err == 0) { pool[ms].prev = -1; lane_dirty(ms); }
-                    head = ms;
-                    L.fr[k] = make_int4((int32_t)ntr, 0, 0, 0);
-                } else if (kind == FK_REST) {                 // addOrder's rest (KP:205-221)
-                    const int4 id = L.trd[k];
-                    const int32_t slot = f.w;
-                    int32_t nprev = -1, hp = 0;
-                    int64_t poid = 0;
-                    if (head < 0) {
-                        head = slot;
-                    } else {
-                        pool[tail].next = slot;
-                        lane_dirty(tail);
-                        nprev = tail; poid = toid; hp = 1;
-                    }
-                    tail = slot;
-                    toid = mk64(id.x, id.y);
-                    const int32_t sidl = ((f.y >> 17) & 1) ? -g : g;
-                    KG int4* nd = reinterpret_cast<KG int4*>(&pool[slot]);
-                    nd[0] = id;
-                    nd[1] = make_int4(sidl, sidl < 0 ? -1 : 0, f.z, -1);
-                    nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
-                    nd[3] = make_int4(price, f.y & 0xFF, 1, 0);
-                    lane_dirty(slot);
-                    L.fr[k] = make_int4(0, hp, lo32(poid), hi32(poid));
-                } else {                                      // removeOrder's unlink (KP:297-320)
-                    const int32_t vs = f.w;
-                    const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[vs]);
-                    const int4 n1 = nd[1], n2 = nd[2], n3 = nd[3];
-                    const int32_t next = n1.w, prev = n2.z;
-                    const int64_t prev_oid = mk64(n2.x, n2.y);
-                    if (prev < 0 && next < 0) {
-                        head = -1; tail = -1;
-                    } else if (prev < 0) {
-                        head = next;
-                        pool[next].prev = -1;
-                        lane_dirty(next);
-                    } else if (next < 0) {
-                        tail = prev; toid = prev_oid;
-                        pool[prev].next = -1;
-                        lane_dirty(prev);
-                    } else {
-                        pool[prev].next = next;
-                        pool[next].prev = prev;
-                        pool[next].prev_oid = prev_oid;
-                        lane_dirty(prev);
-                        lane_dirty(next);
-                    }
-                    lane_free(vs);
-                    if (Sp->ledger_replay)                    // the removed order, for postRemoveAdjustments
-                        Sp->vic[f.x] = make_int4(price | ((n3.y == SELL ? SELL : BUY) << 8), n1.z, n1.y < 0 ? -g : g,
-                                                 n1.y < 0 ? -1 : 0);
-                    L.fr[k] = make_int4(0, 0, 0, 0);
-                }
-            }
-            L.ht[li] = make_int2(head, tail);
-            L.toid[li] = toid;
-        }
+        // ---- 2. the level step, 64 events at a time
+        KST(const unsigned long long tl0 = stamp();)
+        L.trd[lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
+        L.rin[lane] = make_int4((int32_t)B.i, B.w0, o_size, 0);
+        L.ev[lane] = make_int4(Ex0, Ev0, Ev0, 0);
+        if (nev > 64) L.ev[64 + lane] = make_int4(Ex1, Ev1, Ev1, 0);
         sync_lds();
-        if (__ballot(err != 0)) { die(err == 1 ? KME_E_CAPACITY : KME_E_DOMAIN, err == 1 ? KME_D_CAP_TRADES : KME_D_NPE_ORDER); return je; }
+        int err = 0;
+#pragma nounroll
+        for (int c0 = 0; c0 < nev; c0 += 64) {
+            const int e = c0 + lane;
+            const bool ve = e < nev;
+            const int lev = ((c0 ? Ex1 : Ex0) >> 16) & 0xFF;
+            unsigned long long peers = __ballot(ve);          // the chunk's events at lane's level
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb) {
+                const unsigned long long m = __ballot(ve && ((lev >> bb) & 1));
+                peers &= ((lev >> bb) & 1) ? m : ~m;
+            }
+            if (ve && __builtin_ctzll(peers) == lane) {
+                const int side = lev >> 7, price = lev & 127, li = side * LVP + price;
+                const int2 ht = L.ht[li];
+                int32_t head = ht.x, tail = ht.y;
+                int64_t toid = L.toid[li];
+                unsigned long long m = peers;
+                while (m) {
+                    const int k = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int4 f = L.ev[c0 + k];
+                    const int kind = (f.x >> 6) & 3, rk = f.x & 63;
+                    const uint32_t rank = (uint32_t)(f.x >> 8) & 7;
+                    const int4 ri = L.rin[rk];                // the record's (input index, PRec w0, rest size)
+                    if (kind == EK_TAKE) {                    // tryMatch at one level (KP:237-261)
+                        const int32_t P = (f.x >> 24) & 0x7F;
+                        int32_t x = f.y, ms = head;
+                        uint32_t ntr = 0;
+                        bool moved = false;
+                        if (ms < 0) err = 2;
+                        while (ms >= 0) {
+                            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[ms]);
+                            const int4 n0 = nd[0], n1 = nd[1];
+                            if (!(x > 0 || price >= P)) break;   // KP:237 with size 0 (H3); x > 0: crosses
+                            const int32_t ts = imin(x, n1.z);
+                            x -= ts;
+                            lane_emit(tpos, tlim, (uint32_t)ri.x, ntr++ | (rank << FAST_RANK_SHIFT), n0, n1.y < 0, price, ts, err);
+                            if (n1.z - ts != 0) { pool[ms].size = n1.z - ts; lane_dirty(ms); break; }
+                            lane_free(ms);                    // orders.delete (KP:243)
+                            if (n1.w < 0) { if (x != 0) err = 2; ms = -1; break; }   // the level taken whole
+                            ms = n1.w;
+                            moved = true;
+                        }
+                        if (ms < 0) { head = -1; tail = -1; }
+                        else { if (moved) { pool[ms].prev = -1; lane_dirty(ms); } head = ms; }
+                        L.ev[c0 + k].w = (int32_t)ntr;
+                    } else if (kind == EK_ZERO) {             // the next level's head, size 0 (KP:237, H3)
+                        int32_t n = 0;
+                        if (head < 0) {
+                            err = 2;
+                        } else {
+                            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[head]);
+                            const int4 n0 = nd[0], n1 = nd[1];
+                            lane_emit(tpos, tlim, (uint32_t)ri.x, rank << FAST_RANK_SHIFT, n0, n1.y < 0, price, 0, err);
+                            n = 1;
+                        }
+                        L.ev[c0 + k].w = n;
+                    } else if (kind == EK_REST) {             // addOrder's rest (KP:205-221)
+                        const int4 id = L.trd[rk];
+                        const int32_t slot = f.z;
+                        int32_t nprev = -1, hp = 0;
+                        int64_t poid = 0;
+                        if (head < 0) {
+                            head = slot;
+                        } else {
+                            pool[tail].next = slot;
+                            lane_dirty(tail);
+                            nprev = tail; poid = toid; hp = 1;
+                        }
+                        tail = slot;
+                        toid = mk64(id.x, id.y);
+                        const int32_t sidl = ((ri.y >> 17) & 1) ? -g : g;
+                        KG int4* nd = reinterpret_cast<KG int4*>(&pool[slot]);
+                        nd[0] = id;
+                        nd[1] = make_int4(sidl, sidl < 0 ? -1 : 0, ri.z, -1);
+                        nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
+                        nd[3] = make_int4(price, ri.y & 0xFF, 1, 0);
+                        lane_dirty(slot);
+                        L.ev[c0 + k] = make_int4(f.x, hp, lo32(poid), hi32(poid));
+                    } else {                                  // removeOrder's unlink (KP:297-320)
+                        const int32_t vs = f.z;
+                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[vs]);
+                        const int4 n1 = nd[1], n2 = nd[2], n3 = nd[3];
+                        const int32_t next = n1.w, prev = n2.z;
+                        const int64_t prev_oid = mk64(n2.x, n2.y);
+                        if (prev < 0 && next < 0) {
+                            head = -1; tail = -1;
+                        } else if (prev < 0) {
+                            head = next;
+                            pool[next].prev = -1;
+                            lane_dirty(next);
+                        } else if (next < 0) {
+                            tail = prev; toid = prev_oid;
+                            pool[prev].next = -1;
+                            lane_dirty(prev);
+                        } else {
+                            pool[prev].next = next;
+                            pool[next].prev = prev;
+                            pool[next].prev_oid = prev_oid;
+                            lane_dirty(prev);
+                            lane_dirty(next);
+                        }
+                        lane_free(vs);
+                        if (Sp->ledger_replay)                // the removed order, for postRemoveAdjustments
+                            Sp->vic[ri.x] = make_int4(price | ((n3.y == SELL ? SELL : BUY) << 8), n1.z, n1.y < 0 ? -g : g,
+                                                      n1.y < 0 ? -1 : 0);
+                    }
+                }
+                L.ht[li] = make_int2(head, tail);
+                L.toid[li] = toid;
+            }
+            sync_lds();
+        }
+        KST(const unsigned long long te0 = stamp(); acc[ST_FAST_LEVEL] += te0 - tl0;)
         {
             const int fsp = U32(L.gs[GS_FSP]);
             if (fsp > FSTK) set_gs(GS_FSP, FSTK);
         }
-        // per record: its results, its oid-table entry (the rest slot, or dead: KP:221)
-        const int4 fo = L.fr[lane];
-        if (inseg) {
-            o_ntr = f_kind == FK_TAKE ? fo.x : 0;
-            if (f_kind == FK_REST && fo.y) { o_act |= KME_OUT_HAS_PREV << 16; o_plo = fo.z; o_phi = fo.w; }
-            if (b_act == BUY || b_act == SELL) otab_final(cold().otab, B.tgt, f_kind == FK_REST ? f_slot : -1);
+        // per record: its results, its events' trade bases, its oid-table entry (the rest slot, or
+        // dead: KP:221)
+        if (lane >= j0 && lane < je) {
+            const int eb = o_plo & 0xFF, en = (o_plo >> 8) & 0xFF;
+            const int32_t rs = o_phi;
+            o_act &= ~RR_REMOVED;
+            o_plo = 0; o_phi = 0;
+            uint32_t ntr = 0;
+            for (int e = eb; e < eb + en; ++e) {
+                const int4 f = L.ev[e];
+                const int kind = (f.x >> 6) & 3, rank = (f.x >> 8) & 7;
+                if (kind == EK_TAKE || kind == EK_ZERO) {
+                    if (rank) Sp->lvbase[(size_t)B.i * FAST_LVB + rank - 1] = ntr;
+                    ntr += (uint32_t)f.w;
+                } else if (kind == EK_REST && f.y) {
+                    o_act |= KME_OUT_HAS_PREV << 16;
+                    o_plo = f.z; o_phi = f.w;
+                }
+            }
+            o_ntr = (int32_t)ntr;
+            if (b_bs) otab_final(cold().otab, B.tgt, (o_act >> 16) & 2 ? rs : -1);
         }
         sync_lds();
+        KST(acc[ST_FAST_EPI] += stamp() - te0;)
+        if (__ballot(err != 0)) {
+            if (__ballot(err == 2)) { cur = (uint32_t)rl32((int32_t)B.i, j0); die(KME_E_DOMAIN, KME_D_NPE_ORDER); }
+            else dead = true;                                 // CAP_TRADES, raised at its record by lane_emit
+        }
         return je;
     }
 
@@ -2413,12 +2590,17 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
         // cancels: the target node, if it came to rest before this batch (an earlier epoch, or an
         // earlier batch of this group), is fetched now; valid unless written since (dirty filter)
         B.pf_slot = -1;
-        if (valid && b_action == CANCEL) {
-            if (B.tgt >= 0) B.pf_slot = B.tgt;
-            else if (B.tgt <= -2) B.pf_slot = otab_epoch_slot(C.otab, -(B.tgt + 2));   // final unless the
-                                                      // order is in this batch (then still pending: -1)
-        }
         B.pf_meta = 0; B.pf_size = B.pf_next = B.pf_prev = 0; B.pf_poid = 0;
+        if (valid && b_action == CANCEL) {
+            if (B.tgt >= 0) {
+                B.pf_slot = B.tgt;
+            } else if (B.tgt <= -2) {   // final unless the order is in this batch (then still pending:
+                                        // pf_meta keeps the raw entry, OT_PENDING | its input index)
+                const uint32_t v = reinterpret_cast<const KG uint32_t*>(C.otab)[2 * (size_t)(-(B.tgt + 2))];
+                if (v & OT_PENDING) B.pf_meta = (int32_t)v;
+                else B.pf_slot = (int32_t)v;
+            }
+        }
         if (B.pf_slot >= 0) {
             const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[B.pf_slot]);
             const int4 c0 = nd[0], c1 = nd[1], c2 = nd[2], c3 = nd[3];
@@ -2487,9 +2669,17 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             o_ntr = me ? (int32_t)o.ntr : o_ntr;
             KST(w.acc[ST_REC_OUT] += stamp() - tr0;)
         }
+        {   // a record with more trades than an ordinal counts: the fault is that record (the ones before
+            // it in the batch are answered)
+            const unsigned long long big = __ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR);
+            if (big) {
+                done = __builtin_ctzll(big);
+                w.cur = (uint32_t)rl32((int32_t)B.i, done);
+                w.die(KME_E_CAPACITY, KME_D_CAP_TRADES);
+            }
+        }
         n_rest += (uint32_t)__popcll(__ballot(lane < done && ((o_act >> 16) & 2)));
         n_cancel += (uint32_t)__popcll(__ballot(lane < done && b_action == CANCEL && (o_act & 0xFFFF) == CANCEL));
-        if (__ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR)) { w.die(KME_E_CAPACITY, KME_D_CAP_TRADES); break; }
         {   // one 16-B record per lane, at the record's input index (k_unsort reads them in order); lanes
             // past the batch's last answered record store to a dump slot behind the array instead of
             // branching: a divergent branch here joins the loop latch, and the uniformity analysis then
@@ -3228,8 +3418,17 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
             r[q].seq = -1;
             if (k < cnt) r[q] = S.ttmp[base + k];
         }
+        uint32_t ord[SCATTER_ITEMS];
 #pragma unroll
-        for (int q = 0; q < SCATTER_ITEMS; ++q) off[q] = r[q].seq >= 0 && (uint32_t)r[q].seq < lim ? io.trade_off[r[q].seq] : 0;
+        for (int q = 0; q < SCATTER_ITEMS; ++q) {
+            const bool use = r[q].seq >= 0 && (uint32_t)r[q].seq < lim;
+            off[q] = use ? io.trade_off[r[q].seq] : 0;
+            // a fast segment's trade: index within its record's event | event rank << 20, the event's
+            // base in lvbase (GroupWave::fast_segment)
+            const uint32_t o = r[q].ordp & ((1u << TT_ORD_BITS) - 1), rk = o >> FAST_RANK_SHIFT;
+            ord[q] = (o & ((1u << FAST_RANK_SHIFT) - 1)) +
+                     (use && rk ? S.lvbase[(size_t)r[q].seq * FAST_LVB + rk - 1] : 0u);
+        }
 #pragma unroll
         for (int q = 0; q < SCATTER_ITEMS; ++q)
             if (r[q].seq >= 0 && (uint32_t)r[q].seq < lim) {
@@ -3239,7 +3438,7 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
                 t.msid = (ordp >> 30) & 1 ? -(int64_t)r[q].group : (int64_t)r[q].group;
                 t.mprice = (int32_t)((ordp >> TT_ORD_BITS) & 0x7F);
                 t.size = r[q].size;
-                io.trades[off[q] + (ordp & ((1u << TT_ORD_BITS) - 1))] = t;
+                io.trades[off[q] + ord[q]] = t;
             }
     }
 }

@@ -276,6 +276,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(S.cancel_tgt, E);
     ALLOC(S.rest_slot, E);
     if (funded) ALLOC(S.prec, 2 * (size_t)E);
+    if (funded) ALLOC(S.lvbase, (size_t)FAST_LVB * E);
     // OUT echo: one 16-B record per input index, stored by the matching kernels where the record
     // arrived (k_unsort then reads it sequentially; no sorted-position map)
     S.os_base = E;

@@ -106,3 +106,56 @@ def test_constructed_batch_interactions(kme_mod, oracle_mod, fast):
              (W.BUY, 505, 0, 1, 50, 2)]       # rests at the new tail
     stream = W.Orders.from_rows(body)
     _run(kme_mod, oracle_mod, setup, stream, 1, 4, fast, epoch=1 << 10)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_constructed_sweeps_and_same_batch_cancels(kme_mod, oracle_mod, fast):
+    """One symbol, hand-made, one batch: sweeps that take whole levels and end exactly on a level's
+    end (the zero-size trade is against the NEXT level's head when it still crosses with size 0,
+    KP:237 / H3), a sweep over more levels than a segment takes (the serial path), cancels of
+    orders rested earlier in the same batch (fast), one of them twice, one of another account, one
+    of an order that traded away, and one of an order whose level was taken from since."""
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(4)] + \
+           [(W.TRANSFER, 0, a, 0, 0, 2_000_000_000) for a in range(4)] + [(W.ADD_SYMBOL, 0, 0, 1, 0, 0)]
+    setup = W.Orders.from_rows(rows)
+    body, oid = [], 100
+    for p, sizes in ((52, (3,)), (53, (2, 2)), (55, (1, 4)), (56, (2,)), (57, (3,)), (58, (1,)), (60, (5,))):
+        for s in sizes:
+            body.append((W.SELL, oid, oid % 4, 1, p, s)); oid += 1
+    for p, sizes in ((50, (5,)), (49, (2, 6)), (47, (1,)), (46, (2,)), (45, (2,)), (44, (1,)), (43, (9,))):
+        for s in sizes:
+            body.append((W.BUY, oid, oid % 4, 1, p, s)); oid += 1
+    body += [(W.BUY, 900, 0, 1, 53, 3),        # takes 52 whole, ends on its end: zero trade with 53's head
+             (W.SELL, 901, 1, 1, 49, 5),       # takes 50 whole: zero trade with 49's head (49 >= 49)
+             (W.SELL, 902, 2, 1, 51, 4),       # rests at 51 (ask side)
+             (W.BUY, 903, 3, 1, 48, 2),        # rests at 48
+             (W.CANCEL, 902, 2, 0, 0, 0),      # an order of this batch: removed
+             (W.CANCEL, 902, 2, 0, 0, 0),      # again: rejected
+             (W.CANCEL, 903, 1, 0, 0, 0),      # another account's: rejected
+             (W.CANCEL, 900, 0, 0, 0, 0),      # traded away: rejected
+             (W.BUY, 904, 1, 1, 56, 5),        # 53 (2+2 left) then 55 (1 of 1+4): two levels
+             (W.SELL, 905, 0, 1, 47, 8),       # 49 (2 + 6) whole, ends exactly: 47 >= 47 -> zero trade
+             (W.SELL, 906, 3, 1, 46, 3),       # 47 (1) whole, 46 (2) whole, exactly: next 45 < 46, none
+             (W.BUY, 907, 2, 1, 48, 1),        # rests at 48 behind 903
+             (W.SELL, 908, 1, 1, 48, 2),       # takes 903 (2)
+             (W.CANCEL, 907, 2, 0, 0, 0),      # its level was taken from since it rested: serial
+             (W.BUY, 909, 0, 1, 70, 40),       # sweeps the whole ask side: more levels than a segment
+             (W.SELL, 910, 3, 1, 43, 1)]       # after the serial record
+    stream = W.Orders.from_rows(body)
+    _run(kme_mod, oracle_mod, setup, stream, 1, 4, fast, epoch=1 << 10)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("seed", [5, 6])
+def test_sweeps_over_thin_levels(kme_mod, oracle_mod, fast, seed):
+    """Thin levels (sizes 1-3) in a 10-tick band on 2 symbols, takers 1-12: most takes sweep several
+    levels, many end on a level's end (zero trades against the next level), cancels of live orders
+    of the same and earlier batches."""
+    n_sym, n_acc, n = 2, 32, 60_000
+    rng = np.random.Generator(np.random.PCG64(seed))
+    o = W.uniform(n, n_symbols=n_sym, n_accounts=n_acc, seed=seed, price_lo=45, price_hi=55, cancels="live")
+    bs = np.isin(o.action, (W.BUY, W.SELL))
+    big = rng.random(n) < 0.3
+    o.size = np.where(bs, np.where(big, rng.integers(4, 13, n), rng.integers(1, 4, n)), o.size).astype(np.int32)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    _run(kme_mod, oracle_mod, setup, o, n_sym, n_acc, fast)
