@@ -275,17 +275,18 @@ KDEV bool otab_insert(const DevState& S, int64_t oid, int32_t slot) {
 }
 
 // A BUY/SELL's pending entry (k_emap) becomes its rest slot, or OT_DEAD when it did not rest: the
-// entry's low word only (the fingerprint stays), stored by the matching kernel that decided it.
+// entry's low word only (the fingerprint stays).  FUNDED: k_unsort stores it from rest_slot.
 KDEV void otab_final(decltype(DevState::otab) otab, int32_t h, int32_t slot) {
     if (h >= 0) reinterpret_cast<KG uint32_t*>(otab)[2 * (size_t)h] = slot >= 0 ? (uint32_t)slot : OT_DEAD;
 }
 
-// The rest slot of a BUY/SELL of this epoch from its entry at position h (otab_final has run for it:
-// the matchers take a group's records in arrival order), or -1 when it did not rest.
-KDEV int32_t otab_epoch_slot(decltype(DevState::otab) otab, int32_t h) {
-    const uint32_t v = reinterpret_cast<const KG uint32_t*>(otab)[2 * (size_t)h];
-    return (v & OT_PENDING) ? -1 : (int32_t)v;
-}
+// DevState::rest_slot[i] of BUY/SELL i of the epoch: RS_PENDING until the matching kernel decides
+// it (k_route sets it), then its rest slot, or -1 when it did not rest.  The matchers store there
+// (a 4-byte store into an array of the epoch's size, which stays in the Infinity Cache) instead of
+// into the oid table's random line (a partial-line write to HBM in the middle of the record loop);
+// a same-epoch cancel reads its target's final slot there (the matchers take a group's records in
+// arrival order), and k_unsort copies the epoch's finals into the oid table in one streaming pass.
+constexpr int32_t RS_PENDING = -2;
 
 // ------------------------------------------------------------------ epoch kernels: emap / ledger / route
 // Sum of a per-thread count over a 256-thread block (DPP wave scans, then LDS); valid in thread 0.
@@ -309,6 +310,12 @@ KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int3
     io.out_flags[i] = has_prev ? (uint8_t)KME_OUT_HAS_PREV : (uint8_t)0;
 }
 
+#ifndef KME_DIAG_EMAP_NOCAS
+#define KME_DIAG_EMAP_NOCAS 0     // diagnostic builds only: one oid-table probe per BUY/SELL
+#endif
+#ifndef KME_DIAG_EMAP_NONEED
+#define KME_DIAG_EMAP_NONEED 0    // diagnostic builds only: no per-account need accumulation
+#endif
 // BUY/SELL oid -> input index of this epoch; duplicate / sentinel oid checks; FUNDED: range domain
 // and per-account reservation need (max over adj of checkBalance's risk, KP:172-176).
 __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded, EpochIO* io_dev) {
@@ -329,7 +336,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
             const unsigned long long ent = hentry(fp, OT_PENDING | i);
             uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
             bool placed = false;
-            for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
+            for (uint32_t probes = 0; probes <= (KME_DIAG_EMAP_NOCAS ? 0u : S.otab_mask); ++probes) {
                 const unsigned long long prev = atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent);
                 if (prev == 0) { S.epos[i] = h; placed = true; break; }
                 const uint32_t v = (uint32_t)prev;
@@ -357,7 +364,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                 const int64_t aid = io.aid[i];
                 if (price < 0 || price > 100 || size < 0) {
                     raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
-                } else if (aid >= 0 && aid < S.A) {
+                } else if (aid >= 0 && aid < S.A && !KME_DIAG_EMAP_NONEED) {
                     const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
                     atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
                 }
@@ -548,8 +555,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     const int32_t a = io.action[i];
     int32_t grp = -1, vlev = 0;
     int64_t tgt = -1;
-    int64_t ptgt = 0;             // PRec word 6 when it differs from tgt (a same-epoch cancel target)
-    S.rest_slot[i] = -1;
+    S.rest_slot[i] = (a == BUY || a == SELL) ? RS_PENDING : -1;
     io.n_trades[i] = 0;
     if (funded && (a == BUY || a == SELL)) {   // routed by k_emap
         if (S.fallback) S.cancel_tgt[i] = -1;
@@ -597,7 +603,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
             const int64_t sj = io.sid[j];
             const int32_t gj = group_of(sj, S.G);
             if (gj >= 0) {
-                grp = gj; tgt = t; ptgt = -((int64_t)hpos + 2);
+                grp = gj; tgt = t;
                 const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
                 vlev = (io.price[j] & 0xFF) | (side << 8) | (1 << 9);
             }
@@ -623,10 +629,9 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
     if (grp >= 0) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
-        // word 6: a cancel's target (a same-epoch order: -(its entry's position + 2), the slot read
-        // from the entry the matcher finalised); a FUNDED BUY/SELL's packed record is k_emap's, with
-        // its own entry's position there
-        if (ptgt <= -2) tgt = ptgt;
+        // word 6: a cancel's target (a same-epoch order j: -(j + 2), its final slot read from
+        // rest_slot[j]); a FUNDED BUY/SELL's packed record is k_emap's, with its own entry's position
+        // there
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
@@ -1505,7 +1510,7 @@ struct Lanes {
     int32_t w0, size, tgt;        // PRec word 0 (action | price << 8 | acct_ok << 16 | sid < 0 << 17)
     int64_t oid, aid;
     int32_t pf_slot, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10 | ok << 11
-                                                           // (pf_slot < 0: the raw oid-table entry of this epoch's target)
+                                                           // (pf_slot < 0: rest_slot of this epoch's target)
     int64_t pf_poid;
 };
 
@@ -1899,7 +1904,7 @@ struct GroupWave {
         const int32_t w = q1 ? (q0 ? 0 : g) : (q0 ? -1 : hi32(r.aid));
         if (lane < 4) reinterpret_cast<KG int4*>(&pool[slot])[lane] = make_int4(x, y, z, w);
         mark_dirty(slot);
-        otab_final(cold().otab, (int32_t)r.tgt, slot);
+        rest_slot[r.i] = slot;
         o.rested = true;
         KST(acc[ST_REST_NODE] += stamp() - ts2;)
     }
@@ -1933,7 +1938,7 @@ struct GroupWave {
     KDEV bool cancel(const Rec& r, const Lanes& B) {
         int32_t slot = -1;
         if (r.tgt >= 0) slot = (int32_t)r.tgt;
-        else if (r.tgt <= -2) slot = U32(otab_epoch_slot(cold().otab, (int32_t)(-(r.tgt + 2))));
+        else if (r.tgt <= -2) slot = U32(rest_slot[-(r.tgt + 2)]);   // (RS_PENDING cannot be: arrival order)
         if (slot < 0) return false;                          // orders.get(oid) == null
         Victim o;
         if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
@@ -2173,7 +2178,7 @@ struct GroupWave {
                     else cls = dirty || !exists ? PC_SERIAL : PC_CANCEL_PF;   // written since the prefetch /
                     vlev = ((B.pf_meta >> 8) & 1) * 128 + (B.pf_meta & 0xFF);  // KP:294's NPE: serial
                 } else {                                      // an order of this epoch not final at the prefetch
-                    cls = (uint32_t)B.pf_meta == OT_DEAD ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
+                    cls = B.pf_meta != RS_PENDING ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
                 }
             }
             pk = cls | (b_act == BUY ? 16 : 0) | (P << 8) | (b_act << 16) | (vlev << 24);
@@ -2289,7 +2294,7 @@ struct GroupWave {
                         vsz = rl32(B.pf_size, j);
                     }
                 } else {                                      // pending: a BUY/SELL of this batch
-                    const uint32_t ti = (uint32_t)rl32(B.pf_meta, j) & ~OT_PENDING;
+                    const uint32_t ti = (uint32_t)(-(rl32(B.tgt, j) + 2));
                     const uint64_t hit = __ballot(lane < nb && B.i == ti);
                     if (!hit) break;
                     const int jt = __builtin_ctzll(hit);
@@ -2482,7 +2487,7 @@ struct GroupWave {
                 }
             }
             o_ntr = (int32_t)ntr;
-            if (b_bs) otab_final(cold().otab, B.tgt, (o_act >> 16) & 2 ? rs : -1);
+            if (b_bs) rest_slot[B.i] = (o_act >> 16) & 2 ? rs : -1;
         }
         sync_lds();
         KST(acc[ST_FAST_EPI] += stamp() - te0;)
@@ -2516,7 +2521,7 @@ struct GroupWave {
             break;
         case BUY:
         case SELL: {
-            if (!gsv(GS_EXISTS) || !r.acct_ok) { otab_final(cold().otab, (int32_t)r.tgt, -1); break; }   // books.get(sid) == null / balances.get == null
+            if (!gsv(GS_EXISTS) || !r.acct_ok) { rest_slot[r.i] = -1; break; }   // books.get(sid) == null / balances.get == null
             const bool is_buy = r.action == BUY;
             const int os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
             int32_t tsize = r.size;
@@ -2527,7 +2532,7 @@ struct GroupWave {
             o.ntr = ntr;
             if (dead) return o;
             if (!filled) { rest(r, tsize, o); if (dead) return o; }
-            else otab_final(cold().otab, (int32_t)r.tgt, -1);
+            else rest_slot[r.i] = -1;
             ok = true;
             o.size = tsize;
             break;
@@ -2595,10 +2600,10 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             if (B.tgt >= 0) {
                 B.pf_slot = B.tgt;
             } else if (B.tgt <= -2) {   // final unless the order is in this batch (then still pending:
-                                        // pf_meta keeps the raw entry, OT_PENDING | its input index)
-                const uint32_t v = reinterpret_cast<const KG uint32_t*>(C.otab)[2 * (size_t)(-(B.tgt + 2))];
-                if (v & OT_PENDING) B.pf_meta = (int32_t)v;
-                else B.pf_slot = (int32_t)v;
+                                        // pf_meta keeps the raw word, RS_PENDING; -1: did not rest)
+                const int32_t v = C.rest_slot[-(B.tgt + 2)];
+                if (v < 0) B.pf_meta = v;
+                else B.pf_slot = v;
             }
         }
         if (B.pf_slot >= 0) {
@@ -2984,7 +2989,7 @@ struct GroupLane {
         nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
         nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
         nd[3] = make_int4(p, r.action, 1, 0);
-        otab_final(S.otab, (int32_t)r.tgt, slot);
+        S.rest_slot[r.i] = slot;
         o.rested = true;
     }
 
@@ -3116,7 +3121,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                     c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
                 } else if (r.tgt <= -2) {
-                    vslot = otab_epoch_slot(S.otab, (int32_t)(-(r.tgt + 2)));
+                    vslot = S.rest_slot[-(r.tgt + 2)];   // final (arrival order); -1: did not rest
                 }
             }
             if (order) w.request_spare();
@@ -3178,7 +3183,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 pend_a = os_pack(o.action, o.has_prev, o.ntr, o.size, o.has_prev ? o.prev : 0);
                 pend = true;
             }
-            if ((r.action == BUY || r.action == SELL) && !o.rested) otab_final(S.otab, (int32_t)r.tgt, -1);
+            if ((r.action == BUY || r.action == SELL) && !o.rested) S.rest_slot[r.i] = -1;
             n_rest += o.rested ? 1u : 0u;
             n_cancel += (cxl && ok) ? 1u : 0u;
             LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
@@ -3361,12 +3366,12 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t g = S.route_grp[i];
-        if (g < 0 || i >= lim) {   // k_table's work for the BUY/SELL no matching kernel finalised (otab_final)
+        {   // k_table's work: the BUY/SELL's oid-table entry becomes its rest slot (rest_slot, stored by
+            // the matcher), or dead (not rested, not matched, or from a fault on)
             const int32_t act = io.action[i];
             if (act == BUY || act == SELL) {
-                const uint32_t h = S.epos[i];   // still pending: the order did not rest
-                if (h != OT_DEAD && (reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)h] & OT_PENDING))
-                    otab_final(S.otab, (int32_t)h, -1);
+                const uint32_t h = S.epos[i];
+                if (h != OT_DEAD) otab_final(S.otab, (int32_t)h, g >= 0 && i < lim ? S.rest_slot[i] : -1);
             }
         }
         if (g < 0) continue;
