@@ -223,8 +223,11 @@ KDEV uint32_t oid_fp(int64_t oid) { return (uint32_t)(mix64((uint64_t)oid ^ 0x9e
 KDEV uint64_t hentry(uint32_t fp, uint32_t v) { return ((uint64_t)fp << 32) | v; }
 
 // Entry values: a node slot (< 2^31); OT_PENDING | i for BUY/SELL i of the epoch in flight (k_emap
-// inserts every BUY/SELL; k_table turns the entry into the order's rest slot, or OT_DEAD when it
-// did not rest), so one table answers both "an earlier order of this epoch" and "a resting order".
+// inserts every BUY/SELL; the entry becomes the order's rest slot when it rests -- k_unsort, or
+// k_table for EXACT / serial epochs, which also mark the others OT_DEAD), so one table answers both
+// "an earlier order of this epoch" and "a resting order".  A FUNDED order that did not rest keeps
+// its pending entry until the next rebuild; a pending entry is only ever read as "record j of the
+// current epoch is a BUY/SELL with this oid", which the reader checks against the epoch's input.
 constexpr uint32_t OT_PENDING = 0x80000000u;
 constexpr uint32_t OT_DEAD = 0xFFFFFFFFu;
 
@@ -253,9 +256,9 @@ KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oi
         if (e == 0) return -1;
         const uint32_t v = (uint32_t)e;
         if ((uint32_t)(e >> 32) == fp && v != OT_DEAD) {
-            if (v & OT_PENDING) {
+            if (v & OT_PENDING) {   // (possibly an earlier epoch's: it counts only as a fact of this one)
                 const uint32_t j = v & ~OT_PENDING;
-                if (j < i && io.oid[j] == oid) { pos = h; return -((int64_t)j + 2); }
+                if (j < i && io.oid[j] == oid && (io.action[j] == BUY || io.action[j] == SELL)) { pos = h; return -((int64_t)j + 2); }
             } else if (S.pool[v].live && S.pool[v].oid == oid) {
                 return (int64_t)v;
             }
@@ -280,8 +283,9 @@ KDEV void otab_final(decltype(DevState::otab) otab, int32_t h, int32_t slot) {
     if (h >= 0) reinterpret_cast<KG uint32_t*>(otab)[2 * (size_t)h] = slot >= 0 ? (uint32_t)slot : OT_DEAD;
 }
 
-// DevState::rest_slot[i] of BUY/SELL i of the epoch: RS_PENDING until the matching kernel decides
-// it (k_route sets it), then its rest slot, or -1 when it did not rest.  The matchers store there
+// DevState::rest_slot[i] of BUY/SELL i of the epoch: RS_PENDING (k_route) until the order rests,
+// then its rest slot; once the matcher has passed i, RS_PENDING means it did not rest (a reader is a
+// later record of the same group: arrival order).  The matchers store there
 // (a 4-byte store into an array of the epoch's size, which stays in the Infinity Cache) instead of
 // into the oid table's random line (a partial-line write to HBM in the middle of the record loop);
 // a same-epoch cancel reads its target's final slot there (the matchers take a group's records in
@@ -341,9 +345,9 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                 if (prev == 0) { S.epos[i] = h; placed = true; break; }
                 const uint32_t v = (uint32_t)prev;
                 if ((uint32_t)(prev >> 32) == fp && v != OT_DEAD) {
-                    if (v & OT_PENDING) {
-                        const uint32_t j = v & ~OT_PENDING;
-                        if (io.oid[j] == oid) {
+                    if (v & OT_PENDING) {   // (an earlier epoch's entry counts only as a fact of this
+                        const uint32_t j = v & ~OT_PENDING;   // one: a BUY/SELL j != i with this oid)
+                        if (j != i && j < io.n && io.oid[j] == oid && (io.action[j] == BUY || io.action[j] == SELL)) {
                             // the later of the two is the fault; the earlier one takes effect and
                             // keeps its entry (cancels before the fault must find it), so it goes on
                             // probing past a later one that got there first
@@ -2487,7 +2491,7 @@ struct GroupWave {
                 }
             }
             o_ntr = (int32_t)ntr;
-            if (b_bs) rest_slot[B.i] = (o_act >> 16) & 2 ? rs : -1;
+            if (b_bs && ((o_act >> 16) & 2)) rest_slot[B.i] = rs;
         }
         sync_lds();
         KST(acc[ST_FAST_EPI] += stamp() - te0;)
@@ -2521,7 +2525,7 @@ struct GroupWave {
             break;
         case BUY:
         case SELL: {
-            if (!gsv(GS_EXISTS) || !r.acct_ok) { rest_slot[r.i] = -1; break; }   // books.get(sid) == null / balances.get == null
+            if (!gsv(GS_EXISTS) || !r.acct_ok) break;   // books.get(sid) == null / balances.get == null
             const bool is_buy = r.action == BUY;
             const int os = r.sid == 0 ? 0 : 1 - book_side(r.sid, is_buy);   // opposite book (the same for sid 0)
             int32_t tsize = r.size;
@@ -2532,7 +2536,6 @@ struct GroupWave {
             o.ntr = ntr;
             if (dead) return o;
             if (!filled) { rest(r, tsize, o); if (dead) return o; }
-            else rest_slot[r.i] = -1;
             ok = true;
             o.size = tsize;
             break;
@@ -2602,8 +2605,8 @@ __global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, c
             } else if (B.tgt <= -2) {   // final unless the order is in this batch (then still pending:
                                         // pf_meta keeps the raw word, RS_PENDING; -1: did not rest)
                 const int32_t v = C.rest_slot[-(B.tgt + 2)];
-                if (v < 0) B.pf_meta = v;
-                else B.pf_slot = v;
+                if (v < 0) B.pf_meta = v;   // (RS_PENDING also when it did not rest: the pass finds it
+                else B.pf_slot = v;         // outside the batch and leaves it to the serial path)
             }
         }
         if (B.pf_slot >= 0) {
@@ -3121,7 +3124,7 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                     c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
                 } else if (r.tgt <= -2) {
-                    vslot = S.rest_slot[-(r.tgt + 2)];   // final (arrival order); -1: did not rest
+                    vslot = S.rest_slot[-(r.tgt + 2)];   // final (arrival order); < 0: did not rest
                 }
             }
             if (order) w.request_spare();
@@ -3183,7 +3186,6 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 pend_a = os_pack(o.action, o.has_prev, o.ntr, o.size, o.has_prev ? o.prev : 0);
                 pend = true;
             }
-            if ((r.action == BUY || r.action == SELL) && !o.rested) S.rest_slot[r.i] = -1;
             n_rest += o.rested ? 1u : 0u;
             n_cancel += (cxl && ok) ? 1u : 0u;
             LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
@@ -3366,12 +3368,15 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t g = S.route_grp[i];
-        {   // k_table's work: the BUY/SELL's oid-table entry becomes its rest slot (rest_slot, stored by
-            // the matcher), or dead (not rested, not matched, or from a fault on)
+        {   // k_table's work for a BUY/SELL that rested: its oid-table entry becomes the rest slot
+            // (rest_slot, stored by the matcher).  The entry of one that did not stays pending
+            // (OT_PENDING | i): a reader takes a pending entry only where it names a BUY/SELL of the
+            // epoch it reads in with this oid, a fact either way (otab_cancel_target, k_emap).
             const int32_t act = io.action[i];
-            if (act == BUY || act == SELL) {
+            if ((act == BUY || act == SELL) && g >= 0 && i < lim) {
+                const int32_t rs = S.rest_slot[i];
                 const uint32_t h = S.epos[i];
-                if (h != OT_DEAD) otab_final(S.otab, (int32_t)h, g >= 0 && i < lim ? S.rest_slot[i] : -1);
+                if (rs >= 0 && h != OT_DEAD) otab_final(S.otab, (int32_t)h, rs);
             }
         }
         if (g < 0) continue;
