@@ -244,6 +244,11 @@ typedef struct kme_row {
  * harness both use it. */
 kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_result* res, kme_row* rows,
                            size_t cap, size_t* n_rows);
+/* The same rows, written by n_threads host threads (records split into contiguous ranges; each
+ * range's first row follows from trade_off alone), for callers that hand whole epochs to one
+ * consumer (the JNI glue).  n_threads 0 = the machine's hardware threads, at most 16; at most 64. */
+kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_result* res, kme_row* rows,
+                              size_t cap, size_t* n_rows, uint32_t n_threads);
 
 /* Identifies the sources libkme was built from (a hash of csrc/ and include/): the test session
  * rebuilds the library when it differs from the tree's. */

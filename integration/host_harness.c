@@ -4,9 +4,9 @@
  *   fill     the epoch's records go into the slot's registered input columns (Java's absolute
  *            ByteBuffer puts, one per field and record);
  *   submit   kme_submit_epoch_host: H2D, kernels, D2H queued, returns at once;
- *   complete kme_wait + kme_expand_rows into the slot's registered row buffer (exactly what
- *            Java_GpuMatchingEngine_complete does), then one pass over the rows (Java builds an
- *            Order per row from them).
+ *   complete kme_wait + kme_expand_rows_mt into the slot's registered row buffer (exactly what
+ *            Java_GpuMatchingEngine_complete does: up to 16 native threads), then one pass over the
+ *            rows on the calling thread (Java's stream thread builds an Order per row from them).
  * Two slots and at most two epochs in flight: the schedule of GpuMatchingEngine.process / flush /
  * completeOldest.  The clock runs from the first fill to the last completed epoch, so the figure is
  * PCIe- and host-inclusive; it is reported beside the device-resident value, never as it.
@@ -86,7 +86,7 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
             if (rc != KME_OK) break;
             const kme_orders in = {h->action, h->oid, h->aid, h->sid, h->price, h->size};
             size_t nr = 0;
-            rc = kme_expand_rows(&in, h->n, &h->res, h->rows, h->rows_cap, &nr);
+            rc = kme_expand_rows_mt(&in, h->n, &h->res, h->rows, h->rows_cap, &nr, 0);
             if (rc != KME_OK) break;
             for (size_t q = 0; q < nr; ++q)   /* the JVM reads every row (one Order each) */
                 check += (uint64_t)h->rows[q].oid + (uint64_t)h->rows[q].size + h->rows[q].kind;

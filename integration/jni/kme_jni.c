@@ -10,7 +10,7 @@
  *   bind(h, slot, action, oid, aid, sid, price, size, rows)   the slot's buffers (checked, registered)
  *   submit(h, slot, n)        kme_submit_epoch_host: H2D, kernels, D2H queued; returns at once
  *   poll(h)                   kme_poll: 1 when the oldest epoch in flight is done (punctuator)
- *   complete(h, slot, st)     kme_wait + kme_expand_rows into the slot's row buffer, in the
+ *   complete(h, slot, st)     kme_wait + kme_expand_rows_mt into the slot's row buffer, in the
  *                             reference's order: IN (KP:97), maker / taker fill per trade
  *                             (executeTrade, KP:265-274), OUT (KP:124); st[0..3] = status, domain
  *                             detail, error index, records that took effect (kme_epoch_status)
@@ -212,7 +212,7 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, 
     sl->n = 0;
     const uint32_t ne = s == KME_OK ? n : (st.n_effective < n ? st.n_effective : n);
     size_t rows = 0;
-    const kme_status x = ne ? kme_expand_rows(&sl->in, ne, &sl->res, sl->rows, sl->rows_cap, &rows) : KME_OK;
+    const kme_status x = ne ? kme_expand_rows_mt(&sl->in, ne, &sl->res, sl->rows, sl->rows_cap, &rows, 0) : KME_OK;
     jlong stv[4];
     stv[0] = (jlong)(s != KME_OK ? s : x);
     stv[1] = (jlong)(s != KME_OK ? st.detail : (x != KME_OK ? KME_D_CAP_TRADES : 0));

@@ -11,6 +11,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
+#include <algorithm>
 
 #include "kme.h"
 
@@ -63,14 +66,9 @@ extern "C" {
 // The processor's MatchOut rows for records [0, n): IN (KP:97), per trade the maker fill then the
 // taker fill (executeTrade, KP:265-274), OUT (KP:124).  Same order and values as kme_tape_json, as
 // binary rows the JNI glue hands to Java (one Order per row) instead of text.
-kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
-                           size_t* n_rows) {
-    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
-    const size_t need = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
-    *n_rows = need;
-    if (need > cap) return KME_E_CAPACITY;
-    kme_row* w = rows;
-    for (uint32_t i = 0; i < n; ++i) {
+// Rows of records [a, b) from w on (the caller checked the capacity).
+static void expand_range(const kme_orders* in, uint32_t a, uint32_t b, const kme_epoch_result* r, kme_row* w) {
+    for (uint32_t i = a; i < b; ++i) {
         const int32_t a = in->action[i], price = in->price[i];
         const int64_t oid = in->oid[i], aid = in->aid[i], sid = in->sid[i];
         kme_row x;
@@ -96,6 +94,36 @@ kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_res
         x.prev = x.has_prev ? r->out_prev[i] : 0;
         *w++ = x;
     }
+}
+
+kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
+                           size_t* n_rows) {
+    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
+    const size_t need = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
+    *n_rows = need;
+    if (need > cap) return KME_E_CAPACITY;
+    expand_range(in, 0, n, r, rows);
+    return KME_OK;
+}
+
+kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
+                              size_t* n_rows, uint32_t n_threads) {
+    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
+    const size_t need = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
+    *n_rows = need;
+    if (need > cap) return KME_E_CAPACITY;
+    uint32_t T = n_threads ? n_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    T = std::min<uint32_t>(std::min<uint32_t>(T, 64), std::max<uint32_t>(1, n / 4096));   // >= 4,096 records each
+    if (T <= 1) { expand_range(in, 0, n, r, rows); return KME_OK; }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (uint32_t t = 0; t < T; ++t) {
+        const uint32_t a = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T);
+        kme_row* w = rows + 2 * (size_t)a + 2 * (size_t)(r->trade_off[a] - r->trade_off[0]);
+        if (t + 1 == T) expand_range(in, a, b, r, w);
+        else th.emplace_back(expand_range, in, a, b, r, w);
+    }
+    for (auto& x : th) x.join();
     return KME_OK;
 }
 

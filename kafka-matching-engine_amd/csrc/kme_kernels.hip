@@ -315,7 +315,10 @@ KDEV void write_out(const EpochIO& io, uint32_t i, int32_t action, bool ok, int3
 }
 
 #ifndef KME_DIAG_EMAP_NOCAS
-#define KME_DIAG_EMAP_NOCAS 0     // diagnostic builds only: one oid-table probe per BUY/SELL
+#define KME_DIAG_EMAP_NOCAS 0     // diagnostic builds only: 1 = one oid-table probe per BUY/SELL, 2 = none
+#endif
+#ifndef KME_DIAG_EMAP_NOPREC
+#define KME_DIAG_EMAP_NOPREC 0    // diagnostic builds only: no packed-record stores
 #endif
 #ifndef KME_DIAG_EMAP_NONEED
 #define KME_DIAG_EMAP_NONEED 0    // diagnostic builds only: no per-account need accumulation
@@ -340,7 +343,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
             const unsigned long long ent = hentry(fp, OT_PENDING | i);
             uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
             bool placed = false;
-            for (uint32_t probes = 0; probes <= (KME_DIAG_EMAP_NOCAS ? 0u : S.otab_mask); ++probes) {
+            for (uint32_t probes = 0; KME_DIAG_EMAP_NOCAS < 2 && probes <= (KME_DIAG_EMAP_NOCAS ? 0u : S.otab_mask); ++probes) {
                 const unsigned long long prev = atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent);
                 if (prev == 0) { S.epos[i] = h; placed = true; break; }
                 const uint32_t v = (uint32_t)prev;
@@ -386,8 +389,10 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                     const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
                     const int32_t w0 = (a & 0xFF) | ((price & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((sid < 0 ? 1 : 0) << 17);
                     KG int4* p = &S.prec[2 * (size_t)i];
-                    p[0] = make_int4(w0, size, (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
-                    p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), placed ? (int32_t)h : -1, 0);
+                    if (!KME_DIAG_EMAP_NOPREC) {
+                        p[0] = make_int4(w0, size, (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
+                        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), placed ? (int32_t)h : -1, 0);
+                    }
                 }
             }
         } else if (funded && (a == CREATE_BALANCE || a == TRANSFER)) {

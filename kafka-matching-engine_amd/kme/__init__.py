@@ -72,7 +72,7 @@ EXPORTS = [
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
-    "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_build_id",
+    "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_expand_rows_mt", "kme_build_id",
     "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
     "kme_credit_adjust", "kme_credit_rebalance",
 ]
@@ -143,6 +143,8 @@ def lib():
         "kme_poll": (st, [vp, C.POINTER(C.c_int)]),
         "kme_expand_rows": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                  C.POINTER(C.c_size_t)]),
+        "kme_expand_rows_mt": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
+                                    C.POINTER(C.c_size_t), u32]),
         "kme_build_id": (C.c_char_p, []),
         "kme_comm_unique_id": (st, [vp]),
         "kme_comm_init": (st, [vp, u32, u32, vp, C.POINTER(vp)]),
@@ -548,8 +550,9 @@ def new_result(n: int, trades_cap: int) -> EpochResult:
                        arr(trades_cap, TRADE_DTYPE), kme_epoch_status())
 
 
-def expand_rows(orders: Orders, res: EpochResult, n: int | None = None) -> np.ndarray:
-    """kme_expand_rows: the MatchOut rows (ROW_DTYPE) of records [0, n) -- IN, fills, OUT."""
+def expand_rows(orders: Orders, res: EpochResult, n: int | None = None, threads: int = 1) -> np.ndarray:
+    """kme_expand_rows (threads == 1) / kme_expand_rows_mt: the MatchOut rows (ROW_DTYPE) of records
+    [0, n) -- IN, fills, OUT."""
     L = lib()
     n = len(orders) if n is None else n
     s, keep = _soa(orders)
@@ -558,7 +561,11 @@ def expand_rows(orders: Orders, res: EpochResult, n: int | None = None) -> np.nd
     need = C.c_size_t(0)
     L.kme_expand_rows(C.byref(s), n, C.byref(r), None, 0, C.byref(need))
     rows = np.zeros(need.value, ROW_DTYPE)
-    rc = L.kme_expand_rows(C.byref(s), n, C.byref(r), C.c_void_p(rows.ctypes.data), len(rows), C.byref(need))
+    if threads == 1:
+        rc = L.kme_expand_rows(C.byref(s), n, C.byref(r), C.c_void_p(rows.ctypes.data), len(rows), C.byref(need))
+    else:
+        rc = L.kme_expand_rows_mt(C.byref(s), n, C.byref(r), C.c_void_p(rows.ctypes.data), len(rows), C.byref(need),
+                                  threads)
     if rc:
         raise KmeError(rc, "kme_expand_rows")
     del keep

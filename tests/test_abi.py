@@ -188,3 +188,32 @@ def test_expand_rows_order_and_values(kme_mod):
     small = np.zeros(3, kme_mod.ROW_DTYPE)
     assert L.kme_expand_rows(C.byref(s), 3, C.byref(r), C.c_void_p(small.ctypes.data), 3, C.byref(need)) == 2
     assert need.value == 8 and not small["oid"].any()
+
+
+@pytest.mark.parametrize("threads", [0, 3, 16])
+def test_expand_rows_threads_equal_one_thread(kme_mod, threads):
+    """kme_expand_rows_mt: each thread's range starts where trade_off puts it; the rows are those of
+    kme_expand_rows, byte for byte (ragged trade counts, an epoch not a multiple of the ranges)."""
+    import numpy as np
+
+    from kme import workloads as W
+
+    n = 50_001
+    rng = np.random.Generator(np.random.PCG64(5))
+    orders = W.uniform(n, n_symbols=64, n_accounts=128, seed=5)
+    counts = np.where(rng.random(n) < 0.3, rng.integers(1, 6, n), 0).astype(np.uint32)
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum(counts)
+    res = kme_mod.new_result(n, int(off[-1]))
+    res.out_action[:] = orders.action
+    res.out_size[:] = rng.integers(0, 100, n)
+    res.out_flags[:] = rng.integers(0, 2, n)
+    res.out_prev[:] = rng.integers(1, 1 << 40, n)
+    res.trade_off[:] = off
+    t = res.trades
+    t["maker_oid"] = rng.integers(1, 1 << 40, len(t))
+    t["size"] = rng.integers(0, 50, len(t))
+    one = kme_mod.expand_rows(orders, res)
+    many = kme_mod.expand_rows(orders, res, threads=threads)
+    assert len(one) == 2 * n + 2 * int(off[-1])
+    assert one.tobytes() == many.tobytes()
