@@ -402,7 +402,7 @@ def main():
                                           "steps": d[7], "ms_per_epoch_match": float(np.mean(match_ms))}}), flush=True)
         return
     if args.stamps:  # -DKME_STAMPS build: cycle shares of k_match (kme_kernels.hip enum Stamp)
-        rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 32)
+        rows_ = eng.debug_counters().astype(np.float64).reshape(-1, 48)
         hot = int(np.argmax(rows_[:, 7]))   # the group with the most k_match cycles (C4: the hot symbol)
         d = rows_[hot] if os.environ.get("KME_STAMPS_HOT") else rows_.sum(axis=0)
         names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",

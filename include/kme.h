@@ -377,7 +377,7 @@ uint64_t kme_router_directory_size(const kme_router* r);
 
 /* Diagnostics: per-symbol-group words written by a -DKME_STAMPS build of the match kernel
  * (in-kernel s_memtime stamps; zero in the product build).  Copies min(n, max_symbols * 32). */
-#define KME_DBG_WORDS 32
+#define KME_DBG_WORDS 48
 kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n);
 
 const char* kme_strerror(int status);

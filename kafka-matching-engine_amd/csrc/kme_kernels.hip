@@ -1529,7 +1529,7 @@ enum Stamp : int {
     ST_N_TRADE_REC, ST_N_REST_REC, ST_N_CANCEL_REC, ST_MAKER_WAIT, ST_N_MAKER, ST_VICTIM_WAIT, ST_N_VICTIM, ST_FLUSH,
     ST_REST_ALLOC, ST_REST_LEVEL, ST_REST_NODE, ST_REC_PICK, ST_REC_OUT, ST_TM_PRE, ST_REST_PRE,
     ST_FAST, ST_N_FAST_REC, ST_N_FAST_SEG, ST_FAST_PASS, ST_FAST_DRAIN, ST_FAST_LEVEL, ST_FAST_EPI,
-    ST_N = 32
+    ST_N = 40
 };
 
 struct GroupWave {
@@ -2171,6 +2171,7 @@ struct GroupWave {
         // action << 16 | victim level << 24 (a prefetched cancel's).  A BUY/SELL with a negative sid
         // (its side is the other book, KP:201) takes the serial path.
         const int exists = gsv(GS_EXISTS);
+        const uint32_t bi0 = (uint32_t)rl32((int32_t)B.i, 0);   // the batch's first record
         int32_t pk;
         {
             const int32_t P = (B.w0 >> 8) & 0xFF;
@@ -2187,7 +2188,10 @@ struct GroupWave {
                     else cls = dirty || !exists ? PC_SERIAL : PC_CANCEL_PF;   // written since the prefetch /
                     vlev = ((B.pf_meta >> 8) & 1) * 128 + (B.pf_meta & 0xFF);  // KP:294's NPE: serial
                 } else {                                      // an order of this epoch not final at the prefetch
-                    cls = B.pf_meta != RS_PENDING ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
+                    // (a target before the batch was decided by an earlier batch, and its slot is
+                    // still pending: it did not rest, orders.get(oid) == null)
+                    const uint32_t ti = (uint32_t)(-(B.tgt + 2));
+                    cls = B.pf_meta != RS_PENDING || ti < bi0 ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
                 }
             }
             pk = cls | (b_act == BUY ? 16 : 0) | (P << 8) | (b_act << 16) | (vlev << 24);
@@ -2344,11 +2348,13 @@ struct GroupWave {
         set_bm(0, b0l, b0m);
         set_bm(1, b1l, b1m);
         set_gs(GS_FSP, fsp0 - nrest);
-        qv[0] = mk64(Ql0, Qh0); qv[1] = mk64(Ql1, Qh1); qv[2] = mk64(Ql2, Qh2); qv[3] = mk64(Ql3, Qh3);
+        {                                                     // quantities back (occupied levels)
+            qv[0] = mk64(Ql0, Qh0); qv[1] = mk64(Ql1, Qh1); qv[2] = mk64(Ql2, Qh2); qv[3] = mk64(Ql3, Qh3);
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {                         // quantities back (occupied levels)
-            const int sd = h >> 1, p = lane + 64 * (h & 1);
-            if (p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = qv[h];
+            for (int h = 0; h < 4; ++h) {
+                const int sd = h >> 1, p = lane + 64 * (h & 1);
+                if (p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = qv[h];
+            }
         }
         // ---- 2. the level step, 64 events at a time
         KST(const unsigned long long tl0 = stamp();)

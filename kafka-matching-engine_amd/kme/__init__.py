@@ -380,11 +380,11 @@ class Engine:
             self._L.kme_free(p)
 
     def debug_counters(self) -> np.ndarray:
-        out = np.zeros(int(self.cfg.max_symbols) * 32, np.uint64)
+        out = np.zeros(int(self.cfg.max_symbols) * 48, np.uint64)
         rc = self._L.kme_debug_counters(self._h, C.c_void_p(out.ctypes.data), out.size)
         if rc:
             raise KmeError(rc, "kme_debug_counters")
-        return out.reshape(-1, 32)
+        return out.reshape(-1, 48)
 
     def checkpoint(self, path: str):
         rc = self._L.kme_checkpoint(self._h, str(path).encode())
