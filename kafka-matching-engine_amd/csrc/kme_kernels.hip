@@ -903,6 +903,8 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t* out, uint32_t L, con
 // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding (vmcnt bits 3:0 and 15:14)
 constexpr int VMCNT0 = 0x0F70;
 KDEV int32_t rl32(int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
+// v_writelane_b32 (the intrinsic has no clang builtin here; bound by name)
+extern "C" __device__ int32_t kme_writelane_i32(int32_t v, int32_t lane, int32_t old) __asm("llvm.amdgcn.writelane.i32");
 KDEV int64_t rl64(int64_t v, int j) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
@@ -1427,7 +1429,7 @@ constexpr int LVP = 101;          // LDS level entries per book side: prices 0..
 constexpr int FSTK = 128;         // LDS free-slot stack
 constexpr int TRD = 32;           // trades staged in LDS between reservations (GroupWave::emit)
 constexpr int DIRTY_WORDS = 64;   // 2048-bit filter of node slots written since the batch prefetch
-constexpr int FAST_EVCAP = 128;   // events of one fast segment (GroupWave::fast_segment)
+constexpr int FAST_EVCAP = 64;    // events of one fast segment (GroupWave::fast_segment): one lane each
 
 struct GroupLds {
     int2 ht[2 * LVP];             // head / tail node slot of level (side, price)
@@ -2024,33 +2026,31 @@ struct GroupWave {
                                                      // zero trade is event rank FAST_RMAX at most)
     static constexpr int32_t RR_REMOVED = 1 << 24;   // rr flag: rested in the segment, then cancelled in it
     // lane l of the result is v, the others old's (v_cmp + v_cndmask; v scalar)
-    KDEV static int32_t wlane(int32_t v, int l, int32_t old) { return lane_id() == l ? v : old; }
-    // The pass's level quantities: lane l of Ql<k> / Qh<k> (k = 2 * side + h) holds the low / high word
-    // of level (side, 64 * h + l) -- read and written with readlane / lane selects, no LDS round trip
-    // (the 8 words are locals of fast_segment: a struct behind a reference becomes a dynamically
-    // indexed stack array, scratch memory)
-#define KME_QGET(s, p) mk64(rl32((s) ? ((p) < 64 ? Ql2 : Ql3) : ((p) < 64 ? Ql0 : Ql1), (p) & 63), \
-                            rl32((s) ? ((p) < 64 ? Qh2 : Qh3) : ((p) < 64 ? Qh0 : Qh1), (p) & 63))
+    // single-lane register writes (v_writelane: one VALU op; l uniform)
+    KDEV static int32_t wl(int32_t v, int l, int32_t old) { return kme_writelane_i32(v, l, old); }
+    // The pass's level quantities, 32 bits (fast_segment checks the bound at its start): lane p of QA
+    // / QC holds level (side 0 / 1, price p) for p < 63 and lane p - 63 of QB / QD the prices above,
+    // the bitmap words' split -- read with one readlane, written with two writelanes (side and price
+    // uniform; the register the level is not in takes the write in its lane 63, which holds no level:
+    // prices 63 and 126+ are QB's / no FUNDED price).  They are locals of fast_segment: a struct behind a reference
+    // becomes a dynamically indexed stack array (scratch memory).
+#define KME_QGET(s, p) ((s) ? ((p) < 63 ? rl32(QC, (p)) : rl32(QD, (p) - 63)) : ((p) < 63 ? rl32(QA, (p)) : rl32(QB, (p) - 63)))
 #define KME_QSET(s, p, v)                                                                              \
     do {                                                                                               \
-        const int _k = (s) * 2 + ((p) >= 64 ? 1 : 0), _l = (p) & 63;                                   \
-        const int64_t _v = (v);                                                                        \
-        const int32_t _lo = lo32(_v), _hi = hi32(_v);                                                  \
-        Ql0 = wlane(_lo, _k == 0 ? _l : -1, Ql0); Qh0 = wlane(_hi, _k == 0 ? _l : -1, Qh0);            \
-        Ql1 = wlane(_lo, _k == 1 ? _l : -1, Ql1); Qh1 = wlane(_hi, _k == 1 ? _l : -1, Qh1);            \
-        Ql2 = wlane(_lo, _k == 2 ? _l : -1, Ql2); Qh2 = wlane(_hi, _k == 2 ? _l : -1, Qh2);            \
-        Ql3 = wlane(_lo, _k == 3 ? _l : -1, Ql3); Qh3 = wlane(_hi, _k == 3 ? _l : -1, Qh3);            \
+        const int _p = (p);                                                                            \
+        const int32_t _v = (v);                                                                        \
+        const int _lo = _p < 63 ? _p : 63, _hi = _p < 63 ? 63 : _p - 63;   /* lane 63: a dummy */     \
+        if (s) { QC = wl(_v, _lo, QC); QD = wl(_v, _hi, QD); }                                         \
+        else   { QA = wl(_v, _lo, QA); QB = wl(_v, _hi, QB); }                                         \
     } while (0)
-    // events of the pass: event e in lane e & 63 of Ex0, Ev0 / Ex1, Ev1 (e >> 6): x = record lane |
-    // kind << 6 | rank << 8 | level (side * 128 + price) << 16 | P << 24, v = the amount taken (a take)
-    // or the node slot (a rest, an unlink)
+    // events of the pass: event e in lane e of Ex, Ev: x = record lane | kind << 6 | rank << 8 | level
+    // (side * 128 + price) << 16 | P << 24, v = the amount taken (a take) or the node slot (a rest, an
+    // unlink)
 #define KME_PUT_EV(e, k, kind, rank, lev, P, v)                                                        \
     do {                                                                                               \
-        const int32_t _x = (k) | ((kind) << 6) | ((rank) << 8) | ((lev) << 16) | ((P) << 24);          \
-        const int _e = (e), _l0 = _e < 64 ? _e : -1, _l1 = _e >= 64 ? _e - 64 : -1;                    \
-        const int32_t _v = (v);                                                                        \
-        Ex0 = wlane(_x, _l0, Ex0); Ev0 = wlane(_v, _l0, Ev0);                                          \
-        Ex1 = wlane(_x, _l1, Ex1); Ev1 = wlane(_v, _l1, Ev1);                                          \
+        const int _e = (e);                                                                            \
+        Ex = wl((k) | ((kind) << 6) | ((rank) << 8) | ((lev) << 16) | ((P) << 24), _e, Ex);            \
+        Ev = wl((v), _e, Ev);                                                                          \
     } while (0)
     enum { PC_TAKE_REST = 0, PC_REJECT = 1, PC_CANCEL_PF = 2, PC_CANCEL_BATCH = 3, PC_SERIAL = 4 };
 
@@ -2157,16 +2157,21 @@ struct GroupWave {
         uint64_t b0l = bl(0), b0m = bm(0), b1l = bl(1), b1m = bm(1);
         // the level quantities into lanes; levels unoccupied as the segment starts read as empty in
         // the level step
-        int64_t qv[4];
+        int64_t qv[4];                                        // QA, QB, QC, QD (see KME_QGET)
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            const int sd = h >> 1, p = lane + 64 * (h & 1);
-            const bool occ = p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p);
+            const int sd = h >> 1, p = (h & 1) ? lane + 63 : lane;
+            const bool lv = (h & 1) ? p <= 100 : lane < 63;
+            const bool occ = lv && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p);
             qv[h] = occ ? L.qty[sd * LVP + p] : 0;
-            if (p <= 100 && !occ) L.ht[sd * LVP + p] = make_int2(-1, -1);
+            if (lv && !occ) L.ht[sd * LVP + p] = make_int2(-1, -1);
         }
-        int32_t Ql0 = lo32(qv[0]), Ql1 = lo32(qv[1]), Ql2 = lo32(qv[2]), Ql3 = lo32(qv[3]);
-        int32_t Qh0 = hi32(qv[0]), Qh1 = hi32(qv[1]), Qh2 = hi32(qv[2]), Qh3 = hi32(qv[3]);
+        // 32-bit quantities: every level below 2^30 and every order of the segment below 2^23, so 64
+        // rests on one level stay below 2^31; otherwise the records take the serial path
+        if (__ballot(qv[0] >= (1 << 30) || qv[1] >= (1 << 30) || qv[2] >= (1 << 30) || qv[3] >= (1 << 30) ||
+                     (inrange && b_bs && B.size >= (1 << 23))))
+            return j0;
+        int32_t QA = lo32(qv[0]), QB = lo32(qv[1]), QC = lo32(qv[2]), QD = lo32(qv[3]);
         // each record's class, decided per lane before the serial pass: pk = class | BUY << 4 | P << 8 |
         // action << 16 | victim level << 24 (a prefetched cancel's).  A BUY/SELL with a negative sid
         // (its side is the other book, KP:201) takes the serial path.
@@ -2198,7 +2203,7 @@ struct GroupWave {
         }
         uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;         // levels taken from in the segment
         int32_t f_vslot = -1;                                 // lane j: the prefetched victim record j removes
-        int32_t Ex0 = 0, Ex1 = 0, Ev0 = 0, Ev1 = 0;
+        int32_t Ex = 0, Ev = 0;
         int nrest = 0, nev = 0;
         int j = j0;
         int32_t oact = 0, osize = 0, flags = 0, rslot = -1, rlev = 0;
@@ -2218,8 +2223,8 @@ struct GroupWave {
             int32_t pb = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
             if (pb != -1 && !check_bit(olo, ohi, pb)) return false;   // the H5 NPE: the serial path raises it
             if (pb != -1 && crosses(IB, rem, pb, P)) {
-                const int64_t q = KME_QGET(OS, pb);
-                if ((int64_t)rem < q) {                        // the best level absorbs it (KP:237-261)
+                const int32_t q = KME_QGET(OS, pb);
+                if (rem < q) {                        // the best level absorbs it (KP:237-261)
                     if (nev + 1 > FAST_EVCAP) return false;
                     KME_QSET(OS, pb, q - rem);
                     if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
@@ -2232,11 +2237,11 @@ struct GroupWave {
 #pragma nounroll
                     for (;;) {                                 // KP:237-253
                         if (nt == FAST_RMAX) { bad = true; break; }
-                        const int64_t qq = KME_QGET(OS, p);
-                        const int32_t x = qq < (int64_t)r ? (int32_t)qq : r;
+                        const int32_t qq = KME_QGET(OS, p);
+                        const int32_t x = qq < r ? qq : r;
                         r -= x;
                         ++nt;
-                        if ((int64_t)x < qq) break;            // stops inside the level
+                        if (x < qq) break;                     // stops inside the level
                         unset_bit(lo, hi, p);                  // taken whole (KP:244-252)
                         const int32_t np = IB ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
                         if (np != -1 && !check_bit(lo, hi, np)) { bad = true; break; }   // H5
@@ -2247,13 +2252,13 @@ struct GroupWave {
                     if (bad || nev + nt + (zl >= 0) + (r > 0) > FAST_EVCAP) return false;
 #pragma nounroll
                     for (int t = 0; t < nt; ++t) {
-                        const int64_t qq = KME_QGET(OS, pb);
-                        const int32_t x = qq < (int64_t)rem ? (int32_t)qq : rem;
+                        const int32_t qq = KME_QGET(OS, pb);
+                        const int32_t x = qq < rem ? qq : rem;
                         rem -= x;
                         KME_QSET(OS, pb, qq - x);
                         if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
                         KME_PUT_EV(nev++, j, EK_TAKE, t, OS * 128 + pb, P, x);
-                        if ((int64_t)x == qq) {
+                        if (x == qq) {
                             unset_bit(olo, ohi, pb);
                             pb = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
                         }
@@ -2263,7 +2268,7 @@ struct GroupWave {
             }
             if (rem > 0) {                                     // addOrder (KP:200-223)
                 if (nev + 1 > FAST_EVCAP) return false;       // (only when nothing was taken: rem == size)
-                const int64_t q = check_bit(slo, shi, P) ? KME_QGET(SIDE, P) : 0;
+                const int32_t q = check_bit(slo, shi, P) ? KME_QGET(SIDE, P) : 0;
                 KME_QSET(SIDE, P, q + rem);
                 set_bit(slo, shi, P);
                 rslot = rl32(fslot, nrest);
@@ -2327,20 +2332,20 @@ struct GroupWave {
                     const int vs = vlev >> 7, vp = vlev & 127;
                     const uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
                     if ((cw >> (vp & 63)) & 1) break;         // its level was taken from: serial
-                    const int64_t q = KME_QGET(vs, vp) - vsz;
+                    const int32_t q = KME_QGET(vs, vp) - vsz;
                     KME_QSET(vs, vp, q);
                     if (q == 0) {
                         if (vs) unset_bit(b1l, b1m, vp); else unset_bit(b0l, b0m, vp);
                     }
-                    if (vrec >= 0) o_act = wlane(rl32(o_act, vrec) | RR_REMOVED, vrec, o_act);
-                    else f_vslot = wlane(vsl, j, f_vslot);
+                    if (vrec >= 0) o_act = wl(rl32(o_act, vrec) | RR_REMOVED, vrec, o_act);
+                    else f_vslot = wl(vsl, j, f_vslot);
                     KME_PUT_EV(nev++, j, EK_CANCEL, 0, vlev, 0, vsl);
                 }
             }
-            o_act = wlane((oact & 0xFFFF) | (flags << 16), j, o_act);
-            o_size = wlane(osize, j, o_size);
-            o_plo = wlane(evb | ((nev - evb) << 8) | (rlev << 16), j, o_plo);
-            o_phi = wlane(rslot, j, o_phi);
+            o_act = wl((oact & 0xFFFF) | (flags << 16), j, o_act);
+            o_size = wl(osize, j, o_size);
+            o_plo = wl(evb | ((nev - evb) << 8) | (rlev << 16), j, o_plo);
+            o_phi = wl(rslot, j, o_phi);
         }
         const int je = j;
         KST(acc[ST_FAST_PASS] += stamp() - tp0;)
@@ -2349,26 +2354,26 @@ struct GroupWave {
         set_bm(1, b1l, b1m);
         set_gs(GS_FSP, fsp0 - nrest);
         {                                                     // quantities back (occupied levels)
-            qv[0] = mk64(Ql0, Qh0); qv[1] = mk64(Ql1, Qh1); qv[2] = mk64(Ql2, Qh2); qv[3] = mk64(Ql3, Qh3);
+            const int32_t qs[4] = {QA, QB, QC, QD};
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                const int sd = h >> 1, p = lane + 64 * (h & 1);
-                if (p <= 100 && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = qv[h];
+                const int sd = h >> 1, p = (h & 1) ? lane + 63 : lane;
+                const bool lv = (h & 1) ? p <= 100 : lane < 63;
+                if (lv && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = (int64_t)qs[h];
             }
         }
         // ---- 2. the level step, 64 events at a time
         KST(const unsigned long long tl0 = stamp();)
         L.trd[lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
         L.rin[lane] = make_int4((int32_t)B.i, B.w0, o_size, 0);
-        L.ev[lane] = make_int4(Ex0, Ev0, Ev0, 0);
-        if (nev > 64) L.ev[64 + lane] = make_int4(Ex1, Ev1, Ev1, 0);
+        L.ev[lane] = make_int4(Ex, Ev, Ev, 0);
         sync_lds();
         int err = 0;
 #pragma nounroll
         for (int c0 = 0; c0 < nev; c0 += 64) {
             const int e = c0 + lane;
             const bool ve = e < nev;
-            const int lev = ((c0 ? Ex1 : Ex0) >> 16) & 0xFF;
+            const int lev = (Ex >> 16) & 0xFF;
             unsigned long long peers = __ballot(ve);          // the chunk's events at lane's level
 #pragma unroll
             for (int bb = 0; bb < 8; ++bb) {
@@ -2566,7 +2571,13 @@ struct GroupWave {
 // (2) FUNDED: one wavefront per symbol group, the group's records in arrival order.
 // all: k_match_lanes is not launched this epoch (its last launch found no light group), so the
 // light groups are k_match's too.
-__global__ void __launch_bounds__(64) k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf,
+// Four wavefronts per SIMD (<= 128 VGPRs; left to itself the compiler takes 134 and three): same-box
+// A/B against three, C2 / C5 / the N = 8 shard shape 1-10% faster (diagnostic builds: -DKME_MATCH_WAVES)
+#ifndef KME_MATCH_WAVES
+#define KME_MATCH_WAVES 4
+#endif
+#define KME_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(KME_MATCH_WAVES)))
+__global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf,
                                               int all) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
