@@ -149,6 +149,34 @@ def exchange_market_data(dist, tob_local, tob_all):
     dist.all_gather_into_tensor(tob_all, tob_local)
 
 
+def library_comm(dist, torch, kme, eng, world: int, rank: int, dev):
+    """The library's own RCCL communicator over the ranks' engines (kme_comm_init; the unique id
+    made on rank 0 and broadcast over torch.distributed), for kme_market_data_allgather.  None when it
+    cannot be made (RCCL not loadable by the library): the bench then all-gathers through torch's
+    RCCL and says so in its line."""
+    # one RCCL for both: the library dlopens the copy torch's own collectives already use
+    trccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if os.path.exists(trccl):
+        os.environ.setdefault("KME_RCCL_LIB", trccl)
+    uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if rank == 0:
+        try:
+            uid.copy_(torch.frombuffer(bytearray(kme.comm_unique_id()), dtype=torch.uint8))
+        except Exception as ex:   # noqa: BLE001 (the fallback is reported)
+            print(f"kme_comm_unique_id: {ex}", file=sys.stderr, flush=True)
+            err.fill_(1)
+    dist.broadcast(err, 0)
+    if int(err.item()):
+        return None
+    dist.broadcast(uid, 0)
+    try:
+        return eng.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+    except Exception as ex:   # noqa: BLE001
+        print(f"rank {rank}: kme_comm_init: {ex}", file=sys.stderr, flush=True)
+        return None
+
+
 def verify_market_data(tob_all, tob_local, rank: int, rows: int) -> bool:
     """After the all-gather, block `rank` of every rank's copy is this rank's own snapshot."""
     return bool((tob_all[rank * rows:(rank + 1) * rows] == tob_local).all().item())
@@ -302,6 +330,16 @@ def main():
     tobs = [torch.full((rows, 4), -1, dtype=torch.int32, device=dev) for _ in range(2)]
     tob = tobs[0]
     tob_all = torch.zeros((world * rows, 4), dtype=torch.int32, device=dev)
+    # N > 1 on GPU ranks: the market data goes through the library's ABI entry (its own RCCL
+    # communicator, kme_market_data_allgather on the engine stream); torch's RCCL all-gather only if
+    # that communicator cannot be made, and in the gloo rehearsal
+    comm = library_comm(dist, torch, kme, eng, world, rank, dev) if world > 1 and not rehearsal else None
+    if world > 1 and not rehearsal:
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()) and comm is not None:
+            comm.close()
+            comm = None
 
     def epoch_ptrs(k):
         return {name: t.data_ptr() + k * E * t.element_size() for name, t in cols.items()}
@@ -315,6 +353,10 @@ def main():
         nonlocal tob
         tob = tobs[k % 2]
         eng.submit_device(epoch_ptrs(k), E)
+        if comm is not None:   # own rows into this rank's block, all-gathered in place over xGMI
+            comm.market_data_allgather(groups.data_ptr(), len(sids), rows, tob_all.data_ptr())
+            tob = tob_all[rank * rows:(rank + 1) * rows]
+            return
         eng.top_of_book_groups(groups.data_ptr(), len(sids), tob.data_ptr())
         if world > 1:
             exchange_market_data(dist, tob, tob_all)   # market-data snapshot over RCCL / xGMI
@@ -382,6 +424,11 @@ def main():
     torch.cuda.synchronize(dev)
     md_local = bool((full[groups.long()] == tob[:len(sids)]).all().item()) and bool((tob[:len(sids), 0] >= 0).any().item())
     md_gather = verify_market_data(tob_all, tob, rank, rows) if world > 1 else True
+    if comm is not None:   # the library's all-gather against torch's, on the last snapshot
+        ref = torch.zeros_like(tob_all)
+        exchange_market_data(dist, tob_all[rank * rows:(rank + 1) * rows].contiguous(), ref)
+        torch.cuda.synchronize(dev)
+        md_gather = md_gather and bool(torch.equal(ref, tob_all))
     md_ok = md_local and md_gather
     if not md_ok:
         print(f"rank {rank}: market data check failed (own snapshot vs full-range: {md_local}, "
@@ -470,7 +517,9 @@ def main():
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
             "market_data": {"symbols": int(sum(len(p) for p in per_rank)), "bytes_per_epoch": int(world * rows * 16),
-                            "collective": ("gloo all_gather (one-GPU rehearsal)" if rehearsal else "RCCL all_gather_into_tensor per epoch")
+                            "collective": ("gloo all_gather (one-GPU rehearsal)" if rehearsal else
+                                           "kme_market_data_allgather (libkme's RCCL communicator) per epoch" if comm is not None
+                                           else "torch.distributed RCCL all_gather_into_tensor per epoch (libkme communicator unavailable)")
                             if world > 1 else "none (N = 1)",
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
@@ -494,6 +543,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(setup, stream, args.cpu_sample)
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     eng.close()
     if world > 1:
         dist.destroy_process_group()
