@@ -22,7 +22,14 @@ def _max_risk(o):
 
 
 def test_one_rank_communicator_market_data_and_rebalance(kme_mod):
+    import os
+
     import torch
+
+    # the RCCL copy bench.py points the library at (torch's own), so one RCCL serves both
+    trccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if os.path.exists(trccl):
+        os.environ.setdefault("KME_RCCL_LIB", trccl)
 
     n_sym, n_acc = 64, 128
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
