@@ -23,7 +23,7 @@ f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
 python3 tools/trace_summary.py $f 5 $OUT/trace_summary.json "C3, 65,536 symbols, E = 2^22, 5 timed epochs" > /dev/null
 bash tools/pmc_kmatch.sh $TAG/pmc k_match_lanes --host-path-epochs 0 || exit $?
 bash tools/pmc_tcc.sh $TAG/tcc k_match_lanes kafka-matching-engine_amd/kme/libkme.so || exit $?
-for extra in "--workload c3 --symbols 8192" "--workload c3 --symbols 32768" "--workload c2" "--workload c5" "--workload c4 --steps 2 --warmup 1" "--workload c4 --epoch 262144 --steps 16 --warmup 2"; do
+for extra in "--workload c3 --symbols 8192" "--workload c3 --symbols 16384" "--workload c3 --symbols 32768" "--workload c2" "--workload c5" "--workload c4 --steps 2 --warmup 1" "--workload c4 --epoch 262144 --steps 16 --warmup 2"; do
   timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --host-path-epochs 0 $extra >> $OUT/bench_extra.jsonl 2>> $OUT/bench_extra.err
   rc=$?; echo "extra [$extra] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
