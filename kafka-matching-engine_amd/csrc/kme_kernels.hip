@@ -1446,6 +1446,38 @@ struct GroupLds {
                                   // their results (trades; has_prev, prev oid)
 };
 
+// Two-wavefront k_match (few busy groups: C2, C4, C5): wave 0 runs the batch loop, the fast
+// segments' aggregate passes and the serial path; wave 1 runs the segments' level steps and
+// epilogues one segment behind, so a busy group costs max(pass, level step) per record instead of
+// their sum (GroupWave::fast_segment<true>, GroupWave::run_levels).  They meet at one workgroup
+// barrier per segment ("phase"); what wave 1 needs crosses in this block.
+constexpr int LFREE = 64;         // node slots wave 1 frees per segment before it chains them as blocks
+struct TwoLds {
+    // double-buffered by phase parity (the next batch's first segment reuses the record lanes of the
+    // segment wave 1 may still have in hand):
+    int4 ev[2][FAST_EVCAP];       // a segment's events
+    int4 rin[2][64];              // record lane k: (input index, PRec w0, rest size, -)
+    int4 rid[2][64];              // record lane k: (oid lo, oid hi, aid lo, aid hi)
+    int4 rec[2][64];              // record lane k: the pass's (action | flags << 16, events, rest slot, BUY/SELL)
+    uint64_t cb[4];               // levels the segment wave 1 has in hand takes from (the pass's c*)
+    int32_t fv[64];               // lane k: the prefetched victim that segment's record k removes
+    uint64_t bcb[4];              // ... and the same of the segment wave 1 had in hand when the batch's
+    int32_t bfv[64];              //     prefetch ran (its writes may predate the batch's dirty filter)
+    int32_t seg[2][4];            // per buffer: first record, end record, events, command
+    int32_t lfree[2][LFREE];      // per buffer: slots wave 1 freed
+    int32_t lfcnt[2], lch_head[2], lch_tail[2];   // ... their count, and the one-slot blocks past LFREE
+    int32_t lerr;                 // wave 1 faulted (its records' fault is raised; wave 0 stops)
+};
+enum { TW_NONE = 0, TW_SEG = 1, TW_EXIT = 2 };
+// The phase barrier of the two wavefronts: each one's memory operations complete before it (the
+// epilogue's rest slots and nodes are read by wave 0's serial path -- through the scalar path, from
+// L2 -- and its batch prefetch; wave 0's serial-path nodes by wave 1's next level step).  Both waves
+// run on one CU and share its L1, so no cache maintenance is needed.
+KDEV void two_barrier() {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+}
+
 KDEV int32_t U32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 // A constant-space view of *p that the compiler cannot hoist: every field read through it is a
 // scalar load at the point of use (GroupWave::cold).
@@ -1543,6 +1575,13 @@ struct GroupWave {
     int32_t g;
     uint32_t cur;                 // input index of the record being processed
     bool dead;
+    TwoLds* tl = nullptr;         // two-wavefront mode (k_match<true>): the block wave 1 reads
+    int kp = 0;                   // wave 0's phase count
+    bool lbusy = false;           // wave 1 has a segment to finish
+    unsigned long long fastmask = 0;   // records of the batch whose results wave 1 produces
+    uint32_t pend_lo = 0, pend_hi = 0; // input indices of the segment wave 1 has in hand
+    uint32_t bpend_lo = 1, bpend_hi = 0;   // ... and of the one it had when the batch's prefetch ran
+    bool bstale = false;          // that segment existed: the prefetched nodes it wrote are not in the dirty filter
 #ifdef KME_STAMPS
     unsigned long long acc[ST_N];
 #endif
@@ -1952,7 +1991,7 @@ struct GroupWave {
         else if (r.tgt <= -2) slot = U32(rest_slot[-(r.tgt + 2)]);   // (RS_PENDING cannot be: arrival order)
         if (slot < 0) return false;                          // orders.get(oid) == null
         Victim o;
-        if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot)) {   // prefetched with the batch
+        if (rl32(B.pf_slot, r.lane) == slot && !is_dirty(slot) && !bstale) {   // prefetched with the batch
             const int32_t meta = rl32(B.pf_meta, r.lane);
             o.ok = (meta >> 11) & 1;
             o.price = meta & 0xFF; o.side = (meta >> 8) & 1; o.sell = (meta >> 9) & 1; o.sid_neg = (meta >> 10) & 1;
@@ -2126,10 +2165,25 @@ struct GroupWave {
     }
     KDEV void lane_dirty(int32_t s) { atomicOr(&L.dirty[(s >> 5) & (DIRTY_WORDS - 1)], 1u << (s & 31)); }
     // a freed node onto the group's free stack (LDS), or, with the stack full, as a one-slot block
-    // pushed on the group's free list
-    KDEV void lane_free(int32_t s) {
+    // pushed on the group's free list.  TWO (wave 1): into buffer lb's list for wave 0 to take at the
+    // phase's end (wave 0 owns the stack), past LFREE as one-slot blocks on a chain of its own
+    template <bool TWO>
+    KDEV void lane_free(int32_t s, int lb) {
         pool[s].live = 0;
         lane_dirty(s);
+        if constexpr (TWO) {
+            const int pos = atomicAdd(&tl->lfcnt[lb], 1);
+            if (pos < LFREE) {
+                tl->lfree[lb][pos] = s;
+            } else {
+                const int32_t old = atomicExch(&tl->lch_head[lb], s);
+                KG int32_t* w = reinterpret_cast<KG int32_t*>(&pool[s]);
+                w[0] = old;
+                w[1] = 0;
+                if (old < 0) tl->lch_tail[lb] = s;
+            }
+            return;
+        }
         const int pos = atomicAdd(&L.gs[GS_FSP], 1);
         if (pos < FSTK) {
             L.fstack[pos] = s;
@@ -2143,6 +2197,7 @@ struct GroupWave {
 
     // Records [j0, nb) of the batch: returns the first record the segment did not take (== j0: none).
     // Per lane (= record) results go to the batch's OUT registers.
+    template <bool TWO>
     KDEV int fast_segment(const Lanes& B, int j0, int nb, int32_t& o_act, int32_t& o_size, int32_t& o_plo,
                           int32_t& o_phi, int32_t& o_ntr, uint32_t& tpos, uint32_t& tlim) {
         const bool inrange = lane >= j0 && lane < nb;
@@ -2164,7 +2219,9 @@ struct GroupWave {
             const bool lv = (h & 1) ? p <= 100 : lane < 63;
             const bool occ = lv && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p);
             qv[h] = occ ? L.qty[sd * LVP + p] : 0;
-            if (lv && !occ) L.ht[sd * LVP + p] = make_int2(-1, -1);
+            // (two waves: only while wave 1 is idle -- its level step keeps the levels it empties
+            // at -1 itself, and only the serial path leaves stale heads behind)
+            if (lv && !occ && (!TWO || !lbusy)) L.ht[sd * LVP + p] = make_int2(-1, -1);
         }
         // 32-bit quantities: every level below 2^30 and every order of the segment below 2^23, so 64
         // rests on one level stay below 2^31; otherwise the records take the serial path
@@ -2199,10 +2256,20 @@ struct GroupWave {
                     cls = B.pf_meta != RS_PENDING || ti < bi0 ? PC_REJECT : (exists ? PC_CANCEL_BATCH : PC_SERIAL);
                 }
             }
+            // Two waves: a same-epoch target in the segment wave 1 had in hand when the batch's
+            // prefetch ran may have rested with its node and slot half written -- the serial path
+            // (after wave 1 is done) reads them again
+            if (TWO && b_act == CANCEL && B.tgt <= -2) {
+                const uint32_t ti = (uint32_t)(-(B.tgt + 2));
+                if (ti >= bpend_lo && ti <= bpend_hi) cls = PC_SERIAL;
+            }
             pk = cls | (b_act == BUY ? 16 : 0) | (P << 8) | (b_act << 16) | (vlev << 24);
         }
-        uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;         // levels taken from in the segment
-        int32_t f_vslot = -1;                                 // lane j: the prefetched victim record j removes
+        // levels taken from in the segment, and lane j: the prefetched victim record j removes (two
+        // waves: the pass also checks those of the segment wave 1 has not finished, tl->cb / tl->fv:
+        // it may not have written their nodes yet)
+        uint64_t c0l = 0, c0m = 0, c1l = 0, c1m = 0;
+        int32_t f_vslot = -1;
         int32_t Ex = 0, Ev = 0;
         int nrest = 0, nev = 0;
         int j = j0;
@@ -2304,7 +2371,7 @@ struct GroupWave {
                 int32_t vlev = -1, vsl = -1, vsz = 0, vrec = -1;
                 if (cls == PC_CANCEL_PF) {
                     const int32_t pfs = rl32(B.pf_slot, j);
-                    if (__ballot(f_vslot == pfs)) {
+                    if (__ballot(f_vslot == pfs || (TWO && lbusy && tl->fv[lane] == pfs) || (TWO && bstale && tl->bfv[lane] == pfs))) {
                         oact = REJECT;                        // removed by an earlier cancel of the segment
                     } else {
                         vlev = (pj >> 24) & 0xFF;
@@ -2330,7 +2397,9 @@ struct GroupWave {
                 if (vlev >= 0) {
                     if (nev + 1 > FAST_EVCAP) break;
                     const int vs = vlev >> 7, vp = vlev & 127;
-                    const uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
+                    uint64_t cw = vs ? (vp < 64 ? c1l : c1m) : (vp < 64 ? c0l : c0m);
+                    if (TWO && lbusy) cw |= U64((int64_t)tl->cb[vs * 2 + (vp < 64 ? 0 : 1)]);
+                    if (TWO && bstale) cw |= U64((int64_t)tl->bcb[vs * 2 + (vp < 64 ? 0 : 1)]);
                     if ((cw >> (vp & 63)) & 1) break;         // its level was taken from: serial
                     const int32_t q = KME_QGET(vs, vp) - vsz;
                     KME_QSET(vs, vp, q);
@@ -2362,126 +2431,35 @@ struct GroupWave {
                 if (lv && check_bit(sd ? b1l : b0l, sd ? b1m : b0m, p)) L.qty[sd * LVP + p] = (int64_t)qs[h];
             }
         }
-        // ---- 2. the level step, 64 events at a time
+        if constexpr (TWO) {
+            // ---- hand the segment to wave 1 (its level step and epilogue run during the next
+            // segment's pass) and end the phase
+            if (lane == 0) { tl->cb[0] = c0l; tl->cb[1] = c0m; tl->cb[2] = c1l; tl->cb[3] = c1m; }
+            tl->fv[lane] = f_vslot;
+            pend_lo = (uint32_t)rl32((int32_t)B.i, j0);
+            pend_hi = (uint32_t)rl32((int32_t)B.i, je - 1);
+            const int buf = kp & 1;
+            if (lane < nev) tl->ev[buf][lane] = make_int4(Ex, Ev, Ev, 0);
+            if (lane >= j0 && lane < je) {
+                tl->rin[buf][lane] = make_int4((int32_t)B.i, B.w0, o_size, 0);
+                tl->rid[buf][lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
+                tl->rec[buf][lane] = make_int4(o_act, o_plo, o_phi, b_bs ? 1 : 0);
+            }
+            if (lane == 0) {
+                tl->seg[buf][0] = j0; tl->seg[buf][1] = je; tl->seg[buf][2] = nev; tl->seg[buf][3] = TW_SEG;
+            }
+            fastmask |= (je >= 64 ? ~0ull : (1ull << je) - 1) & ~((1ull << j0) - 1);
+            phase_end();
+            lbusy = true;
+            return je;
+        }
+        // ---- 2. the level step
         KST(const unsigned long long tl0 = stamp();)
         L.trd[lane] = make_int4(lo32(B.oid), hi32(B.oid), lo32(B.aid), hi32(B.aid));
         L.rin[lane] = make_int4((int32_t)B.i, B.w0, o_size, 0);
         L.ev[lane] = make_int4(Ex, Ev, Ev, 0);
         sync_lds();
-        int err = 0;
-#pragma nounroll
-        for (int c0 = 0; c0 < nev; c0 += 64) {
-            const int e = c0 + lane;
-            const bool ve = e < nev;
-            const int lev = (Ex >> 16) & 0xFF;
-            unsigned long long peers = __ballot(ve);          // the chunk's events at lane's level
-#pragma unroll
-            for (int bb = 0; bb < 8; ++bb) {
-                const unsigned long long m = __ballot(ve && ((lev >> bb) & 1));
-                peers &= ((lev >> bb) & 1) ? m : ~m;
-            }
-            if (ve && __builtin_ctzll(peers) == lane) {
-                const int side = lev >> 7, price = lev & 127, li = side * LVP + price;
-                const int2 ht = L.ht[li];
-                int32_t head = ht.x, tail = ht.y;
-                int64_t toid = L.toid[li];
-                unsigned long long m = peers;
-                while (m) {
-                    const int k = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const int4 f = L.ev[c0 + k];
-                    const int kind = (f.x >> 6) & 3, rk = f.x & 63;
-                    const uint32_t rank = (uint32_t)(f.x >> 8) & 7;
-                    const int4 ri = L.rin[rk];                // the record's (input index, PRec w0, rest size)
-                    if (kind == EK_TAKE) {                    // tryMatch at one level (KP:237-261)
-                        const int32_t P = (f.x >> 24) & 0x7F;
-                        int32_t x = f.y, ms = head;
-                        uint32_t ntr = 0;
-                        bool moved = false;
-                        if (ms < 0) err = 2;
-                        while (ms >= 0) {
-                            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[ms]);
-                            const int4 n0 = nd[0], n1 = nd[1];
-                            if (!(x > 0 || price >= P)) break;   // KP:237 with size 0 (H3); x > 0: crosses
-                            const int32_t ts = imin(x, n1.z);
-                            x -= ts;
-                            lane_emit(tpos, tlim, (uint32_t)ri.x, ntr++ | (rank << FAST_RANK_SHIFT), n0, n1.y < 0, price, ts, err);
-                            if (n1.z - ts != 0) { pool[ms].size = n1.z - ts; lane_dirty(ms); break; }
-                            lane_free(ms);                    // orders.delete (KP:243)
-                            if (n1.w < 0) { if (x != 0) err = 2; ms = -1; break; }   // the level taken whole
-                            ms = n1.w;
-                            moved = true;
-                        }
-                        if (ms < 0) { head = -1; tail = -1; }
-                        else { if (moved) { pool[ms].prev = -1; lane_dirty(ms); } head = ms; }
-                        L.ev[c0 + k].w = (int32_t)ntr;
-                    } else if (kind == EK_ZERO) {             // the next level's head, size 0 (KP:237, H3)
-                        int32_t n = 0;
-                        if (head < 0) {
-                            err = 2;
-                        } else {
-                            const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[head]);
-                            const int4 n0 = nd[0], n1 = nd[1];
-                            lane_emit(tpos, tlim, (uint32_t)ri.x, rank << FAST_RANK_SHIFT, n0, n1.y < 0, price, 0, err);
-                            n = 1;
-                        }
-                        L.ev[c0 + k].w = n;
-                    } else if (kind == EK_REST) {             // addOrder's rest (KP:205-221)
-                        const int4 id = L.trd[rk];
-                        const int32_t slot = f.z;
-                        int32_t nprev = -1, hp = 0;
-                        int64_t poid = 0;
-                        if (head < 0) {
-                            head = slot;
-                        } else {
-                            pool[tail].next = slot;
-                            lane_dirty(tail);
-                            nprev = tail; poid = toid; hp = 1;
-                        }
-                        tail = slot;
-                        toid = mk64(id.x, id.y);
-                        const int32_t sidl = ((ri.y >> 17) & 1) ? -g : g;
-                        KG int4* nd = reinterpret_cast<KG int4*>(&pool[slot]);
-                        nd[0] = id;
-                        nd[1] = make_int4(sidl, sidl < 0 ? -1 : 0, ri.z, -1);
-                        nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
-                        nd[3] = make_int4(price, ri.y & 0xFF, 1, 0);
-                        lane_dirty(slot);
-                        L.ev[c0 + k] = make_int4(f.x, hp, lo32(poid), hi32(poid));
-                    } else {                                  // removeOrder's unlink (KP:297-320)
-                        const int32_t vs = f.z;
-                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[vs]);
-                        const int4 n1 = nd[1], n2 = nd[2], n3 = nd[3];
-                        const int32_t next = n1.w, prev = n2.z;
-                        const int64_t prev_oid = mk64(n2.x, n2.y);
-                        if (prev < 0 && next < 0) {
-                            head = -1; tail = -1;
-                        } else if (prev < 0) {
-                            head = next;
-                            pool[next].prev = -1;
-                            lane_dirty(next);
-                        } else if (next < 0) {
-                            tail = prev; toid = prev_oid;
-                            pool[prev].next = -1;
-                            lane_dirty(prev);
-                        } else {
-                            pool[prev].next = next;
-                            pool[next].prev = prev;
-                            pool[next].prev_oid = prev_oid;
-                            lane_dirty(prev);
-                            lane_dirty(next);
-                        }
-                        lane_free(vs);
-                        if (Sp->ledger_replay)                // the removed order, for postRemoveAdjustments
-                            Sp->vic[ri.x] = make_int4(price | ((n3.y == SELL ? SELL : BUY) << 8), n1.z, n1.y < 0 ? -g : g,
-                                                      n1.y < 0 ? -1 : 0);
-                    }
-                }
-                L.ht[li] = make_int2(head, tail);
-                L.toid[li] = toid;
-            }
-            sync_lds();
-        }
+        const int err = level_step<false>(L.ev, L.rin, L.trd, nev, tpos, tlim, 0);
         KST(const unsigned long long te0 = stamp(); acc[ST_FAST_LEVEL] += te0 - tl0;)
         {
             const int fsp = U32(L.gs[GS_FSP]);
@@ -2489,26 +2467,7 @@ struct GroupWave {
         }
         // per record: its results, its events' trade bases, its oid-table entry (the rest slot, or
         // dead: KP:221)
-        if (lane >= j0 && lane < je) {
-            const int eb = o_plo & 0xFF, en = (o_plo >> 8) & 0xFF;
-            const int32_t rs = o_phi;
-            o_act &= ~RR_REMOVED;
-            o_plo = 0; o_phi = 0;
-            uint32_t ntr = 0;
-            for (int e = eb; e < eb + en; ++e) {
-                const int4 f = L.ev[e];
-                const int kind = (f.x >> 6) & 3, rank = (f.x >> 8) & 7;
-                if (kind == EK_TAKE || kind == EK_ZERO) {
-                    if (rank) Sp->lvbase[(size_t)B.i * FAST_LVB + rank - 1] = ntr;
-                    ntr += (uint32_t)f.w;
-                } else if (kind == EK_REST && f.y) {
-                    o_act |= KME_OUT_HAS_PREV << 16;
-                    o_plo = f.z; o_phi = f.w;
-                }
-            }
-            o_ntr = (int32_t)ntr;
-            if (b_bs && ((o_act >> 16) & 2)) rest_slot[B.i] = rs;
-        }
+        if (lane >= j0 && lane < je) epilogue(L.ev, B.i, b_bs, o_act, o_plo, o_phi, o_ntr);
         sync_lds();
         KST(acc[ST_FAST_EPI] += stamp() - te0;)
         if (__ballot(err != 0)) {
@@ -2516,6 +2475,224 @@ struct GroupWave {
             else dead = true;                                 // CAP_TRADES, raised at its record by lane_emit
         }
         return je;
+    }
+
+    // A segment's events replayed level by level (one lane per touched level): appends at the tail,
+    // takes walking the FIFO from the head maker by maker as KP:237-261 does, unlinks (KP:297-320).
+    // ev / rin / rid: the segment's events and its records' (input index, w0, rest size) / (oid, aid)
+    // by record lane.  Returns 2 for the reference's NPE (a take finding no maker), 1 when a trade
+    // reservation failed (raised at its record), else 0.  TWO: wave 1's call, freed slots to buffer lb.
+    template <bool TWO>
+    KDEV int level_step(int4* ev, const int4* rin, const int4* rid, int nev, uint32_t& tpos, uint32_t& tlim, int lb) {
+        int err = 0;
+        const int e = lane;
+        const bool ve = e < nev;
+        const int lev = ve ? (ev[e].x >> 16) & 0xFF : 0;
+        unsigned long long peers = __ballot(ve);              // the segment's events at lane's level
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            const unsigned long long m = __ballot(ve && ((lev >> bb) & 1));
+            peers &= ((lev >> bb) & 1) ? m : ~m;
+        }
+        if (ve && __builtin_ctzll(peers) == lane) {
+            const int side = lev >> 7, price = lev & 127, li = side * LVP + price;
+            const int2 ht = L.ht[li];
+            int32_t head = ht.x, tail = ht.y;
+            int64_t toid = L.toid[li];
+            unsigned long long m = peers;
+            while (m) {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1;
+                const int4 f = ev[k];
+                const int kind = (f.x >> 6) & 3, rk = f.x & 63;
+                const uint32_t rank = (uint32_t)(f.x >> 8) & 7;
+                const int4 ri = rin[rk];                      // the record's (input index, PRec w0, rest size)
+                if (kind == EK_TAKE) {                        // tryMatch at one level (KP:237-261)
+                    const int32_t P = (f.x >> 24) & 0x7F;
+                    int32_t x = f.y, ms = head;
+                    uint32_t ntr = 0;
+                    bool moved = false;
+                    if (ms < 0) err = 2;
+                    while (ms >= 0) {
+                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[ms]);
+                        const int4 n0 = nd[0], n1 = nd[1];
+                        if (!(x > 0 || price >= P)) break;    // KP:237 with size 0 (H3); x > 0: crosses
+                        const int32_t ts = imin(x, n1.z);
+                        x -= ts;
+                        lane_emit(tpos, tlim, (uint32_t)ri.x, ntr++ | (rank << FAST_RANK_SHIFT), n0, n1.y < 0, price, ts, err);
+                        if (n1.z - ts != 0) { pool[ms].size = n1.z - ts; lane_dirty(ms); break; }
+                        lane_free<TWO>(ms, lb);               // orders.delete (KP:243)
+                        if (n1.w < 0) { if (x != 0) err = 2; ms = -1; break; }   // the level taken whole
+                        ms = n1.w;
+                        moved = true;
+                    }
+                    if (ms < 0) { head = -1; tail = -1; }
+                    else { if (moved) { pool[ms].prev = -1; lane_dirty(ms); } head = ms; }
+                    ev[k].w = (int32_t)ntr;
+                } else if (kind == EK_ZERO) {                 // the next level's head, size 0 (KP:237, H3)
+                    int32_t n = 0;
+                    if (head < 0) {
+                        err = 2;
+                    } else {
+                        const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[head]);
+                        const int4 n0 = nd[0], n1 = nd[1];
+                        lane_emit(tpos, tlim, (uint32_t)ri.x, rank << FAST_RANK_SHIFT, n0, n1.y < 0, price, 0, err);
+                        n = 1;
+                    }
+                    ev[k].w = n;
+                } else if (kind == EK_REST) {                 // addOrder's rest (KP:205-221)
+                    const int4 id = rid[rk];
+                    const int32_t slot = f.z;
+                    int32_t nprev = -1, hp = 0;
+                    int64_t poid = 0;
+                    if (head < 0) {
+                        head = slot;
+                    } else {
+                        pool[tail].next = slot;
+                        lane_dirty(tail);
+                        nprev = tail; poid = toid; hp = 1;
+                    }
+                    tail = slot;
+                    toid = mk64(id.x, id.y);
+                    const int32_t sidl = ((ri.y >> 17) & 1) ? -g : g;
+                    KG int4* nd = reinterpret_cast<KG int4*>(&pool[slot]);
+                    nd[0] = id;
+                    nd[1] = make_int4(sidl, sidl < 0 ? -1 : 0, ri.z, -1);
+                    nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
+                    nd[3] = make_int4(price, ri.y & 0xFF, 1, 0);
+                    lane_dirty(slot);
+                    ev[k] = make_int4(f.x, hp, lo32(poid), hi32(poid));
+                } else {                                      // removeOrder's unlink (KP:297-320)
+                    const int32_t vs = f.z;
+                    const KG int4* nd = reinterpret_cast<const KG int4*>(&pool[vs]);
+                    const int4 n1 = nd[1], n2 = nd[2], n3 = nd[3];
+                    const int32_t next = n1.w, prev = n2.z;
+                    const int64_t prev_oid = mk64(n2.x, n2.y);
+                    if (prev < 0 && next < 0) {
+                        head = -1; tail = -1;
+                    } else if (prev < 0) {
+                        head = next;
+                        pool[next].prev = -1;
+                        lane_dirty(next);
+                    } else if (next < 0) {
+                        tail = prev; toid = prev_oid;
+                        pool[prev].next = -1;
+                        lane_dirty(prev);
+                    } else {
+                        pool[prev].next = next;
+                        pool[next].prev = prev;
+                        pool[next].prev_oid = prev_oid;
+                        lane_dirty(prev);
+                        lane_dirty(next);
+                    }
+                    lane_free<TWO>(vs, lb);
+                    if (Sp->ledger_replay)                    // the removed order, for postRemoveAdjustments
+                        Sp->vic[ri.x] = make_int4(price | ((n3.y == SELL ? SELL : BUY) << 8), n1.z, n1.y < 0 ? -g : g,
+                                                  n1.y < 0 ? -1 : 0);
+                }
+            }
+            L.ht[li] = make_int2(head, tail);
+            L.toid[li] = toid;
+        }
+        sync_lds();
+        return err;
+    }
+
+    // One record's results after the level step (the lane of a record of the segment): trade count,
+    // per-event trade bases (lvbase, k_scatter), OUT.prev of an append, its oid-table entry's rest slot.
+    KDEV void epilogue(const int4* ev, uint32_t bi, bool bs, int32_t& o_act, int32_t& o_plo, int32_t& o_phi,
+                       int32_t& o_ntr) {
+        const int eb = o_plo & 0xFF, en = (o_plo >> 8) & 0xFF;
+        const int32_t rs = o_phi;
+        o_act &= ~RR_REMOVED;
+        o_plo = 0; o_phi = 0;
+        uint32_t ntr = 0;
+        for (int e = eb; e < eb + en; ++e) {
+            const int4 f = ev[e];
+            const int kind = (f.x >> 6) & 3, rank = (f.x >> 8) & 7;
+            if (kind == EK_TAKE || kind == EK_ZERO) {
+                if (rank) Sp->lvbase[(size_t)bi * FAST_LVB + rank - 1] = ntr;
+                ntr += (uint32_t)f.w;
+            } else if (kind == EK_REST && f.y) {
+                o_act |= KME_OUT_HAS_PREV << 16;
+                o_plo = f.z; o_phi = f.w;
+            }
+        }
+        o_ntr = (int32_t)ntr;
+        if (bs && ((o_act >> 16) & 2)) rest_slot[bi] = rs;
+    }
+
+    // ---------------- two-wavefront mode (k_match<true>)
+    // wave 0: the end of a phase -- the workgroup barrier; then wave 1 has finished the segment of the
+    // phase before, whose freed slots go onto the group's free stack / free list here
+    KDEV void phase_end() {
+        two_barrier();
+        const int b = (kp + 1) & 1;                           // the buffer wave 1 just finished
+        ++kp;
+        const int n = imin(U32(tl->lfcnt[b]), LFREE);
+        if (n > 0) {
+            const int fsp = gsv(GS_FSP), room = imin(n, FSTK - fsp);
+            const int32_t s = lane < n ? tl->lfree[b][lane] : -1;
+            if (lane < room) L.fstack[fsp + lane] = s;
+            if (room < n) {                                   // the rest as one-slot blocks, chained
+                const int32_t nx = __shfl(s, lane + 1 < n ? lane + 1 : lane);
+                const int32_t old = gsv(GS_FREE_HEAD);
+                if (lane >= room && lane < n) {
+                    KG int32_t* w = reinterpret_cast<KG int32_t*>(&pool[s]);
+                    w[0] = lane + 1 < n ? nx : old;
+                    w[1] = 0;
+                }
+                set_gs(GS_FREE_HEAD, rl32(s, room));
+            }
+            set_gs(GS_FSP, fsp + room);
+        }
+        const int32_t ch = U32(tl->lch_head[b]);
+        if (ch >= 0) {                                        // wave 1's overflow chain onto the free list
+            if (lane == 0) reinterpret_cast<KG int32_t*>(&pool[U32(tl->lch_tail[b])])[0] = gsv(GS_FREE_HEAD);
+            set_gs(GS_FREE_HEAD, ch);
+        }
+        if (lane == 0) { tl->lfcnt[b] = 0; tl->lch_head[b] = -1; tl->lch_tail[b] = -1; }
+        if (U32(tl->lerr)) dead = true;                       // (raised by wave 1 at its record)
+        sync_lds();
+    }
+    // wave 0: wave 1 idle (nothing handed over in this phase), before the serial path, the next
+    // batch's prefetch and the group's end
+    KDEV void drain() {
+        if (!lbusy) return;
+        if (lane == 0) tl->seg[kp & 1][3] = TW_NONE;
+        phase_end();
+        lbusy = false;
+    }
+    // wave 1: every phase, the segment wave 0 handed over in the phase before; returns at TW_EXIT
+    KDEV void run_levels(uint32_t& tpos, uint32_t& tlim) {
+        for (int k = 0;; ++k) {
+            if (k > 0) {
+                const int b = (k - 1) & 1;
+                if (U32(tl->seg[b][3]) == TW_SEG) {
+                    const int j0 = U32(tl->seg[b][0]), je = U32(tl->seg[b][1]), nev = U32(tl->seg[b][2]);
+                    const int err = level_step<true>(tl->ev[b], tl->rin[b], tl->rid[b], nev, tpos, tlim, b);
+                    // the segment's records: epilogue and OUT echo (wave 0 stores the other records')
+                    const bool mine = lane >= j0 && lane < je;
+                    int32_t on = 0;
+                    if (mine) {
+                        const int4 rc = tl->rec[b][lane], ri = tl->rin[b][lane];
+                        int32_t oa = rc.x, op = rc.y, oh = rc.z;
+                        epilogue(tl->ev[b], (uint32_t)ri.x, rc.w != 0, oa, op, oh, on);
+                        Sp->osort[(uint32_t)ri.x] = make_int4((oa & 0xFF) | (((oa >> 16) & KME_OUT_HAS_PREV) << 8) | (on << 9),
+                                                              ri.z, op, oh);
+                    }
+                    // a record with more trades than an ordinal counts (k_match's batch check)
+                    const unsigned long long big = __ballot(mine && (uint32_t)on >= OS_MAX_NTR);
+                    if (big) raise_wave(ctr(), KME_E_CAPACITY, KME_D_CAP_TRADES, (int64_t)U32(tl->rin[b][__builtin_ctzll(big)].x));
+                    if (__ballot(err != 0) && __ballot(err == 2))
+                        raise_wave(ctr(), KME_E_DOMAIN, KME_D_NPE_ORDER, (int64_t)U32(tl->rin[b][j0].x));
+                    if ((big || __ballot(err != 0)) && lane == 0) tl->lerr = 1;
+                }
+            }
+            two_barrier();
+            if (U32(tl->seg[k & 1][3]) == TW_EXIT) break;
+        }
+        for (uint32_t q = tpos; q < tlim; ++q) Sp->ttmp[q].seq = -1;   // unused trade reservations
     }
 
     // ---------------- one record (MatchingEngine.process, KP:96-126)
@@ -2577,8 +2754,10 @@ struct GroupWave {
 #define KME_MATCH_WAVES 4
 #endif
 #define KME_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(KME_MATCH_WAVES)))
-__global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf,
-                                              int all) {
+// TWO: two wavefronts per group (TwoLds): wave 0 below, wave 1 GroupWave::run_levels.
+template <bool TWO>
+__global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
+                                                                      int buf, int all) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
     const int32_t g = blockIdx.x;
@@ -2590,9 +2769,20 @@ __global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __r
     if (threadIdx.x == 0 && e - b > (uint32_t)S.light_max) atomicAdd(&S.ctr[ci(C_BUSY)], 1ull);
     KST(const unsigned long long tk0 = stamp();)
     GroupWave w(S, lds, g);
+    const int lane = lane_id();
+    if constexpr (TWO) {
+        __shared__ TwoLds tls;
+        w.tl = &tls;
+        if (threadIdx.x >= 64) {                            // wave 1: the level steps
+            uint32_t tpos = 0, tlim = 0;
+            w.run_levels(tpos, tlim);
+            return;
+        }
+        if (lane < 2) { tls.lfcnt[lane] = 0; tls.lch_head[lane] = -1; tls.lch_tail[lane] = -1; }
+        if (lane == 0) tls.lerr = 0;
+    }
     w.load_group();
     KST(w.acc[ST_GROUP_IN] += stamp() - tk0;)
-    const int lane = lane_id();
     uint32_t n_rest = 0, n_cancel = 0;
     bool stop = false;
     // fast segments (GroupWave::fast_segment): not for group 0 (one shared book, H4) nor once a
@@ -2644,6 +2834,15 @@ __global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __r
             B.pf_size = c1.z; B.pf_next = c1.w; B.pf_prev = c2.z;
         }
         lds.dirty[lane] = 0;
+        if constexpr (TWO) {   // the segment wave 1 has in hand: its writes may predate the filter
+            w.bstale = w.lbusy;
+            w.bpend_lo = w.lbusy ? w.pend_lo : 1u;
+            w.bpend_hi = w.lbusy ? w.pend_hi : 0u;
+            if (w.lbusy) {
+                if (lane < 4) w.tl->bcb[lane] = w.tl->cb[lane];
+                w.tl->bfv[lane] = w.tl->fv[lane];
+            }
+        }
         w.sync_lds();
         // The lane registers are read with readlane inside the record loop.  Waiting for them here
         // once keeps the waitcnt pass from placing a vmcnt(0) at the loop header, which would make
@@ -2660,10 +2859,14 @@ __global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __r
         for (int j = 0; j < nb; ++j) {
             if (fast) {
                 KST(const unsigned long long tf0 = stamp(); const int jf0 = j;)
-                j = w.fast_segment(B, j, nb, o_act, o_size, o_plo, o_phi, o_ntr, ftpos, ftlim);
+                j = w.fast_segment<TWO>(B, j, nb, o_act, o_size, o_plo, o_phi, o_ntr, ftpos, ftlim);
                 KST(w.acc[ST_FAST] += stamp() - tf0; w.acc[ST_N_FAST_REC] += (unsigned long long)(j - jf0); w.acc[ST_N_FAST_SEG] += j > jf0;)
                 if (w.dead) { done = j; break; }
                 if (j >= nb) break;
+            }
+            if constexpr (TWO) {                            // the serial path: every node final
+                w.drain();
+                if (w.dead) { done = j; break; }
             }
             KST(const unsigned long long tr0 = stamp();)
             Rec r;
@@ -2701,7 +2904,9 @@ __global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __r
         }
         {   // a record with more trades than an ordinal counts: the fault is that record (the ones before
             // it in the batch are answered)
-            const unsigned long long big = __ballot(lane < done && (uint32_t)o_ntr >= OS_MAX_NTR);
+            // (two waves: wave 1 checks the records of fast segments, GroupWave::run_levels)
+            const bool mine = !TWO || !((w.fastmask >> lane) & 1);
+            const unsigned long long big = __ballot(lane < done && mine && (uint32_t)o_ntr >= OS_MAX_NTR);
             if (big) {
                 done = __builtin_ctzll(big);
                 w.cur = (uint32_t)rl32((int32_t)B.i, done);
@@ -2714,13 +2919,24 @@ __global__ void __launch_bounds__(64) KME_MATCH_ATTR k_match(const DevState* __r
             // past the batch's last answered record store to a dump slot behind the array instead of
             // branching: a divergent branch here joins the loop latch, and the uniformity analysis then
             // takes the batch loop's exit (w.dead) as divergent, demoting its state to lane masks
-            const size_t dst = lane < done ? (size_t)B.i : (size_t)opaque_const(Sp).os_base + (size_t)lane;
+            // (two waves: wave 1 stores those of fast segments)
+            const bool mine = !TWO || !((w.fastmask >> lane) & 1);
+            const size_t dst = lane < done && mine ? (size_t)B.i : (size_t)opaque_const(Sp).os_base + (size_t)lane;
             opaque_const(Sp).osort[dst] = make_int4((o_act & 0xFF) | (((o_act >> 16) & KME_OUT_HAS_PREV) << 8) | (o_ntr << 9),
                                                     o_size, o_plo, o_phi);
+        }
+        if constexpr (TWO) {
+            w.fastmask = 0;
+            if (S.fast & 2) w.drain();                      // (diagnostic: no overlap across batches)
         }
     }
     KST(const unsigned long long to0 = stamp();)
     w.flush_trades();
+    if constexpr (TWO) {                                    // wave 1 finishes, then leaves
+        w.drain();
+        if (lane == 0) w.tl->seg[w.kp & 1][3] = TW_EXIT;
+        two_barrier();
+    }
     for (uint32_t q = ftpos; q < ftlim; ++q) S.ttmp[q].seq = -1;   // the fast segments' unused reservations
     KST(w.acc[ST_FLUSH] += stamp() - to0;)
     w.store_group();
@@ -3636,8 +3852,9 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src);
     return src;
 }
-void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all) {
-    hipLaunchKernelGGL(k_match, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all);
+void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two) {
+    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all);
+    else hipLaunchKernelGGL(k_match<false>, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

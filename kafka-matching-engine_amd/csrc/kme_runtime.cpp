@@ -43,6 +43,9 @@ struct kme_engine {
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint64_t last_busy = 1;              // groups k_match took in the last epoch (C_BUSY)
+    // k_match in two-wavefront mode up to this many busy groups (KME_TWO_MAX); off by default: built
+    // and parity-green, but measured +1-2% at C2 / C4 and -10% at C5
+    uint64_t two_max = 0;
     uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
     DevState S{};
@@ -282,6 +285,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.os_base = E;
     S.fast = 1;
     if (const char* v = std::getenv("KME_FAST")) S.fast = std::atoi(v) != 0;   // A/B diagnostics
+    if (const char* v = std::getenv("KME_TWO_DRAIN")) if (S.fast && std::atoi(v)) S.fast |= 2;   // diagnostics
+    if (const char* v = std::getenv("KME_TWO_MAX")) e->two_max = (uint64_t)std::max(0, std::atoi(v));   // A/B diagnostics
     if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
@@ -430,7 +435,10 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         } else if (lanes) {
             launch_match_lanes(S, e->d_S, e->d_io, buf, st);
         }
-        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1);
+        // two wavefronts per busy group when few groups were busy (KME_TWO_MAX, off by default), where
+        // a group's record chain, not the CU's issue rate, is the bound
+        const bool two = S.fast && e->two_max > 0 && e->last_busy <= e->two_max;
+        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);

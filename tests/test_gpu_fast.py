@@ -5,7 +5,8 @@ end exactly on a maker boundary (H3's zero-size trades, KP:237), cancels of make
 the level a later record takes from, several cancels of one level in one batch, duplicate cancels,
 cancels of orders of the same batch (the serial path), and takes that empty their level (the serial
 path).  Every test runs with the fast path on and off (KME_FAST=0) and requires both to be the
-oracle's tape and books byte for byte."""
+oracle's tape and books byte for byte; "two" runs the fast path in k_match's two-wavefront mode
+(KME_TWO_MAX: the aggregate pass on one wavefront, the level steps one segment behind on another).""" 
 import os
 
 import numpy as np
@@ -16,18 +17,23 @@ from kme import workloads as W
 pytestmark = pytest.mark.gpu
 
 
+MODES = [True, False, "two"]
+
+
 def _run(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, fast, epoch=1 << 14, light_max=-1):
-    old = os.environ.get("KME_FAST")
-    os.environ["KME_FAST"] = "1" if fast else "0"
+    env = {"KME_FAST": "1" if fast else "0", "KME_TWO_MAX": "4096" if fast == "two" else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=epoch,
                                                     max_resting=1 << 20, max_trades=4 * epoch, max_accounts=n_acc,
                                                     light_max=light_max))
     finally:
-        if old is None:
-            os.environ.pop("KME_FAST")
-        else:
-            os.environ["KME_FAST"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     o = oracle_mod.Oracle()
     for part in [setup] + [stream.slice(a, min(len(stream), a + epoch)) for a in range(0, len(stream), epoch)]:
         got = eng.process(part).tape_json(part)
@@ -42,7 +48,7 @@ def _run(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, fast, epoch=1 << 14, 
     eng.close()
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 @pytest.mark.parametrize("n_sym,seed", [(1, 1), (3, 2), (16, 3)])
 def test_deep_books_few_symbols(kme_mod, oracle_mod, fast, n_sym, seed):
     """Uniform flow on 1-16 symbols: thousands of records per group and epoch, most batches one
@@ -53,7 +59,7 @@ def test_deep_books_few_symbols(kme_mod, oracle_mod, fast, n_sym, seed):
     _run(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, fast)
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 def test_narrow_band_exact_boundaries(kme_mod, oracle_mod, fast):
     """Prices in a 3-tick band and sizes from {1, 2, 3}: takes end exactly on maker boundaries all
     the time (zero-size trades against the next maker of the level, SELL always, BUY when the level
@@ -67,7 +73,7 @@ def test_narrow_band_exact_boundaries(kme_mod, oracle_mod, fast):
     _run(kme_mod, oracle_mod, setup, o, n_sym, n_acc, fast)
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 def test_cancel_replace_churn_and_sweeps(kme_mod, oracle_mod, fast):
     """C5's shape on 8 symbols: quotes cancelled and replaced at the touch, sweeps across levels (the
     serial path) between fast segments."""
@@ -77,7 +83,7 @@ def test_cancel_replace_churn_and_sweeps(kme_mod, oracle_mod, fast):
     _run(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, fast)
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 def test_constructed_batch_interactions(kme_mod, oracle_mod, fast):
     """One symbol, hand-made: a deep bid level, then in one batch cancels of its head maker and of a
     maker right behind the head, a SELL taking across the head region, rests appended behind, a
@@ -108,7 +114,7 @@ def test_constructed_batch_interactions(kme_mod, oracle_mod, fast):
     _run(kme_mod, oracle_mod, setup, stream, 1, 4, fast, epoch=1 << 10)
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 def test_constructed_sweeps_and_same_batch_cancels(kme_mod, oracle_mod, fast):
     """One symbol, hand-made, one batch: sweeps that take whole levels and end exactly on a level's
     end (the zero-size trade is against the NEXT level's head when it still crosses with size 0,
@@ -145,7 +151,7 @@ def test_constructed_sweeps_and_same_batch_cancels(kme_mod, oracle_mod, fast):
     _run(kme_mod, oracle_mod, setup, stream, 1, 4, fast, epoch=1 << 10)
 
 
-@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("fast", MODES)
 @pytest.mark.parametrize("seed", [5, 6])
 def test_sweeps_over_thin_levels(kme_mod, oracle_mod, fast, seed):
     """Thin levels (sizes 1-3) in a 10-tick band on 2 symbols, takers 1-12: most takes sweep several
