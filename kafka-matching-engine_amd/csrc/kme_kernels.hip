@@ -1463,6 +1463,7 @@ struct TwoLds {
     int32_t fv[64];               // lane k: the prefetched victim that segment's record k removes
     uint64_t bcb[4];              // ... and the same of the segment wave 1 had in hand when the batch's
     int32_t bfv[64];              //     prefetch ran (its writes may predate the batch's dirty filter)
+    uint32_t tb[8], btb[8];       // levels (side * 128 + price) with events in those two segments
     int32_t seg[2][4];            // per buffer: first record, end record, events, command
     int32_t lfree[2][LFREE];      // per buffer: slots wave 1 freed
     int32_t lfcnt[2], lch_head[2], lch_tail[2];   // ... their count, and the one-slot blocks past LFREE
@@ -1555,6 +1556,7 @@ struct Lanes {
     int32_t pf_slot, pf_meta, pf_size, pf_next, pf_prev;   // pf_meta = price | side << 8 | sell << 9 | sid<0 << 10 | ok << 11
                                                            // (pf_slot < 0: rest_slot of this epoch's target)
     int64_t pf_poid;
+    int32_t vl;                   // a cancel's target level from k_route (price | side << 8 | 1 << 9), or 0
 };
 
 // Diagnostic stamp slots of the -DKME_STAMPS build (cycles unless named n_*), per group.
@@ -1736,8 +1738,8 @@ struct GroupWave {
     // is the only writer of its LDS, so a plain read-modify-write by all lanes is exact).
     KDEV void mark_dirty(int32_t s) {
         const int w = (s >> 5) & (DIRTY_WORDS - 1);
-        const uint32_t v = L.dirty[w];
-        L.dirty[w] = v | (1u << (s & 31));
+        // (an atomic: in the two-wavefront mode wave 1 may be marking the same word)
+        atomicOr(&L.dirty[w], 1u << (s & 31));
     }
     KDEV bool is_dirty(int32_t s) const { return (U32((int32_t)L.dirty[(s >> 5) & (DIRTY_WORDS - 1)]) >> (s & 31)) & 1; }
 
@@ -2009,6 +2011,9 @@ struct GroupWave {
             uint64_t lo = bl(o.side), hi = bm(o.side);
             unset_bit(lo, hi, o.price);
             set_bm(o.side, lo, hi);
+            // (an empty level's head for the fast segments' level step: in the two-wavefront mode
+            // this cancel may run beside wave 1, and no segment start resets the heads then)
+            L.ht[li] = make_int2(-1, -1);
         } else if (o.prev < 0) {
             L.ht[li].x = o.next;
             pool[o.next].prev = -1;
@@ -2438,6 +2443,9 @@ struct GroupWave {
             tl->fv[lane] = f_vslot;
             pend_lo = (uint32_t)rl32((int32_t)B.i, j0);
             pend_hi = (uint32_t)rl32((int32_t)B.i, je - 1);
+            if (lane < 8) tl->tb[lane] = 0;
+            sync_lds();
+            if (lane < nev) atomicOr(&tl->tb[(Ex >> 21) & 7], 1u << ((Ex >> 16) & 31));
             const int buf = kp & 1;
             if (lane < nev) tl->ev[buf][lane] = make_int4(Ex, Ev, Ev, 0);
             if (lane >= j0 && lane < je) {
@@ -2626,7 +2634,9 @@ struct GroupWave {
     // wave 0: the end of a phase -- the workgroup barrier; then wave 1 has finished the segment of the
     // phase before, whose freed slots go onto the group's free stack / free list here
     KDEV void phase_end() {
+        KST(const unsigned long long tw0 = stamp();)
         two_barrier();
+        KST(acc[ST_FAST_LEVEL] += stamp() - tw0;)          // (two waves: wave 0's wait for wave 1)
         const int b = (kp + 1) & 1;                           // the buffer wave 1 just finished
         ++kp;
         const int n = imin(U32(tl->lfcnt[b]), LFREE);
@@ -2803,8 +2813,9 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
             const int4 p0 = prec[2 * (size_t)B.i], p1 = prec[2 * (size_t)B.i + 1];
             B.w0 = p0.x; B.size = p0.y;
             B.oid = mk64(p0.z, p0.w); B.aid = mk64(p1.x, p1.y); B.tgt = p1.z;
+            B.vl = (p0.x & 0xFF) == CANCEL ? p1.w : 0;
         } else {
-            B.w0 = 0xFF; B.size = 0; B.oid = B.aid = 0; B.tgt = -1;
+            B.w0 = 0xFF; B.size = 0; B.oid = B.aid = 0; B.tgt = -1; B.vl = 0;
         }
         const int32_t b_action = B.w0 & 0xFF;
         // cancels: the target node, if it came to rest before this batch (an earlier epoch, or an
@@ -2840,6 +2851,7 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
             w.bpend_hi = w.lbusy ? w.pend_hi : 0u;
             if (w.lbusy) {
                 if (lane < 4) w.tl->bcb[lane] = w.tl->cb[lane];
+                if (lane < 8) w.tl->btb[lane] = w.tl->tb[lane];
                 w.tl->bfv[lane] = w.tl->fv[lane];
             }
         }
@@ -2864,8 +2876,25 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
                 if (w.dead) { done = j; break; }
                 if (j >= nb) break;
             }
-            if constexpr (TWO) {                            // the serial path: every node final
-                w.drain();
+            if constexpr (TWO) {
+                // the serial path needs every node it reads final: wave 1 finishes its segment first,
+                // except for a cancel whose victim's level neither the segment in flight nor the one
+                // in flight at the batch's prefetch touches (their levels' lists, heads and nodes are
+                // the cancel's alone) and whose same-epoch target is in neither
+                bool wait = true;
+                if (w.lbusy && (rl32(B.w0, j) & 0xFF) == CANCEL) {
+                    const int32_t vl = rl32(B.vl, j), tg = rl32(B.tgt, j);
+                    if ((vl >> 9) & 1) {
+                        const int lev = ((vl >> 8) & 1) * 128 + (vl & 0xFF);
+                        const uint32_t bit = 1u << (lev & 31);
+                        wait = (U32((int32_t)w.tl->tb[lev >> 5]) & bit) || (w.bstale && (U32((int32_t)w.tl->btb[lev >> 5]) & bit));
+                        if (tg <= -2) {
+                            const uint32_t ti = (uint32_t)(-(tg + 2));
+                            wait = wait || (ti >= w.pend_lo && ti <= w.pend_hi) || (ti >= w.bpend_lo && ti <= w.bpend_hi);
+                        }
+                    }
+                }
+                if (wait) w.drain();
                 if (w.dead) { done = j; break; }
             }
             KST(const unsigned long long tr0 = stamp();)
