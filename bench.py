@@ -350,13 +350,18 @@ def main():
     def submit_epoch(k):
         """Queue epoch k and its market-data snapshot (double-buffered: the next epoch may be queued
         before this one is waited for)."""
-        nonlocal tob
+        nonlocal tob, comm
         tob = tobs[k % 2]
         eng.submit_device(epoch_ptrs(k), E)
         if comm is not None:   # own rows into this rank's block, all-gathered in place over xGMI
-            comm.market_data_allgather(groups.data_ptr(), len(sids), rows, tob_all.data_ptr())
-            tob = tob_all[rank * rows:(rank + 1) * rows]
-            return
+            try:
+                comm.market_data_allgather(groups.data_ptr(), len(sids), rows, tob_all.data_ptr())
+                tob = tob_all[rank * rows:(rank + 1) * rows]
+                return
+            except kme.KmeError as ex:   # (reported in the line: the collective falls back to torch's)
+                print(f"rank {rank}: kme_market_data_allgather: {ex}; torch.distributed from here on",
+                      file=sys.stderr, flush=True)
+                comm = None
         eng.top_of_book_groups(groups.data_ptr(), len(sids), tob.data_ptr())
         if world > 1:
             exchange_market_data(dist, tob, tob_all)   # market-data snapshot over RCCL / xGMI
