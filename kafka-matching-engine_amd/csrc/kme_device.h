@@ -82,7 +82,7 @@ struct TradeTmp {                  // unordered trade scratch written by the gro
 static_assert(sizeof(TradeTmp) == 32, "TradeTmp");
 constexpr uint32_t TT_ORD_BITS = 23;       // a record's trade ordinals (OS_MAX_NTR) fit
 constexpr uint32_t FAST_RANK_SHIFT = 20;   // fast segments: ordinal = index | event rank << 20
-constexpr int FAST_LVB = 4;                // lvbase words per record: event ranks 1..4
+constexpr int FAST_LVB = 7;                // lvbase words per record: event ranks 1..7 (a sweep over <= 7 levels)
 KDEV_HOST_INLINE uint32_t tt_ordp(uint32_t ord, int32_t price, bool sneg) {
     return ord | ((uint32_t)price << TT_ORD_BITS) | (sneg ? 1u << 30 : 0u);
 }
@@ -149,7 +149,7 @@ struct DevState {
     KG int32_t* route_grp;
     KG int64_t* cancel_tgt;           // EXACT: cancel target (FUNDED: in the packed record)
     KG int32_t* rest_slot;
-    KG uint32_t* lvbase;              // FUNDED: fast segments' per-record trade bases of event ranks 1..4
+    KG uint32_t* lvbase;              // FUNDED: fast segments' per-record trade bases of event ranks 1..FAST_LVB
     KG int4* vic;                     // FUNDED + exact ledger: per accepted cancel, the removed order
                                       // (price | action << 8, size, sid) for postRemoveAdjustments
     KG int4* prec;                    // FUNDED: packed records, 32 B each (k_route -> k_match):

@@ -919,6 +919,7 @@ struct Rec {
 };
 constexpr uint32_t OS_MAX_NTR = 1u << FAST_RANK_SHIFT;   // trades of one record: a plain ordinal in TradeTmp::ordp
 static_assert(FAST_RANK_SHIFT + 3 <= TT_ORD_BITS, "a fast segment's ordinal (index | event rank << 20) in TradeTmp::ordp");
+static_assert(FAST_LVB <= 7, "a sweep's event ranks 0..FAST_LVB in three bits");
 // What process() decided for one record (the OUT echo fields and its trade count).
 struct Out {
     int32_t action, size;

@@ -43,9 +43,11 @@ struct kme_engine {
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint64_t last_busy = 1;              // groups k_match took in the last epoch (C_BUSY)
-    // k_match in two-wavefront mode up to this many busy groups (KME_TWO_MAX); off by default: built
-    // and parity-green, but measured +1-2% at C2 / C4 and -10% at C5
-    uint64_t two_max = 0;
+    // k_match in two-wavefront mode when 1 .. two_max groups were busy in the last epoch (KME_TWO_MAX;
+    // 0: never) and fewer than 1 in 8 of its records were cancels that removed an order: the serial
+    // path a cancel-heavy stream takes often makes wave 0 wait
+    uint64_t two_max = 4096;
+    bool last_cancel_heavy = false;
     uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
     DevState S{};
@@ -435,9 +437,9 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         } else if (lanes) {
             launch_match_lanes(S, e->d_S, e->d_io, buf, st);
         }
-        // two wavefronts per busy group when few groups were busy (KME_TWO_MAX, off by default), where
-        // a group's record chain, not the CU's issue rate, is the bound
-        const bool two = S.fast && e->two_max > 0 && e->last_busy <= e->two_max;
+        // two wavefronts per busy group when few groups were busy (a group's record chain, not the
+        // CU's issue rate, is then the bound) and the stream is not cancel-heavy
+        const bool two = S.fast && e->last_busy > 0 && e->last_busy <= e->two_max && !e->last_cancel_heavy;
         launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
@@ -514,6 +516,7 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_effective = last_n;
     e->last_busy = c[ci(C_BUSY)];
     e->last_light = c[ci(C_LIGHT)];
+    e->last_cancel_heavy = c[ci(C_CANCEL_OK)] * 8 > (uint64_t)last_n;
     if (host_overflow && c[ci(C_ERR)] == ~0ull) {   // the caller's trades buffer is too small for the epoch
         s.status = KME_E_CAPACITY; s.detail = KME_D_CAP_TRADES; s.n_effective = 0;
         e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_TRADES;
