@@ -2871,11 +2871,16 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
 #pragma nounroll
         for (int j = 0; j < nb; ++j) {
             if (fast) {
-                KST(const unsigned long long tf0 = stamp(); const int jf0 = j;)
+                const int jf0 = j;
+                KST(const unsigned long long tf0 = stamp();)
                 j = w.fast_segment<TWO>(B, j, nb, o_act, o_size, o_plo, o_phi, o_ntr, ftpos, ftlim);
                 KST(w.acc[ST_FAST] += stamp() - tf0; w.acc[ST_N_FAST_REC] += (unsigned long long)(j - jf0); w.acc[ST_N_FAST_SEG] += j > jf0;)
                 if (w.dead) { done = j; break; }
                 if (j >= nb) break;
+                // a segment that took records and stopped (a full event buffer, a check of the pass)
+                // leaves its next record to a new segment; the serial path takes a record only when a
+                // segment starting at it takes nothing
+                if (j > jf0) { --j; continue; }
             }
             if constexpr (TWO) {
                 // the serial path needs every node it reads final: wave 1 finishes its segment first,
