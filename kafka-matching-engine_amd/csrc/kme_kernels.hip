@@ -2303,38 +2303,35 @@ struct GroupWave {
                     if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
                     KME_PUT_EV(nev++, j, EK_TAKE, 0, OS * 128 + pb, P, rem);
                     rem = 0;
-                } else {                                       // a sweep: dry run, then commit
-                    uint64_t lo = olo, hi = ohi;
-                    int32_t r = rem, p = pb, nt = 0, zl = -1;
+                } else {                                       // a sweep, undone if it cannot be taken
+                    int32_t& ql = OS ? QC : QA;
+                    int32_t& qh = OS ? QD : QB;
+                    const int32_t sql = ql, sqh = qh, snev = nev;
+                    const uint64_t s_lo = olo, s_hi = ohi, s_cl = col, s_ch = coh;
+                    int32_t p = pb, nt = 0, zl = -1;
                     bool bad = false;
 #pragma nounroll
                     for (;;) {                                 // KP:237-253
-                        if (nt == FAST_RMAX) { bad = true; break; }
+                        if (nt == FAST_RMAX || nev + 1 > FAST_EVCAP) { bad = true; break; }
                         const int32_t qq = KME_QGET(OS, p);
-                        const int32_t x = qq < r ? qq : r;
-                        r -= x;
-                        ++nt;
-                        if (x < qq) break;                     // stops inside the level
-                        unset_bit(lo, hi, p);                  // taken whole (KP:244-252)
-                        const int32_t np = IB ? min_price_ptr(lo, hi) : max_price_ptr(lo, hi);
-                        if (np != -1 && !check_bit(lo, hi, np)) { bad = true; break; }   // H5
-                        if (r == 0) { if (np != -1 && np >= P) zl = np; break; }        // H3 zero trade
-                        if (np == -1 || !crosses(IB, r, np, P)) break;
-                        p = np;
-                    }
-                    if (bad || nev + nt + (zl >= 0) + (r > 0) > FAST_EVCAP) return false;
-#pragma nounroll
-                    for (int t = 0; t < nt; ++t) {
-                        const int32_t qq = KME_QGET(OS, pb);
                         const int32_t x = qq < rem ? qq : rem;
                         rem -= x;
-                        KME_QSET(OS, pb, qq - x);
-                        if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
-                        KME_PUT_EV(nev++, j, EK_TAKE, t, OS * 128 + pb, P, x);
-                        if (x == qq) {
-                            unset_bit(olo, ohi, pb);
-                            pb = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
-                        }
+                        KME_QSET(OS, p, qq - x);
+                        if (p < 64) col |= 1ull << p; else coh |= 1ull << (p - 64);
+                        KME_PUT_EV(nev++, j, EK_TAKE, nt, OS * 128 + p, P, x);
+                        ++nt;
+                        if (x < qq) break;                     // stops inside the level
+                        unset_bit(olo, ohi, p);                // taken whole (KP:244-252)
+                        const int32_t np = IB ? min_price_ptr(olo, ohi) : max_price_ptr(olo, ohi);
+                        if (np != -1 && !check_bit(olo, ohi, np)) { bad = true; break; }   // H5
+                        if (rem == 0) { if (np != -1 && np >= P) zl = np; break; }        // H3 zero trade
+                        if (np == -1 || !crosses(IB, rem, np, P)) break;
+                        p = np;
+                    }
+                    if (bad || nev + (zl >= 0) + (rem > 0) > FAST_EVCAP) {
+                        ql = sql; qh = sqh; nev = snev;
+                        olo = s_lo; ohi = s_hi; col = s_cl; coh = s_ch;
+                        return false;
                     }
                     if (zl >= 0) KME_PUT_EV(nev++, j, EK_ZERO, nt, OS * 128 + zl, P, 0);
                 }
