@@ -460,7 +460,9 @@ def main():
         names = ["group_in", "batch", "trade_rec", "rest_rec", "cancel_rec", "other_rec", "group_out", "kernel",
                  "n_trade_rec", "n_rest_rec", "n_cancel_rec", "maker_wait", "n_maker", "victim_wait", "n_victim",
                  "flush", "rest_alloc", "rest_level", "rest_node", "rec_pick", "rec_out", "tm_pre_norest", "rest_pre",
-                 "fast", "n_fast_rec", "n_fast_seg", "fast_pass", "fast_drain", "fast_level", "fast_epi"]
+                 "fast", "n_fast_rec", "n_fast_seg", "fast_pass", "fast_drain", "fast_level", "fast_epi",
+                 "pass_rest", "n_pass_rest", "pass_sweep", "n_pass_sweep", "pass_cancel", "n_pass_cancel",
+                 "pass_reject", "n_pass_reject", "pass_absorb", "n_pass_absorb"]
         v = dict(zip(names, d))
         per = {"share_of_kernel": {n: v[n] / v["kernel"] for n in ("group_in", "batch", "trade_rec", "rest_rec",
                                                                      "cancel_rec", "other_rec", "group_out", "flush")},
@@ -482,7 +484,9 @@ def main():
                         "drain_cycles_per_fast_rec": v["fast_drain"] / max(1, v["n_fast_rec"]),
                         "level_cycles_per_fast_rec": v["fast_level"] / max(1, v["n_fast_rec"]),
                         "epilogue_cycles_per_fast_rec": v["fast_epi"] / max(1, v["n_fast_rec"]),
-                        "records_per_segment": v["n_fast_rec"] / max(1, v["n_fast_seg"])}}
+                        "records_per_segment": v["n_fast_rec"] / max(1, v["n_fast_seg"]),
+                        "pass_by_kind": {k: {"records": v["n_pass_" + k], "cycles_per_rec": v["pass_" + k] / max(1, v["n_pass_" + k])}
+                                         for k in ("rest", "absorb", "sweep", "cancel", "reject")}}}
         per["group"] = hot if os.environ.get("KME_STAMPS_HOT") else "all"
         print(json.dumps({"stamps": per}), flush=True)
         return

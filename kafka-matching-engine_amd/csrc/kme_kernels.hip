@@ -1566,6 +1566,8 @@ enum Stamp : int {
     ST_N_TRADE_REC, ST_N_REST_REC, ST_N_CANCEL_REC, ST_MAKER_WAIT, ST_N_MAKER, ST_VICTIM_WAIT, ST_N_VICTIM, ST_FLUSH,
     ST_REST_ALLOC, ST_REST_LEVEL, ST_REST_NODE, ST_REC_PICK, ST_REC_OUT, ST_TM_PRE, ST_REST_PRE,
     ST_FAST, ST_N_FAST_REC, ST_N_FAST_SEG, ST_FAST_PASS, ST_FAST_DRAIN, ST_FAST_LEVEL, ST_FAST_EPI,
+    ST_PASS_REST, ST_N_PASS_REST, ST_PASS_SWEEP, ST_N_PASS_SWEEP, ST_PASS_CANCEL, ST_N_PASS_CANCEL,
+    ST_PASS_REJECT, ST_N_PASS_REJECT, ST_PASS_ABSORB, ST_N_PASS_ABSORB,
     ST_N = 40
 };
 
@@ -2282,6 +2284,7 @@ struct GroupWave {
         int32_t oact = 0, osize = 0, flags = 0, rslot = -1, rlev = 0;
         // A BUY (IB) or SELL of sid +g: takes from book side 1 - SIDE, rests on SIDE (KP:201, 292).
         // Returns false where the record goes to the serial path.
+        KST(int ksw = 0;)                                    // (stamps: the record swept / took from one level)
         auto take_rest = [&](auto ib_tag) -> bool {
             constexpr bool IB = decltype(ib_tag)::value;
             constexpr int SIDE = IB ? 0 : 1, OS = 1 - SIDE;
@@ -2298,12 +2301,14 @@ struct GroupWave {
             if (pb != -1 && crosses(IB, rem, pb, P)) {
                 const int32_t q = KME_QGET(OS, pb);
                 if (rem < q) {                        // the best level absorbs it (KP:237-261)
+                    KST(ksw = 2;)
                     if (nev + 1 > FAST_EVCAP) return false;
                     KME_QSET(OS, pb, q - rem);
                     if (pb < 64) col |= 1ull << pb; else coh |= 1ull << (pb - 64);
                     KME_PUT_EV(nev++, j, EK_TAKE, 0, OS * 128 + pb, P, rem);
                     rem = 0;
                 } else {                                       // a sweep, undone if it cannot be taken
+                    KST(ksw = 1;)
                     int32_t& ql = OS ? QC : QA;
                     int32_t& qh = OS ? QD : QB;
                     const int32_t sql = ql, sqh = qh, snev = nev;
@@ -2359,6 +2364,7 @@ struct GroupWave {
         // events << 8 | rest level << 16, o_phi = rest slot; the epilogue replaces the last two).
 #pragma nounroll
         for (; j < nb; ++j) {
+            KST(const unsigned long long tr0 = stamp(); ksw = 0;)
             const int32_t pj = rl32(pk, j);
             const int cls = pj & 7;
             if (cls == PC_SERIAL) break;
@@ -2418,6 +2424,15 @@ struct GroupWave {
             o_size = wl(osize, j, o_size);
             o_plo = wl(evb | ((nev - evb) << 8) | (rlev << 16), j, o_plo);
             o_phi = wl(rslot, j, o_phi);
+            KST(const unsigned long long trd = stamp() - tr0;)
+            KST(const bool k_t = cls == PC_TAKE_REST && !ksw; const bool k_s = cls == PC_TAKE_REST && ksw == 1;)
+            KST(const bool k_a = cls == PC_TAKE_REST && ksw == 2;)
+            KST(acc[ST_PASS_ABSORB] += k_a ? trd : 0; acc[ST_N_PASS_ABSORB] += k_a;)
+            KST(const bool k_r = cls == PC_REJECT; const bool k_c = cls != PC_TAKE_REST && !k_r;)
+            KST(acc[ST_PASS_REST] += k_t ? trd : 0; acc[ST_N_PASS_REST] += k_t;)
+            KST(acc[ST_PASS_SWEEP] += k_s ? trd : 0; acc[ST_N_PASS_SWEEP] += k_s;)
+            KST(acc[ST_PASS_CANCEL] += k_c ? trd : 0; acc[ST_N_PASS_CANCEL] += k_c;)
+            KST(acc[ST_PASS_REJECT] += k_r ? trd : 0; acc[ST_N_PASS_REJECT] += k_r;)
         }
         const int je = j;
         KST(acc[ST_FAST_PASS] += stamp() - tp0;)

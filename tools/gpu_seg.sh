@@ -1,4 +1,5 @@
 #!/bin/bash
-# pass variant: A/B against the previous build (diagnostic)
+# pass cycles by record kind (stamps build, diagnostic)
 set -o pipefail
-bash tools/ab_lib.sh kafka-matching-engine_amd/kme/libkme_var.so "--workload c2 --steps 5 --warmup 2 --host-path-epochs 0" "--workload c4 --steps 3 --warmup 1 --host-path-epochs 0" "--workload c3 --symbols 8192 --steps 5 --warmup 2 --host-path-epochs 0" "--workload c5 --steps 5 --warmup 2 --host-path-epochs 0"
+bash tools/gpu_stamps_env.sh st6 '' 'HOT=1 --workload c4 --steps 2 --warmup 1' '--workload c2 --steps 3 --warmup 1' '--workload c3 --symbols 8192 --steps 3 --warmup 1' > /dev/null
+rc=$?; cat gpurun_out/st6/stamps.jsonl 2>/dev/null; exit $rc
