@@ -1580,6 +1580,7 @@ struct GroupWave {
     int32_t g;
     uint32_t cur;                 // input index of the record being processed
     bool dead;
+    bool seg_retry;               // the last fast segment stopped at a record a new segment may take
     TwoLds* tl = nullptr;         // two-wavefront mode (k_match<true>): the block wave 1 reads
     int kp = 0;                   // wave 0's phase count
     bool lbusy = false;           // wave 1 has a segment to finish
@@ -2435,6 +2436,26 @@ struct GroupWave {
             KST(acc[ST_PASS_REJECT] += k_r ? trd : 0; acc[ST_N_PASS_REJECT] += k_r;)
         }
         const int je = j;
+        // where a new segment can go on: a stop at a (nearly) full event buffer, or at a prefetched
+        // cancel whose level this segment took from (two waves: only the segment wave 1 has in hand);
+        // at any other stop the record is the serial path's and a new segment's set-up would be lost
+        seg_retry = false;
+        if (je < nb) {
+            const int32_t pj = rl32(pk, je);
+            if (nev >= FAST_EVCAP - FAST_RMAX - 2) {
+                seg_retry = true;
+            } else if ((pj & 7) == PC_CANCEL_PF) {
+                const int vlev = (pj >> 24) & 0xFF, vs = vlev >> 7, vp = vlev & 127, w = vp < 64 ? 0 : 1;
+                const uint64_t own = vs ? (w ? c1m : c1l) : (w ? c0m : c0l);
+                if (!TWO) {
+                    seg_retry = (own >> (vp & 63)) & 1;
+                } else {
+                    const uint64_t bw = bstale ? U64((int64_t)tl->bcb[vs * 2 + w]) : 0;
+                    const uint64_t tw = lbusy ? U64((int64_t)tl->cb[vs * 2 + w]) : 0;
+                    seg_retry = !(((own | bw) >> (vp & 63)) & 1) && ((tw >> (vp & 63)) & 1);
+                }
+            }
+        }
         KST(acc[ST_FAST_PASS] += stamp() - tp0;)
         if (je == j0) return j0;
         set_bm(0, b0l, b0m);
@@ -2889,10 +2910,9 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
                 KST(w.acc[ST_FAST] += stamp() - tf0; w.acc[ST_N_FAST_REC] += (unsigned long long)(j - jf0); w.acc[ST_N_FAST_SEG] += j > jf0;)
                 if (w.dead) { done = j; break; }
                 if (j >= nb) break;
-                // a segment that took records and stopped (a full event buffer, a check of the pass)
-                // leaves its next record to a new segment; the serial path takes a record only when a
-                // segment starting at it takes nothing
-                if (j > jf0) { --j; continue; }
+                // a segment that took records and stopped where a new segment can go on leaves its
+                // next record to one (fast_segment's seg_retry)
+                if (j > jf0 && w.seg_retry) { --j; continue; }
             }
             if constexpr (TWO) {
                 // the serial path needs every node it reads final: wave 1 finishes its segment first,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU tests of the current build, then builds of earlier commits against it (diagnostic)
+# GPU tests of the current build, then earlier builds against it (diagnostic)
 set -o pipefail
 mkdir -p gpurun_out/ab
 K=kafka-matching-engine_amd/kme
@@ -13,7 +13,7 @@ run() {
     python3 -c "import json;d=json.load(open('gpurun_out/ab/one.json'));print('$(basename $L)', '$args', round(d['value']/1e6,1), d['phase_ms_last_epoch']['match'])"
   done
 }
-run "--workload c2 --steps 5 --warmup 2" $K/libkme_3844a19.so $K/libkme.so $K/libkme_3844a19.so $K/libkme.so
 run "--workload c5 --steps 5 --warmup 2" $K/libkme_8fef8c7.so $K/libkme_3844a19.so $K/libkme.so $K/libkme_8fef8c7.so $K/libkme_3844a19.so $K/libkme.so
-run "--workload c4 --steps 3 --warmup 1" $K/libkme_3844a19.so $K/libkme.so
+run "--workload c2 --steps 5 --warmup 2" $K/libkme_3844a19.so $K/libkme.so $K/libkme_3844a19.so $K/libkme.so
 run "--workload c3 --symbols 8192 --steps 5 --warmup 2" $K/libkme_3844a19.so $K/libkme.so $K/libkme_3844a19.so $K/libkme.so
+run "--workload c4 --steps 3 --warmup 1" $K/libkme_3844a19.so $K/libkme.so
