@@ -94,6 +94,32 @@ def make_workload(name: str, n_orders: int, rank: int, world: int, symbols: int 
     return setup, stream, sids, nacc, shards, desc
 
 
+def parse_flags(text: str) -> int:
+    """--flags exact_ledger,serial_fallback -> kme_config.flags (include/kme.h KME_FLAG_*)."""
+    names = {"exact_ledger": 1, "serial_fallback": 2}
+    flags = 0
+    for f in filter(None, (x.strip() for x in text.split(","))):
+        if f not in names:
+            raise SystemExit(f"bench.py: unknown flag {f!r} (known: {', '.join(names)})")
+        flags |= names[f]
+    if flags & 2:
+        flags |= 1   # the serial fallback runs on the exact ledger
+    return flags
+
+
+def pmc_for_build(path: str, build_id: str):
+    """(traffic, derived) of the committed PMC summary, only when it was collected on the library
+    this process loaded (its `build_id` = kme_build_id()); (None, None) otherwise, so the line never
+    carries counters of code that is not the code measured."""
+    if not os.path.exists(path):
+        return None, None, "no PMC summary committed for this configuration"
+    with open(path) as f:
+        pj = json.load(f)
+    if pj.get("build_id") != build_id:
+        return None, None, f"PMC summary of build {pj.get('build_id')}, not of the loaded build {build_id}"
+    return pj.get("hbm_bytes_per_launch"), pj.get("per_kernel_derived"), pj.get("source")
+
+
 def cpu_baseline(setup, stream, max_orders: int):
     """The oracle (CPU restatement of KProcessor.MatchingEngine, single thread) on a bounded
     prefix of the same stream.  The reference itself (Java/Kafka Streams) cannot run here."""
@@ -252,6 +278,11 @@ def parse_args(argv=None):
     ap.add_argument("--host-path-epochs", type=int, default=3,
                     help="N = 1: epochs of the host-buffer path (pinned H2D + kernels + D2H, pipelined) "
                          "measured after the device-resident ones (0 = skip)")
+    ap.add_argument("--flags", default="",
+                    help="kme_config.flags, comma-separated: exact_ledger, serial_fallback (the drop-in's own "
+                         "configuration, GpuMatchingEngine.java: exact_ledger,serial_fallback; N = 1 only)")
+    ap.add_argument("--ledger-capacity", type=int, default=0,
+                    help="with --flags exact_ledger: Balances / Positions capacity (0 = sized for the stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: print k_match cycle shares and exit")
     ap.add_argument("--lane-stamps", action="store_true", help="diagnostic: print k_match_lanes step-segment shares and exit")
@@ -300,11 +331,17 @@ def main():
     setup, stream, sids, nacc, shards, desc = make_workload(
         args.workload, total, rank, world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
     max_sid = int(sids.max())
+    flags = parse_flags(args.flags)
+    if flags and world > 1:
+        raise SystemExit("bench.py: --flags exact_ledger needs one engine (the exact ledger couples every symbol)")
 
     cfg = kme.default_config(kme.MODE_FUNDED, max_symbols=max_sid + 1, max_epoch=E,
                              max_resting=args.max_resting or min(total, (1 << 29) - 64 * (max_sid + 2) - E), max_trades=2 * E + (1 << 16),
                              max_accounts=nacc, device=local_rank, light_max=args.light_max)
     cfg.credit_shards = shards
+    cfg.flags = flags
+    if flags:   # a Positions entry per (account, symbol) filled, none ever removed by a fill (KP:283, H2)
+        cfg.ledger_capacity = args.ledger_capacity or max(1 << 20, total + nacc)
     eng = kme.Engine(cfg)
     # one explicit stream for the engine and every torch / collective op of this rank, so they are
     # ordered (the default stream's handle is 0, which would leave the engine on its own
@@ -496,14 +533,13 @@ def main():
     if rank == 0:
         avg_match_s = float(np.mean(match_ms)) / 1e3
         achieved = float(np.mean(bytes_alg)) / avg_match_s / 1e9 if avg_match_s > 0 else 0.0
-        traffic, pmc_derived = None, None
+        build_id = kme.lib().kme_build_id().decode()
+        traffic, pmc_derived, pmc_src = None, None, "PMC passes cover the default single-GPU configurations only"
         pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
-        # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round.sh)
-        if os.path.exists(pmc) and world == 1 and not args.symbols and not args.mix and E == (1 << 22):
-            with open(pmc) as f:
-                pj = json.load(f)
-            traffic = pj.get("hbm_bytes_per_launch")
-            pmc_derived = pj.get("per_kernel_derived")
+        # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round.sh),
+        # and counts only when it profiled this very build
+        if world == 1 and not args.symbols and not args.mix and E == (1 << 22) and not flags:
+            traffic, pmc_derived, pmc_src = pmc_for_build(pmc, build_id)
         out = {
             "metric": METRIC,
             "value": n_orders_all / elapsed,
@@ -518,9 +554,12 @@ def main():
             "dtype": "int64",
             "data": "synthetic",
             "config": {"workload": desc, "symbols_per_gpu_rank0": int(len(sids)), "accounts": nacc, "epoch_records": E,
-                       "stream_records_per_gpu": total, "mode": "FUNDED (symbol groups in parallel)",
+                       "stream_records_per_gpu": total,
+                       "mode": "FUNDED (symbol groups in parallel)" + (" + exact ledger" if flags & 1 else "")
+                               + (" + serial fallback" if flags & 2 else ""),
                        "parallelism": f"symbol-keyed x{world} (murmur2, Kafka's keyed partitioner)",
-                       "credit_shards": shards},
+                       "credit_shards": shards, "flags": args.flags or "none"},
+            "build_id": build_id,
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),
             "fills_per_s": 2 * n_trades_all / elapsed,
@@ -541,7 +580,8 @@ def main():
                                    "one wavefront each, concurrent)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_model": "SURVEY §8d: 52/in + 36/trade + 32/rest + 32/maker visit + 48/cancel",
-                         "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg))},
+                         "avg_launch_ms": avg_match_s * 1e3, "alg_bytes_per_launch": float(np.mean(bytes_alg)),
+                         "traffic_source": pmc_src},
             # occupancy and LDS bank conflicts of the match-phase kernels, from the committed rocprofv3
             # PMC passes of this configuration (tools/pmc_kmatch.sh, tools/pmc_summary.py)
             "pmc_match_phase": pmc_derived,

@@ -65,7 +65,9 @@ enum kme_domain {
     KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17,
     KME_D_UNPROVEN = 18      /* KME_E_UNFUNDED of the epoch as a whole: the funded proof failed, so
                                 none of its records took effect (error_index -1, n_effective 0),
-                                whatever other fault the epoch holds further on */
+                                whatever other fault the epoch holds further on -- except a fault of
+                                record 0 itself, which is reported instead (the reference throws
+                                there whatever the ledger holds; nothing takes effect either way) */
 };
 
 /* Engine modes.
@@ -264,6 +266,15 @@ const char* kme_build_id(void);
  * would.  KME_E_INVALID on a config / format mismatch, KME_E_FAILED if the engine has failed. */
 kme_status kme_checkpoint(kme_engine* e, const char* path);
 kme_status kme_restore(kme_engine* e, const char* path);
+/* The same with an application record stored beside the state in the one file: what the caller needs
+ * to resume exactly at that point -- the Java processor keeps the last input offset the state covers
+ * and the MatchOut rows of completed epochs it has not forwarded yet.  The file is
+ * written to `path`.tmp, flushed to disk and renamed over `path`, so a crash leaves the previous
+ * checkpoint whole.  kme_restore_app: *app_bytes = the record's size; when it exceeds app_cap (app
+ * may be NULL with app_cap 0) the call returns KME_E_CAPACITY and changes nothing (call again with a
+ * large enough buffer); a format-1 file restores with an empty record. */
+kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes);
+kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t app_cap, size_t* app_bytes);
 
 /* Canonical text snapshots (sorted), identical in format to the reference stores' contents:
  *   books : "B <key> <msb> <lsb>" (Books), "K <bucketPtr> <firstOid> <lastOid>" (Buckets),
@@ -306,13 +317,46 @@ kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t*
  * proves its orders against its own share of an account's cash and the funded bound only falls, so a
  * share can run dry while the others hold cash.  kme_credit_state: this engine's
  * funded bound and demand so far per account, two int64 device arrays of max_accounts
- * (dev_out[0, A) and dev_out[A, 2A)); kme_credit_adjust: the re-split of the pooled bound from every
- * shard's pair (dev_all = N such blocks, shard-major): every engine computes the same split and the
- * shares sum to the pooled bound, so the account's cash still covers all of them;
- * kme_credit_rebalance: state, all-gather over RCCL, adjust (collective: every rank calls it). */
+ * (dev_out[0, A) and dev_out[A, 2A)); an account this engine does not hold reports bound 0 and
+ * demand -1.  kme_credit_adjust: the re-split of the pooled bound from every shard's pair (dev_all =
+ * N such blocks, shard-major) over the shards that hold the account: every engine computes the same
+ * split and the shares sum to the pooled bound, so the account's cash still covers all of them.
+ * kme_credit_rebalance: state, all-gather over RCCL, adjust -- a collective every rank calls and
+ * every rank completes: a rank that cannot re-split (an epoch in flight: KME_E_INVALID, a failed
+ * engine: KME_E_FAILED) still takes part with a status word, and then no rank adjusts; that rank
+ * returns its own status, the others KME_E_INVALID. */
 kme_status kme_credit_state(kme_engine* e, int64_t* dev_out);
 kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_shards, uint32_t my_shard);
 kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c);
+
+/* ---- Multi-GPU drop-in: one MatchIn stream over N engines ----
+ * The reference's processor takes its one-partition MatchIn whole (topic.js:17-18, KP:51-52).  A
+ * kme_multi is N FUNDED engines (devices[k]; a device may repeat) behind the host-epoch calls of one
+ * engine: each epoch is split by symbol (kme_router_split: Kafka's keyed partitioner over |sid|,
+ * cancels to their order's partition, account records to every engine with 1/N of the credit), the
+ * parts run as host epochs on their engines concurrently, and kme_multi_wait merges the results
+ * into input order -- the caller's kme_epoch_result is exactly one engine's over the whole stream.
+ * Before every epoch the engines' funded credit is pooled and split again (kme_credit_state /
+ * kme_credit_adjust), queued on the engine streams behind the epochs in flight (env
+ * KME_MULTI_REBALANCE_EVERY = epochs between re-splits, 0 = never).  cfg: FUNDED, flags 0 (the exact
+ * ledger couples every symbol: one engine), credit_shards is set to N.  The trades of one merged
+ * epoch must fit max_trades.  Any fault of a shard fails the whole (the other shards went past it):
+ * the records before the first fault in input order are answered (n_effective), as one engine
+ * answers them, then it accepts nothing further. */
+typedef struct kme_multi kme_multi;
+kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* devices, kme_multi** out);
+kme_status kme_multi_destroy(kme_multi* m);
+/* as kme_submit_epoch_host / kme_poll / kme_wait (two epochs in flight; out->trades_cap >= max_trades) */
+kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in_host, uint32_t n, const kme_epoch_result* out_host);
+kme_status kme_multi_poll(kme_multi* m, int* done);
+kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st);
+/* as kme_checkpoint_app / kme_restore_app: every engine to `path`.g<generation>.<k>, then a manifest at
+ * `path` (written and renamed last: the commit of the set); a restore also rebuilds the router's
+ * oid directory from the engines' resting orders */
+kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* app, size_t app_bytes);
+kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size_t app_cap, size_t* app_bytes);
+/* engine k (snapshots, diagnostics) */
+kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out);
 
 /* Wall-clock (HIP event) duration in ms of each kernel phase of the last epoch; index by name
  * (kme_phase_names).  Used by bench.py for the roofline of the dominant kernel. */

@@ -1,7 +1,8 @@
 // GpuMatchingEngine -- the MI355X matching engine behind the reference's Processor interface, the
-// one-line swap at the topology (KProcessor.java:52):
+// swap at the topology (KProcessor.java:52-57):
 //
 //     .addProcessor("MatchingEngine", GpuMatchingEngine::new, "Source")
+//     .addStateStore(GpuMatchingEngine.commitHook(), "MatchingEngine")
 //
 // Like the reference's MatchingEngine (KP:63) it is a Processor<String, Order> over the reference's
 // own top-level Order class (KP:449-475), in the same (default) package; it uses only Order's public
@@ -11,27 +12,43 @@
 // Contract kept from MatchingEngine.process (KP:96-126): for every input record the processor
 // forwards ("IN", order), then the maker and the taker fill of each trade (keyed "OUT", KP:272-273),
 // then ("OUT", order) -- same order, same field values.  The difference is timing: records are
-// buffered into an epoch and forwarded when the epoch completes; the offset commit is requested after
-// the epoch's records are forwarded, never before.
+// buffered into an epoch and forwarded when the epoch completes.
 //
-// Path at rate (include/kme.h, "Host epochs at device rate"): two slots of JVM direct ByteBuffers
-// hold an epoch's Order columns (native byte order) and the MatchOut rows that come back; the native
-// side registers them once, so an epoch crosses PCIe straight from and to them.  While the GPU runs
-// epoch k, process() fills the other slot; the wall-clock punctuator polls (never blocks) and
-// forwards a finished epoch, and sends a partly filled one so that latency stays bounded.
+// Path at rate (include/kme.h, "Host epochs at device rate"): two slots of direct ByteBuffers over
+// native, registered memory (kme_jni.c allocates them) hold an epoch's Order columns (native byte
+// order) and the MatchOut rows that come back, so an epoch crosses PCIe straight from and to them.
+// While the GPU runs epoch k, process() fills the other slot; the wall-clock punctuator polls (never
+// blocks) and forwards a finished epoch, and sends a partly filled one so that latency stays bounded.
 //
-// Faults: the records before a fault took effect and are forwarded and committed (as the reference's
-// per-record commit would have, KP:97, 124-125); then the processor fails like the reference's
-// stream thread.  The default flags (EXACT_LEDGER | SERIAL_FALLBACK) give the reference's result for
-// any stream, so KME_E_UNFUNDED cannot occur; in a configuration without SERIAL_FALLBACK it is fatal
-// here too (its records were not processed, and a processor cannot hand records back to Kafka).
+// Commit and restart (INTEGRATION.md §3; the reference keeps its state in changelogged stores,
+// KP:30-49, runs at least once, KP:29, and commits after every record, KP:125).  Kafka Streams
+// commits the consumed offset of every record process() has returned from, and flushes the task's
+// state stores first.  The commit hook is such a store: its flush() is this processor's commit
+// point -- the partly filled epoch is submitted, every epoch in flight is completed (its rows kept,
+// forwarded at the next process() or punctuation: forwarding is not possible inside a store flush),
+// and one file written atomically holds the device state after the last record taken (its Kafka
+// offset) and the rows not yet forwarded.  init() restores that file, forwards those rows first, and
+// skips re-delivered records at or below the offset.  A record whose offset Kafka committed is
+// therefore either forwarded or in the checkpoint; output forwarded after a checkpoint may be
+// forwarded again after a crash (at least once, as the reference).
+//
+// Faults: the records before a fault took effect and are forwarded (as the reference's per-record
+// commit would have, KP:97, 124-125); then the processor fails like the reference's stream thread.
+// The default flags (EXACT_LEDGER | SERIAL_FALLBACK) give the reference's result for any stream, so
+// KME_E_UNFUNDED cannot occur; in a configuration without SERIAL_FALLBACK it is fatal here too (its
+// records were not processed, and a processor cannot hand records back to Kafka).
+import java.io.File;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.time.Duration;
+import java.util.Collections;
+import java.util.Map;
 
 import org.apache.kafka.streams.processor.Processor;
 import org.apache.kafka.streams.processor.ProcessorContext;
 import org.apache.kafka.streams.processor.PunctuationType;
+import org.apache.kafka.streams.processor.StateStore;
+import org.apache.kafka.streams.state.StoreBuilder;
 
 public final class GpuMatchingEngine implements Processor<String, Order> {
     static { System.loadLibrary("kme_jni"); }
@@ -41,42 +58,53 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     static final int KME_FLAG_EXACT_LEDGER = 1, KME_FLAG_SERIAL_FALLBACK = 2;
     static final int KME_OK = 0;
     static final int ROW_BYTES = 48;    // kme_row: oid, aid, sid, prev (long); action, price, size (int); kind, has_prev
+    public static final String COMMIT_STORE = "MatchingEngineCommit";
 
     private static native long create(int mode, int maxSymbols, int maxEpoch, long maxResting, int maxTrades,
-                                      int maxAccounts, int flags, int device);
+                                      int maxAccounts, int flags, int device, int nDevices, long ledgerCapacity);
     private static native void destroy(long h);
-    private static native int bind(long h, int slot, ByteBuffer action, ByteBuffer oid, ByteBuffer aid, ByteBuffer sid,
-                                   ByteBuffer price, ByteBuffer size, ByteBuffer rows);
+    private static native ByteBuffer buffer(long h, int slot, int column);
     private static native int submit(long h, int slot, int n);
     private static native int poll(long h);
     private static native int complete(long h, int slot, long[] status);
+    private static native void forwarded(long h, int slot);
     private static native String statusText(int status);
-    static native int checkpoint(long h, String path);
-    static native int restore(long h, String path);
+    static native int checkpoint(long h, String path, long offset);
+    static native int restore(long h, String path, long[] out);
 
     private final int epoch;
     private final int maxTrades;
-    private final int mode, flags, maxSymbols, maxAccounts, device;
-    private final long maxResting;
+    private final int mode, flags, maxSymbols, maxAccounts, device, nDevices;
+    private final long maxResting, ledgerCapacity;
     private ProcessorContext context;
     private long h;
+    private File checkpointFile;
     // per slot: the six Order columns (KP:451-456) and the MatchOut rows
     private final ByteBuffer[] action = new ByteBuffer[2], oid = new ByteBuffer[2], aid = new ByteBuffer[2],
             sid = new ByteBuffer[2], price = new ByteBuffer[2], size = new ByteBuffer[2], rows = new ByteBuffer[2];
     private final int[] count = new int[2];          // records buffered in the slot
-    private final boolean[] busy = new boolean[2];   // the slot's epoch is in flight
+    private final boolean[] busy = new boolean[2];   // in flight, or its rows not forwarded yet
     private int fill = 0;                            // the slot process() writes into
     private int oldest = 0;                          // the slot of the oldest epoch in flight
     private int inflight = 0;
-    private final long[] status = new long[4];
+    private final int[] ready = new int[2];          // completed slots whose rows wait to be forwarded, oldest first
+    private int nReady = 0;
+    private final int[] readyRows = new int[2];
+    private final long[][] readyStatus = new long[2][4];
+    private long lastOffset = -1;                    // Kafka offset of the last record taken into an epoch
+    private long skipThrough = -1;                   // re-delivered records at or below it are in the checkpoint
+    private long checkpointed = -1;                  // the offset the checkpoint on disk covers
 
     public GpuMatchingEngine() {
-        this(1 << 16, 1 << 18, KME_MODE_FUNDED, KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK, 1 << 16, 1 << 20,
-             1L << 26, 0);
+        // 65,537 symbol groups: sids up to 65,536 (BASELINE C3's universe is 1..65,536)
+        this(1 << 16, 1 << 18, KME_MODE_FUNDED, KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK, 65537, 1 << 20,
+             1L << 26, 0, 1, 1L << 24);
     }
 
+    // nDevices > 1: the symbols keyed over GPUs device .. device + nDevices - 1 behind this one processor
+    // (kme_multi: FUNDED, flags 0 -- the exact ledger couples every symbol, so it stays on one GPU)
     public GpuMatchingEngine(int epoch, int maxTrades, int mode, int flags, int maxSymbols, int maxAccounts,
-                             long maxResting, int device) {
+                             long maxResting, int device, int nDevices, long ledgerCapacity) {
         this.epoch = epoch;
         this.maxTrades = maxTrades;
         this.mode = mode;
@@ -85,36 +113,52 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         this.maxAccounts = maxAccounts;
         this.maxResting = maxResting;
         this.device = device;
-        for (int s = 0; s < 2; s++) {
-            action[s] = direct(4L * epoch);
-            oid[s] = direct(8L * epoch);
-            aid[s] = direct(8L * epoch);
-            sid[s] = direct(8L * epoch);
-            price[s] = direct(4L * epoch);
-            size[s] = direct(4L * epoch);
-            rows[s] = direct((long) ROW_BYTES * (2L * epoch + 2L * maxTrades));
-        }
-    }
-
-    private static ByteBuffer direct(long bytes) {
-        if (bytes > Integer.MAX_VALUE) throw new IllegalArgumentException("kme: buffer over 2 GiB");
-        return ByteBuffer.allocateDirect((int) bytes).order(ByteOrder.nativeOrder());
+        this.nDevices = nDevices;
+        this.ledgerCapacity = ledgerCapacity;
     }
 
     @Override
     public void init(ProcessorContext context) {                         // KP:86-93
         this.context = context;
-        this.h = create(mode, maxSymbols, epoch, maxResting, maxTrades, maxAccounts, flags, device);
+        this.h = create(mode, maxSymbols, epoch, maxResting, maxTrades, maxAccounts, flags, device, nDevices,
+                        ledgerCapacity);
         for (int s = 0; s < 2; s++) {
-            final int rc = bind(h, s, action[s], oid[s], aid[s], sid[s], price[s], size[s], rows[s]);
-            if (rc != KME_OK) throw new IllegalStateException("kme bind: " + statusText(rc));
+            action[s] = buffer(h, s, 0).order(ByteOrder.nativeOrder());
+            oid[s] = buffer(h, s, 1).order(ByteOrder.nativeOrder());
+            aid[s] = buffer(h, s, 2).order(ByteOrder.nativeOrder());
+            sid[s] = buffer(h, s, 3).order(ByteOrder.nativeOrder());
+            price[s] = buffer(h, s, 4).order(ByteOrder.nativeOrder());
+            size[s] = buffer(h, s, 5).order(ByteOrder.nativeOrder());
+            rows[s] = buffer(h, s, 6).order(ByteOrder.nativeOrder());
+        }
+        final StateStore hook = context.getStateStore(COMMIT_STORE);
+        if (hook instanceof CommitHook) ((CommitHook) hook).owner = this;
+        checkpointFile = new File(context.stateDir(), "kme-" + context.taskId() + ".ckpt");
+        if (checkpointFile.exists()) {                                  // the state of the last commit
+            final long[] r = new long[6];
+            final int rc = restore(h, checkpointFile.getPath(), r);
+            if (rc != KME_OK) throw new IllegalStateException("kme restore: " + statusText(rc));
+            skipThrough = checkpointed = lastOffset = r[0];
+            for (int k = 0; k < (int) r[1]; k++) {                      // rows not forwarded before the crash
+                final int s = (int) r[2 + 2 * k];
+                readyRows[s] = (int) r[3 + 2 * k];
+                readyStatus[s][0] = KME_OK;
+                busy[s] = true;
+                ready[nReady++] = s;
+            }
         }
         context.schedule(Duration.ofMillis(1), PunctuationType.WALL_CLOCK_TIME, ts -> punctuate());
     }
 
     @Override
     public void process(String key, Order o) {                          // KP:96
-        while (busy[fill]) completeOldest();                            // both slots in flight
+        forwardReady();
+        final long offset = context.offset();
+        if (offset <= skipThrough) return;                              // taken before the restored checkpoint
+        while (busy[fill]) {                                            // both slots busy
+            if (nReady > 0) forwardReady();
+            else completeOldest(true);
+        }
         final int n = count[fill];
         action[fill].putInt(4 * n, o.action);
         oid[fill].putLong(8 * n, o.oid);
@@ -123,13 +167,14 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         price[fill].putInt(4 * n, o.price);
         size[fill].putInt(4 * n, o.size);
         count[fill] = n + 1;
+        lastOffset = offset;
         if (count[fill] == epoch) flush();
     }
 
     // Sends the slot being filled as one epoch (asynchronous: returns once it is queued).
     private void flush() {
         if (count[fill] == 0) return;
-        while (inflight == 2) completeOldest();
+        while (inflight == 2) completeOldest(true);
         final int rc = submit(h, fill, count[fill]);
         if (rc != KME_OK) throw new IllegalStateException("kme submit: " + statusText(rc));
         if (inflight == 0) oldest = fill;
@@ -138,57 +183,134 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         fill ^= 1;
     }
 
-    // Waits for the oldest epoch in flight, forwards its MatchOut rows in the reference's order and
-    // commits them.
-    private void completeOldest() {
+    // Waits for the oldest epoch in flight; its rows become ready, and are forwarded now unless the
+    // caller is the commit point.
+    private void completeOldest(boolean forward) {
         final int s = oldest;
-        final int n = complete(h, s, status);
-        final ByteBuffer r = rows[s];
-        for (int k = 0; k < n; k++) {
-            final int b = ROW_BYTES * k;
-            final Order o = new Order(r.getInt(b + 32), r.getLong(b), r.getLong(b + 8), r.getLong(b + 16),
-                                      r.getInt(b + 36), r.getInt(b + 40));
-            final int kind = r.get(b + 44);
-            if (kind == 2 && r.get(b + 45) != 0) o.prev = r.getLong(b + 24);     // OUT echo of an append (KP:217)
-            context.forward(kind == 0 ? "IN" : "OUT", o);
-        }
-        busy[s] = false;
-        count[s] = 0;
+        readyRows[s] = complete(h, s, readyStatus[s]);
+        ready[nReady++] = s;
         inflight--;
         oldest = s ^ 1;
-        context.commit();                                               // KP:125, once per epoch
-        if (status[0] != KME_OK) throw new IllegalStateException(statusText((int) status[0]));   // the stream thread dies
+        if (forward) forwardReady();
+    }
+
+    // Forwards the ready rows, oldest epoch first, in the reference's order (IN, fills, OUT per record).
+    private void forwardReady() {
+        while (nReady > 0) {
+            final int s = ready[0];
+            final ByteBuffer r = rows[s];
+            for (int k = 0; k < readyRows[s]; k++) {
+                final int b = ROW_BYTES * k;
+                final Order o = new Order(r.getInt(b + 32), r.getLong(b), r.getLong(b + 8), r.getLong(b + 16),
+                                          r.getInt(b + 36), r.getInt(b + 40));
+                final int kind = r.get(b + 44);
+                if (kind == 2 && r.get(b + 45) != 0) o.prev = r.getLong(b + 24);     // OUT echo of an append (KP:217)
+                context.forward(kind == 0 ? "IN" : "OUT", o);
+            }
+            forwarded(h, s);
+            ready[0] = ready[1];
+            nReady--;
+            busy[s] = false;
+            count[s] = 0;
+            if (readyStatus[s][0] != KME_OK)                            // the stream thread dies
+                throw new IllegalStateException(statusText((int) readyStatus[s][0]));
+        }
     }
 
     // Wall-clock punctuation: forward every epoch the GPU has finished, without blocking, and send
     // a partly filled epoch when a slot is free.
     private void punctuate() {
+        forwardReady();
         while (inflight > 0) {
             final int p = poll(h);
             if (p < 0) throw new IllegalStateException("kme poll: " + statusText(-p));
             if (p == 0) break;
-            completeOldest();
+            completeOldest(true);
         }
-        if (inflight < 2 && count[fill] > 0) flush();
+        if (inflight < 2 && count[fill] > 0 && !busy[fill]) flush();
     }
 
-    // Persistence in place of the RocksDB changelogs (KP:30-49): every epoch received so far is
-    // completed first.
-    public void checkpoint(String path) {
+    // The commit point: the commit hook's flush(), before Kafka Streams commits the offsets of every
+    // record process() took.  Nothing is forwarded here; the checkpoint keeps what is not forwarded.
+    void commitPoint() {
+        if (h == 0 || lastOffset == checkpointed) return;               // nothing taken since the last one
         flush();
-        while (inflight > 0) completeOldest();
-        final int rc = checkpoint(h, path);
+        while (inflight > 0) completeOldest(false);
+        for (int k = 0; k < nReady; k++)                                // a faulted epoch is not a commit point
+            if (readyStatus[ready[k]][0] != KME_OK) throw new IllegalStateException(statusText((int) readyStatus[ready[k]][0]));
+        final int rc = checkpoint(h, checkpointFile.getPath(), lastOffset);
         if (rc != KME_OK) throw new IllegalStateException("kme checkpoint: " + statusText(rc));
+        checkpointed = lastOffset;
     }
 
     @Override
     public void close() {                                               // KP:129
         try {
+            forwardReady();
             flush();
-            while (inflight > 0) completeOldest();
+            while (inflight > 0) completeOldest(true);
+            commitPoint();                                              // everything forwarded: the final state
         } finally {
             destroy(h);
             h = 0;
         }
+    }
+
+    // ---- the commit hook: a state store whose flush() is the processor's commit point
+    public static StoreBuilder<CommitHook> commitHook() {
+        return new CommitHookBuilder(COMMIT_STORE);
+    }
+
+    public static final class CommitHook implements StateStore {
+        private final String name;
+        private GpuMatchingEngine owner;
+        private boolean open;
+
+        CommitHook(String name) { this.name = name; }
+
+        @Override
+        public String name() { return name; }
+
+        @Override
+        public void init(ProcessorContext context, StateStore root) {
+            context.register(root, (key, value) -> { });              // the checkpoint file is the state
+            open = true;
+        }
+
+        @Override
+        public void flush() {                                          // before the offsets are committed
+            if (owner != null) owner.commitPoint();
+        }
+
+        @Override
+        public void close() { open = false; }
+
+        @Override
+        public boolean persistent() { return true; }
+
+        @Override
+        public boolean isOpen() { return open; }
+    }
+
+    static final class CommitHookBuilder implements StoreBuilder<CommitHook> {
+        private final String name;
+
+        CommitHookBuilder(String name) { this.name = name; }
+
+        public StoreBuilder<CommitHook> withCachingEnabled() { return this; }
+
+        public StoreBuilder<CommitHook> withCachingDisabled() { return this; }
+
+        public StoreBuilder<CommitHook> withLoggingEnabled(Map<String, String> config) { return this; }
+
+        public StoreBuilder<CommitHook> withLoggingDisabled() { return this; }
+
+        public CommitHook build() { return new CommitHook(name); }
+
+        public Map<String, String> logConfig() { return Collections.emptyMap(); }
+
+        public boolean loggingEnabled() { return false; }
+
+        public String name() { return name; }
     }
 }

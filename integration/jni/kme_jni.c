@@ -1,19 +1,29 @@
 /* kme_jni.c -- JNI glue for GpuMatchingEngine.java, the processor that replaces the reference's
  * MatchingEngine at its topology (KProcessor.java:52, `.addProcessor("MatchingEngine", ...)`).
  *
- * The product path at rate (include/kme.h, "Host epochs at device rate"): the Java side owns two
- * slots of JVM direct ByteBuffers -- the six Order columns of an epoch (structure of arrays, native
- * byte order) and the MatchOut rows that come back -- and this file registers them with the engine
- * once (kme_host_register), so an epoch crosses PCIe straight from and to them: no array pinning, no
- * copies through the JNI boundary, and the garbage collector is never blocked on the GPU.
+ * The product path at rate (include/kme.h, "Host epochs at device rate"): this file allocates two
+ * slots of page-aligned host memory -- the six Order columns of an epoch (structure of arrays, native
+ * byte order) and the MatchOut rows that come back -- registers them with the engine once, and hands
+ * them to Java as direct ByteBuffers (NewDirectByteBuffer), so an epoch crosses PCIe straight from and
+ * to the buffers Java reads and writes: no array pinning, no copies through the JNI boundary, no two
+ * registrations sharing a page, and the garbage collector is never blocked on the GPU.
  *
- *   bind(h, slot, action, oid, aid, sid, price, size, rows)   the slot's buffers (checked, registered)
+ *   create(...)               the engine (or nDevices symbol-shard engines, kme_multi), its slots and
+ *                             their result buffers
+ *   buffer(h, slot, column)   the slot's column 0..5 (action, oid, aid, sid, price, size) or 6 (rows)
  *   submit(h, slot, n)        kme_submit_epoch_host: H2D, kernels, D2H queued; returns at once
  *   poll(h)                   kme_poll: 1 when the oldest epoch in flight is done (punctuator)
  *   complete(h, slot, st)     kme_wait + kme_expand_rows_mt into the slot's row buffer, in the
  *                             reference's order: IN (KP:97), maker / taker fill per trade
  *                             (executeTrade, KP:265-274), OUT (KP:124); st[0..3] = status, domain
- *                             detail, error index, records that took effect (kme_epoch_status)
+ *                             detail, error index, records that took effect (kme_epoch_status).  The
+ *                             rows stay "ready" (not yet forwarded) until forwarded(h, slot).
+ *   forwarded(h, slot)        Java has forwarded the slot's rows
+ *   checkpoint(h, path, off)  the commit point: kme_checkpoint_app of the engine
+ *                             state with an application record = the last input offset the state
+ *                             covers and the rows of every ready slot, oldest first
+ *   restore(h, path, out)     kme_restore_app: the state, the offset (out[0]) and the ready rows back
+ *                             in their slots (out[1] = how many, then (slot, rows) pairs, oldest first)
  *
  * On an error the rows of the records that took effect ([0, n_effective)) are still produced: the
  * reference forwards and commits every record before the one that throws (KP:97, 124-125).
@@ -24,25 +34,38 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "kme.h"
 
+#define NCOL 7                     /* six Order columns + the row buffer */
+
 typedef struct jslot {
-    kme_orders in;                 /* the slot's direct ByteBuffers (Java writes the records) */
-    kme_row* rows;                 /* direct ByteBuffer of MatchOut rows (Java reads them) */
+    void* col[NCOL];               /* page-aligned, registered; Java sees them as direct ByteBuffers */
+    size_t bytes[NCOL];
+    kme_orders in;
+    kme_row* rows;
     size_t rows_cap;
-    void* regs[7];                 /* what bind() registered */
-    kme_epoch_result res;          /* native host results, registered at create() */
+    kme_epoch_result res;          /* native host results, registered */
     uint32_t n;                    /* records of the epoch in flight (0 = none) */
+    int64_t ready_rows;            /* rows completed and not yet forwarded (-1 = none) */
+    uint64_t ready_seq;            /* completion order of the ready rows */
 } jslot;
 
 typedef struct jkme {
-    kme_engine* e;
+    kme_engine* e;                 /* one engine, or */
+    kme_multi* m;                  /* nDevices > 1: symbol shards on devices device .. device + nDevices - 1 */
     uint32_t max_epoch, max_trades;
+    uint64_t completions;
     jslot slot[2];
 } jkme;
+
+/* the application record of a checkpoint (kme_checkpoint_app) */
+#define JREC_MAGIC 0x4a454d4bu   /* "KMEJ" */
+typedef struct jrec_head { uint32_t magic, n_ready; int64_t offset; } jrec_head;
+typedef struct jrec_slot { uint32_t slot, _pad; uint64_t rows; } jrec_slot;
 
 static void throw_state(JNIEnv* env, const char* msg) {
     jclass c = (*env)->FindClass(env, "java/lang/IllegalStateException");
@@ -51,33 +74,71 @@ static void throw_state(JNIEnv* env, const char* msg) {
 
 static void* aligned(size_t bytes) {
     void* p = NULL;
-    return posix_memalign(&p, 4096, bytes ? bytes : 1) == 0 ? p : NULL;
+    if (posix_memalign(&p, 4096, bytes ? (bytes + 4095) & ~(size_t)4095 : 4096) != 0) return NULL;
+    memset(p, 0, bytes ? bytes : 1);
+    return p;
+}
+
+/* the single-engine and the multi-engine calls behind one handle */
+static kme_status h_submit(jkme* h, const kme_orders* in, uint32_t n, const kme_epoch_result* r) {
+    return h->m ? kme_multi_submit_epoch_host(h->m, in, n, r) : kme_submit_epoch_host(h->e, in, n, r);
+}
+static kme_status h_poll(jkme* h, int* done) { return h->m ? kme_multi_poll(h->m, done) : kme_poll(h->e, done); }
+static kme_status h_wait(jkme* h, kme_epoch_status* st) { return h->m ? kme_multi_wait(h->m, st) : kme_wait(h->e, st); }
+static kme_status h_checkpoint(jkme* h, const char* p, const void* app, size_t bytes) {
+    return h->m ? kme_multi_checkpoint_app(h->m, p, app, bytes) : kme_checkpoint_app(h->e, p, app, bytes);
+}
+static kme_status h_restore(jkme* h, const char* p, void* app, size_t cap, size_t* bytes) {
+    return h->m ? kme_multi_restore_app(h->m, p, app, cap, bytes) : kme_restore_app(h->e, p, app, cap, bytes);
 }
 
 static void free_handle(jkme* h) {
     if (!h) return;
+    if (h->e || h->m) {   /* epochs still in flight (a processor torn down mid-stream): their copies land first */
+        kme_epoch_status st;
+        for (int k = 0; k < 2; ++k)
+            if (h->slot[k].n) {
+                (void)h_wait(h, &st);
+                h->slot[k].n = 0;
+            }
+    }
     for (int s = 0; s < 2; ++s) {
         jslot* sl = &h->slot[s];
-        for (int k = 0; k < 7; ++k)
-            if (sl->regs[k] && h->e) kme_host_unregister(h->e, sl->regs[k]);
         void* res[6] = {sl->res.out_action, sl->res.out_size, sl->res.out_prev, sl->res.out_flags, sl->res.trade_off,
                         sl->res.trades};
+        for (int k = 0; k < NCOL; ++k) {
+            if (sl->col[k] && h->e) kme_host_unregister(h->e, sl->col[k]);
+            free(sl->col[k]);
+        }
         for (int k = 0; k < 6; ++k) {
             if (res[k] && h->e) kme_host_unregister(h->e, res[k]);
             free(res[k]);
         }
     }
     if (h->e) kme_destroy(h->e);
+    if (h->m) kme_multi_destroy(h->m);
     free(h);
 }
 
+/* page-aligned host memory; registered with the engine (one engine: the epochs' PCIe copies go
+   straight from and to it).  A kme_multi reads and writes the slots on the host (split, merge). */
+static int alloc_registered(jkme* h, void** p, size_t bytes) {
+    *p = aligned(bytes);
+    return *p && (!h->e || kme_host_register(h->e, *p, bytes) == KME_OK);
+}
+
 /* static native long create(int mode, int maxSymbols, int maxEpoch, long maxResting, int maxTrades,
- *                           int maxAccounts, int flags, int device) */
+ *                           int maxAccounts, int flags, int device, int nDevices, long ledgerCapacity)
+ * nDevices > 1: symbol shards on devices device .. device + nDevices - 1 (kme_multi: FUNDED, flags 0);
+ * nDevices < 0: -nDevices shards all on `device` (tests on a one-GPU box). */
 JNIEXPORT jlong JNICALL Java_GpuMatchingEngine_create(JNIEnv* env, jclass cls, jint mode, jint maxSymbols,
                                                         jint maxEpoch, jlong maxResting, jint maxTrades,
-                                                        jint maxAccounts, jint flags, jint device) {
+                                                        jint maxAccounts, jint flags, jint device, jint nDevices,
+                                                        jlong ledgerCapacity) {
     (void)cls;
     if (maxEpoch <= 0 || maxTrades <= 0) { throw_state(env, "kme: maxEpoch and maxTrades must be positive"); return 0; }
+    if (nDevices == 0 || nDevices > 1024 || nDevices < -1024) { throw_state(env, "kme: nDevices out of range"); return 0; }
+    if (ledgerCapacity < 0) { throw_state(env, "kme: ledgerCapacity must not be negative"); return 0; }
     kme_config cfg;
     memset(&cfg, 0, sizeof cfg);
     cfg.abi_version = KME_ABI_VERSION;
@@ -87,7 +148,9 @@ JNIEXPORT jlong JNICALL Java_GpuMatchingEngine_create(JNIEnv* env, jclass cls, j
     cfg.max_epoch = (uint32_t)maxEpoch;
     cfg.max_trades = (uint32_t)maxTrades;
     cfg.max_resting = (uint64_t)maxResting;
-    cfg.ledger_capacity = 1u << 20;
+    /* EXACT Balances / Positions (EXACT mode, or FUNDED with the exact ledger): a Positions entry per
+       (account, symbol) ever filled -- fillOrder never removes the entry it reads (KP:283, H2) */
+    cfg.ledger_capacity = (uint64_t)ledgerCapacity;
     cfg.device = device;
     cfg.flags = (uint32_t)flags;   /* KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK: the reference's
                                       semantics for any stream, parallel where the funded proof holds */
@@ -95,32 +158,51 @@ JNIEXPORT jlong JNICALL Java_GpuMatchingEngine_create(JNIEnv* env, jclass cls, j
     if (!h) { throw_state(env, "kme: out of host memory"); return 0; }
     h->max_epoch = (uint32_t)maxEpoch;
     h->max_trades = (uint32_t)maxTrades;
-    const kme_status s = kme_create(&cfg, &h->e);
+    kme_status s;
+    if (nDevices == 1) {
+        s = kme_create(&cfg, &h->e);
+    } else {
+        const int nd = nDevices > 0 ? nDevices : -nDevices;
+        int32_t devs[1024];
+        for (int k = 0; k < nd; ++k) devs[k] = nDevices > 0 ? device + k : device;
+        s = kme_multi_create(&cfg, (uint32_t)nd, devs, &h->m);
+    }
     if (s != KME_OK) {
         h->e = NULL;
+        h->m = NULL;
         free_handle(h);
         throw_state(env, kme_strerror(s));
         return 0;
     }
-    const size_t E = (size_t)maxEpoch;
+    const size_t E = (size_t)maxEpoch, T = (size_t)maxTrades;
     for (int k = 0; k < 2; ++k) {
-        kme_epoch_result* r = &h->slot[k].res;
-        r->out_action = (int32_t*)aligned(sizeof(int32_t) * E);
-        r->out_size = (int32_t*)aligned(sizeof(int32_t) * E);
-        r->out_prev = (int64_t*)aligned(sizeof(int64_t) * E);
-        r->out_flags = (uint8_t*)aligned(E);
-        r->trade_off = (uint32_t*)aligned(sizeof(uint32_t) * (E + 1));
-        r->trades = (kme_trade*)aligned(sizeof(kme_trade) * (size_t)maxTrades);
-        r->trades_cap = (uint32_t)maxTrades;
-        const size_t bytes[6] = {4 * E, 4 * E, 8 * E, E, 4 * (E + 1), sizeof(kme_trade) * (size_t)maxTrades};
-        void* p[6] = {r->out_action, r->out_size, r->out_prev, r->out_flags, r->trade_off, r->trades};
-        for (int q = 0; q < 6; ++q) {
-            if (!p[q] || kme_host_register(h->e, p[q], bytes[q]) != KME_OK) {
-                free_handle(h);
-                throw_state(env, "kme: cannot allocate or register the result buffers");
-                return 0;
-            }
+        jslot* sl = &h->slot[k];
+        const size_t cb[NCOL] = {4 * E, 8 * E, 8 * E, 8 * E, 4 * E, 4 * E, sizeof(kme_row) * (2 * E + 2 * T)};
+        int ok = 1;
+        for (int c = 0; c < NCOL && ok; ++c) {
+            sl->bytes[c] = cb[c];
+            ok = alloc_registered(h, &sl->col[c], cb[c]);
         }
+        kme_epoch_result* r = &sl->res;
+        ok = ok && alloc_registered(h, (void**)&r->out_action, 4 * E) && alloc_registered(h, (void**)&r->out_size, 4 * E) &&
+             alloc_registered(h, (void**)&r->out_prev, 8 * E) && alloc_registered(h, (void**)&r->out_flags, E) &&
+             alloc_registered(h, (void**)&r->trade_off, 4 * (E + 1)) &&
+             alloc_registered(h, (void**)&r->trades, sizeof(kme_trade) * T);
+        if (!ok) {
+            free_handle(h);
+            throw_state(env, "kme: cannot allocate or register the slot buffers");
+            return 0;
+        }
+        r->trades_cap = (uint32_t)maxTrades;
+        sl->in.action = (const int32_t*)sl->col[0];
+        sl->in.oid = (const int64_t*)sl->col[1];
+        sl->in.aid = (const int64_t*)sl->col[2];
+        sl->in.sid = (const int64_t*)sl->col[3];
+        sl->in.price = (const int32_t*)sl->col[4];
+        sl->in.size = (const int32_t*)sl->col[5];
+        sl->rows = (kme_row*)sl->col[6];
+        sl->rows_cap = cb[6] / sizeof(kme_row);
+        sl->ready_rows = -1;
     }
     return (jlong)(intptr_t)h;
 }
@@ -131,43 +213,14 @@ JNIEXPORT void JNICALL Java_GpuMatchingEngine_destroy(JNIEnv* env, jclass cls, j
     free_handle((jkme*)(intptr_t)handle);
 }
 
-/* static native int bind(long h, int slot, ByteBuffer action, ByteBuffer oid, ByteBuffer aid,
- *                        ByteBuffer sid, ByteBuffer price, ByteBuffer size, ByteBuffer rows)
- * Direct buffers of at least maxEpoch elements each (int / long columns) and rows for
- * 2 maxEpoch + 2 maxTrades MatchOut rows of 48 bytes; returns a kme_status. */
-JNIEXPORT jint JNICALL Java_GpuMatchingEngine_bind(JNIEnv* env, jclass cls, jlong handle, jint slot, jobject action,
-                                                     jobject oid, jobject aid, jobject sid, jobject price, jobject size,
-                                                     jobject rows) {
+/* static native ByteBuffer buffer(long h, int slot, int column): the slot's column 0..5 (action, oid,
+ * aid, sid, price, size: maxEpoch elements each) or 6 (the MatchOut rows: 2 maxEpoch + 2 maxTrades of
+ * 48 bytes), as a direct ByteBuffer over the registered native memory (valid until destroy). */
+JNIEXPORT jobject JNICALL Java_GpuMatchingEngine_buffer(JNIEnv* env, jclass cls, jlong handle, jint slot, jint column) {
     (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || slot < 0 || slot > 1 || h->slot[slot].n) return KME_E_INVALID;
-    jslot* sl = &h->slot[slot];
-    const size_t E = h->max_epoch;
-    jobject bufs[7] = {action, oid, aid, sid, price, size, rows};
-    const size_t need[7] = {4 * E, 8 * E, 8 * E, 8 * E, 4 * E, 4 * E,
-                            sizeof(kme_row) * (2 * E + 2 * (size_t)h->max_trades)};
-    void* addr[7];
-    for (int k = 0; k < 7; ++k) {
-        if (!bufs[k]) return KME_E_INVALID;
-        addr[k] = (*env)->GetDirectBufferAddress(env, bufs[k]);
-        const jlong cap = (*env)->GetDirectBufferCapacity(env, bufs[k]);
-        if (!addr[k] || cap < 0 || (size_t)cap < need[k] || ((uintptr_t)addr[k] & 7u)) return KME_E_INVALID;
-    }
-    for (int k = 0; k < 7; ++k) {
-        if (sl->regs[k]) { kme_host_unregister(h->e, sl->regs[k]); sl->regs[k] = NULL; }
-        const kme_status s = kme_host_register(h->e, addr[k], need[k]);
-        if (s != KME_OK) return s;
-        sl->regs[k] = addr[k];
-    }
-    sl->in.action = (const int32_t*)addr[0];
-    sl->in.oid = (const int64_t*)addr[1];
-    sl->in.aid = (const int64_t*)addr[2];
-    sl->in.sid = (const int64_t*)addr[3];
-    sl->in.price = (const int32_t*)addr[4];
-    sl->in.size = (const int32_t*)addr[5];
-    sl->rows = (kme_row*)addr[6];
-    sl->rows_cap = need[6] / sizeof(kme_row);
-    return KME_OK;
+    if (!h || slot < 0 || slot > 1 || column < 0 || column >= NCOL) { throw_state(env, "kme: no such buffer"); return NULL; }
+    return (*env)->NewDirectByteBuffer(env, h->slot[slot].col[column], (jlong)h->slot[slot].bytes[column]);
 }
 
 /* static native int submit(long h, int slot, int n): the slot's n buffered records as one epoch,
@@ -177,8 +230,8 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_submit(JNIEnv* env, jclass cls, jl
     jkme* h = (jkme*)(intptr_t)handle;
     if (!h || slot < 0 || slot > 1 || n <= 0 || (uint32_t)n > h->max_epoch) return KME_E_INVALID;
     jslot* sl = &h->slot[slot];
-    if (sl->n || !sl->rows) return KME_E_INVALID;   /* in flight already, or never bound */
-    const kme_status s = kme_submit_epoch_host(h->e, &sl->in, (uint32_t)n, &sl->res);
+    if (sl->n || sl->ready_rows >= 0) return KME_E_INVALID;   /* in flight, or its rows not forwarded yet */
+    const kme_status s = h_submit(h, &sl->in, (uint32_t)n, &sl->res);
     if (s == KME_OK) sl->n = (uint32_t)n;
     return s;
 }
@@ -190,14 +243,14 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_poll(JNIEnv* env, jclass cls, jlon
     jkme* h = (jkme*)(intptr_t)handle;
     if (!h) return -KME_E_INVALID;
     int done = 0;
-    const kme_status s = kme_poll(h->e, &done);
+    const kme_status s = h_poll(h, &done);
     return s == KME_OK ? (jint)done : -(jint)s;
 }
 
 /* static native int complete(long h, int slot, long[] status): waits for the slot's epoch (the oldest
  * in flight) and writes the MatchOut rows of the records that took effect into the slot's row buffer.
  * Returns the row count; status[0..3] = kme_status, domain detail, error index, records that took
- * effect. */
+ * effect.  The rows are ready until forwarded(h, slot). */
 JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, jlong handle, jint slot,
                                                          jlongArray status) {
     (void)cls;
@@ -207,7 +260,7 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, 
     jslot* sl = &h->slot[slot];
     kme_epoch_status st;
     memset(&st, 0, sizeof st);
-    const kme_status s = kme_wait(h->e, &st);
+    const kme_status s = h_wait(h, &st);
     const uint32_t n = sl->n;
     sl->n = 0;
     const uint32_t ne = s == KME_OK ? n : (st.n_effective < n ? st.n_effective : n);
@@ -219,8 +272,17 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, 
     stv[2] = (jlong)(s != KME_OK ? st.error_index : -1);
     stv[3] = (jlong)(x == KME_OK ? ne : 0);
     (*env)->SetLongArrayRegion(env, status, 0, 4, stv);
-    if (x != KME_OK) return 0;   /* (cannot happen: the row buffer holds 2 maxEpoch + 2 maxTrades rows) */
+    if (x != KME_OK) rows = 0;   /* (cannot happen: the row buffer holds 2 maxEpoch + 2 maxTrades rows) */
+    sl->ready_rows = (int64_t)rows;
+    sl->ready_seq = ++h->completions;
     return (jint)rows;
+}
+
+/* static native void forwarded(long h, int slot): the slot's ready rows have been forwarded. */
+JNIEXPORT void JNICALL Java_GpuMatchingEngine_forwarded(JNIEnv* env, jclass cls, jlong handle, jint slot) {
+    (void)env; (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (h && slot >= 0 && slot <= 1) h->slot[slot].ready_rows = -1;
 }
 
 /* static native String statusText(int status) */
@@ -229,22 +291,100 @@ JNIEXPORT jstring JNICALL Java_GpuMatchingEngine_statusText(JNIEnv* env, jclass 
     return (*env)->NewStringUTF(env, kme_strerror(s));
 }
 
-/* static native int checkpoint(long h, String path) / restore(long h, String path): persistence
- * in place of the RocksDB changelogs (KP:30-49); between epochs (nothing in flight), before commit. */
-static jint ckpt(JNIEnv* env, jlong handle, jstring path, int restore) {
+/* the ready slots, oldest completion first */
+static int ready_order(const jkme* h, int order[2]) {
+    int n = 0;
+    for (int s = 0; s < 2; ++s)
+        if (h->slot[s].ready_rows >= 0) order[n++] = s;
+    if (n == 2 && h->slot[order[0]].ready_seq > h->slot[order[1]].ready_seq) { order[0] = 1; order[1] = 0; }
+    return n;
+}
+
+/* static native int checkpoint(long h, String path, long offset): the commit point (called from the
+ * commit hook's StateStore.flush(), before Kafka Streams commits the consumed offsets; INTEGRATION.md
+ * §3): nothing may be in flight.  The file holds the engine state after every record up to `offset`
+ * and the MatchOut rows of the ready slots, so a restart loses no output of a committed record. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_checkpoint(JNIEnv* env, jclass cls, jlong handle, jstring path,
+                                                           jlong offset) {
+    (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || !path) return KME_E_INVALID;
+    if (!h || !path || h->slot[0].n || h->slot[1].n) return KME_E_INVALID;
+    int order[2];
+    const int nr = ready_order(h, order);
+    size_t bytes = sizeof(jrec_head);
+    for (int k = 0; k < nr; ++k) bytes += sizeof(jrec_slot) + sizeof(kme_row) * (size_t)h->slot[order[k]].ready_rows;
+    char* rec = (char*)malloc(bytes);
+    if (!rec) return KME_E_CAPACITY;
+    jrec_head hd = {JREC_MAGIC, (uint32_t)nr, (int64_t)offset};
+    memcpy(rec, &hd, sizeof hd);
+    size_t at = sizeof hd;
+    for (int k = 0; k < nr; ++k) {
+        const jslot* sl = &h->slot[order[k]];
+        jrec_slot rs = {(uint32_t)order[k], 0, (uint64_t)sl->ready_rows};
+        memcpy(rec + at, &rs, sizeof rs);
+        at += sizeof rs;
+        memcpy(rec + at, sl->rows, sizeof(kme_row) * (size_t)sl->ready_rows);
+        at += sizeof(kme_row) * (size_t)sl->ready_rows;
+    }
     const char* p = (*env)->GetStringUTFChars(env, path, NULL);
-    if (!p) return KME_E_INVALID;
-    const kme_status s = restore ? kme_restore(h->e, p) : kme_checkpoint(h->e, p);
-    (*env)->ReleaseStringUTFChars(env, path, p);
+    kme_status s = KME_E_INVALID;
+    if (p) {
+        s = h_checkpoint(h, p, rec, bytes);
+        (*env)->ReleaseStringUTFChars(env, path, p);
+    }
+    free(rec);
     return (jint)s;
 }
-JNIEXPORT jint JNICALL Java_GpuMatchingEngine_checkpoint(JNIEnv* env, jclass cls, jlong h, jstring path) {
+
+/* static native int restore(long h, String path, long[] out): a fresh engine takes the state of the
+ * checkpoint; out[0] = the last input offset it covers, out[1] = ready slots (rows to forward before
+ * anything else), then (slot, rows) per ready slot, oldest first -- their rows are back in the
+ * slots' row buffers.  Returns a kme_status. */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_restore(JNIEnv* env, jclass cls, jlong handle, jstring path,
+                                                        jlongArray out) {
     (void)cls;
-    return ckpt(env, h, path, 0);
-}
-JNIEXPORT jint JNICALL Java_GpuMatchingEngine_restore(JNIEnv* env, jclass cls, jlong h, jstring path) {
-    (void)cls;
-    return ckpt(env, h, path, 1);
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h || !path || !out || (*env)->GetArrayLength(env, out) < 6) return KME_E_INVALID;
+    if (h->slot[0].n || h->slot[1].n) return KME_E_INVALID;
+    const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!p) return KME_E_INVALID;
+    size_t bytes = 0;
+    kme_status s = h_restore(h, p, NULL, 0, &bytes);
+    char* rec = NULL;
+    if (s == KME_E_CAPACITY) {
+        rec = (char*)malloc(bytes);
+        s = rec ? h_restore(h, p, rec, bytes, &bytes) : KME_E_CAPACITY;
+    }
+    (*env)->ReleaseStringUTFChars(env, path, p);
+    jlong o[6] = {-1, 0, 0, 0, 0, 0};
+    if (s == KME_OK) {
+        jrec_head hd;
+        if (!rec || bytes < sizeof hd || (memcpy(&hd, rec, sizeof hd), hd.magic != JREC_MAGIC) || hd.n_ready > 2) {
+            s = KME_E_INVALID;   /* a checkpoint without the processor's record: not this processor's */
+        } else {
+            o[0] = hd.offset;
+            size_t at = sizeof hd;
+            for (uint32_t k = 0; k < hd.n_ready && s == KME_OK; ++k) {
+                jrec_slot rs;
+                if (at + sizeof rs > bytes) { s = KME_E_INVALID; break; }
+                memcpy(&rs, rec + at, sizeof rs);
+                at += sizeof rs;
+                if (rs.slot > 1 || rs.rows > h->slot[rs.slot].rows_cap || at + sizeof(kme_row) * rs.rows > bytes) {
+                    s = KME_E_INVALID;
+                    break;
+                }
+                jslot* sl = &h->slot[rs.slot];
+                memcpy(sl->rows, rec + at, sizeof(kme_row) * rs.rows);
+                at += sizeof(kme_row) * rs.rows;
+                sl->ready_rows = (int64_t)rs.rows;
+                sl->ready_seq = ++h->completions;
+                o[2 + 2 * k] = rs.slot;
+                o[3 + 2 * k] = (jlong)rs.rows;
+                o[1] = k + 1;
+            }
+        }
+    }
+    free(rec);
+    (*env)->SetLongArrayRegion(env, out, 0, 6, o);
+    return (jint)s;
 }

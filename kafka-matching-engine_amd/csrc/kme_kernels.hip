@@ -470,8 +470,11 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
 // FUNDED per-account proof: balance >= lb_start - need - debits >= 0 >= any single risk remaining,
 // i.e. every checkBalance (KP:177) of this epoch passes.  Otherwise the epoch runs serially
 // (KME_FLAG_SERIAL_FALLBACK) or is refused as a whole: KME_E_UNFUNDED / KME_D_UNPROVEN raised at
-// index 0, the smallest error code there is, so no indexed fault raised elsewhere in the epoch can
-// replace it and err_limit lets no record of the epoch take effect.
+// index 0, so that no fault at a later record can replace it (err_code orders by index first) and
+// err_limit lets no record of the epoch take effect.  At index 0 itself the code orders by detail,
+// and UNPROVEN (18) is the largest: a fault of record 0 (e.g. a duplicate oid) is reported instead.
+// That is the reference's outcome -- it throws at record 0 whatever the ledger holds (KP:96) -- and
+// either way no record of the epoch takes effect.
 __global__ void k_check_funded(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
@@ -519,39 +522,51 @@ __global__ void k_commit_funded(DevState S, EpochIO io) {
 // a mod N.  Every engine computes the same split from the same data, the shares sum to exactly the
 // pooled bound, so the invariant the proof rests on -- the account's cash is at least the sum of the
 // shards' bounds -- holds across the re-split.
+// An account absent on a shard (never created there, or created by an epoch only that shard refused,
+// k_commit_funded) reports demand -1: it takes no share, and the rounding left-over goes to a shard
+// that holds the account, so no credit leaves the pool.
 __global__ void __launch_bounds__(256) k_credit_state(DevState S, int64_t* out) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
-    out[a] = S.acct_since[a] == INT64_MAX ? 0 : S.acct_lb[a];
-    out[S.A + a] = S.acct_demand[a];
+    const bool present = S.acct_since[a] != INT64_MAX;
+    out[a] = present ? S.acct_lb[a] : 0;
+    out[S.A + a] = present ? S.acct_demand[a] : -1;
 }
-__global__ void __launch_bounds__(256) k_credit_adjust(DevState S, const int64_t* all, uint32_t n, uint32_t me) {
+// all: n blocks of `stride` words (bound [0, A), demand [A, 2A)), shard-major.
+__global__ void __launch_bounds__(256) k_credit_adjust(DevState S, const int64_t* all, uint32_t n, uint32_t me, size_t stride) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A || S.acct_since[a] == INT64_MAX) return;
     const size_t A = (size_t)S.A;
     unsigned __int128 tot = 0, dsum = 0;
+    uint32_t npresent = 0;
     for (uint32_t k = 0; k < n; ++k) {
-        const int64_t lb = all[(size_t)k * 2 * A + a], d = all[(size_t)k * 2 * A + A + a];
+        const int64_t lb = all[(size_t)k * stride + a], d = all[(size_t)k * stride + A + a];
+        if (d < 0) continue;   // absent on shard k
         tot += (unsigned __int128)(lb > 0 ? lb : 0);
-        dsum += (unsigned __int128)(d > 0 ? d : 0);
+        dsum += (unsigned __int128)d;
+        ++npresent;
     }
-    const unsigned __int128 mean = dsum / n;
-    unsigned __int128 wsum = 0, w_me = 0, given = 0;
+    const unsigned __int128 mean = dsum / npresent;   // (npresent >= 1: this shard holds the account)
+    unsigned __int128 wsum = 0;
     for (uint32_t k = 0; k < n; ++k) {
-        const int64_t d = all[(size_t)k * 2 * A + A + a];
-        const unsigned __int128 w = (unsigned __int128)(d > 0 ? d : 0) + mean + 1;
-        wsum += w;
-        if (k == me) w_me = w;
+        const int64_t d = all[(size_t)k * stride + A + a];
+        if (d >= 0) wsum += (unsigned __int128)d + mean + 1;
     }
-    unsigned __int128 mine = 0;
+    unsigned __int128 mine = 0, given = 0;
     for (uint32_t k = 0; k < n; ++k) {
-        const int64_t d = all[(size_t)k * 2 * A + A + a];
-        const unsigned __int128 share = tot * ((unsigned __int128)(d > 0 ? d : 0) + mean + 1) / wsum;
+        const int64_t d = all[(size_t)k * stride + A + a];
+        if (d < 0) continue;
+        const unsigned __int128 share = tot * ((unsigned __int128)d + mean + 1) / wsum;
         given += share;
         if (k == me) mine = share;
     }
-    (void)w_me;
-    if ((uint32_t)(a % n) == me) mine += tot - given;   // the rounding left-over
+    // the rounding left-over: the first shard holding the account, from a mod n on (cyclic)
+    uint32_t first = 0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t k = (uint32_t)((a + q) % n);
+        if (all[(size_t)k * stride + A + a] >= 0) { first = k; break; }
+    }
+    if (first == me) mine += tot - given;
     S.acct_lb[a] = (int64_t)mine;
 }
 
@@ -3970,8 +3985,8 @@ void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, vo
 void launch_credit_state(const DevState& S, int64_t* out, hipStream_t st) {
     if (S.A) hipLaunchKernelGGL(k_credit_state, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, out);
 }
-void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, hipStream_t st) {
-    if (S.A) hipLaunchKernelGGL(k_credit_adjust, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, all, n, me);
+void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, size_t stride, hipStream_t st) {
+    if (S.A) hipLaunchKernelGGL(k_credit_adjust, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, all, n, me, stride);
 }
 void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st) {
     hipLaunchKernelGGL(k_export_trades, dim3(128), dim3(256), 0, st, reinterpret_cast<const int4*>(src), count, cap,

@@ -52,7 +52,8 @@ void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, vo
 void launch_init_state(const DevState& S, hipStream_t st);
 // credit between symbol shards: (funded bound, demand) per account out; the re-split from all shards' pairs
 void launch_credit_state(const DevState& S, int64_t* out, hipStream_t st);
-void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, hipStream_t st);
+// all: n blocks of `stride` int64 words each ([0, A) bound, [A, 2A) demand, -1 = absent on that shard)
+void launch_credit_adjust(const DevState& S, const int64_t* all, uint32_t n, uint32_t me, size_t stride, hipStream_t st);
 // host epochs (kme_submit_epoch_host): trades[0, min(trade_off[n], cap)) into device-mapped host memory
 void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t cap, TradeRec* dst_mapped, hipStream_t st);
 

@@ -1,0 +1,448 @@
+// kme_multi.cpp -- one MatchIn stream over N engines (symbol shards), behind the same host-epoch
+// calls as one engine: the drop-in's multi-GPU path (include/kme.h "Multi-GPU drop-in").
+//
+// The reference runs one processor over a one-partition MatchIn (topic.js:17-18,
+// exchange_test.js:14-16; KP:51-52).  Books of different symbols never interact, so an epoch is split
+// by the C router (kme_router_split: Kafka's keyed partitioner over |sid|, cancels to their order's
+// partition, account records to every partition with 1/N of the credit each), each part goes to its
+// engine as a host epoch (device k of the list, credit_shards = N), and the results come back merged
+// into input order through the router's index -- the caller sees one epoch's kme_epoch_result,
+// exactly what one engine over the whole stream returns.  Between epochs the engines' funded credit
+// is pooled and split again (kme_credit_state / kme_credit_adjust), queued on the
+// engine streams behind the epochs in flight, the blocks moved between devices by peer copies.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kme.h"
+#include "kme_internal.h"
+
+namespace {
+
+void* page_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, std::max<size_t>((bytes + 4095) & ~(size_t)4095, 4096)) != 0) return nullptr;
+    std::memset(p, 0, std::max<size_t>(bytes, 1));
+    return p;
+}
+
+// One shard's part of one epoch slot: its records (router output), which of them it answers and
+// their input indices, and its results.
+struct Part {
+    kme_orders_buf in{};
+    uint8_t* echo = nullptr;
+    uint32_t* index = nullptr;
+    kme_epoch_result res{};
+    uint32_t count = 0;
+    std::vector<void*> mem;
+};
+
+constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '1'};
+struct MultiHeader {
+    char magic[8];
+    uint32_t n, _pad;
+    uint64_t generation;
+    uint64_t app_bytes;
+};
+
+}  // namespace
+
+struct kme_multi {
+    kme_config cfg{};                      // per engine (credit_shards = n)
+    uint32_t n = 0;
+    std::vector<kme_engine*> eng;
+    std::vector<int> dev;
+    kme_router* router = nullptr;
+    std::vector<Part> part[2];             // per slot, per shard
+    uint32_t slot_n[2] = {};
+    kme_epoch_result slot_out[2] = {};
+    int inflight = 0;
+    uint32_t sub_count = 0;
+    int failed = 0;
+    // credit re-splitting: per engine n blocks of (bound, demand) on its device
+    std::vector<int64_t*> d_credit;
+    std::vector<hipEvent_t> ev_state, ev_copied;
+    bool credit_used = false;
+    uint32_t rebalance_every = 1, since_rebalance = 0;
+    uint64_t generation = 0;               // checkpoint generation (shard files path.g<gen>.<k>)
+};
+
+static void free_parts(kme_multi* m) {
+    for (auto& slot : m->part)
+        for (size_t k = 0; k < slot.size(); ++k) {
+            for (void* p : slot[k].mem) {
+                if (k < m->eng.size() && m->eng[k]) (void)kme_host_unregister(m->eng[k], p);
+                std::free(p);
+            }
+            slot[k].mem.clear();
+        }
+}
+
+extern "C" {
+
+kme_status kme_multi_destroy(kme_multi* m) {
+    if (!m) return KME_E_INVALID;
+    for (uint32_t k = 0; k < m->eng.size(); ++k) {   // queued epochs land before their buffers go
+        if (!m->eng[k]) continue;
+        kme_epoch_status st;
+        for (int q = 0; q < m->inflight; ++q) (void)kme_wait(m->eng[k], &st);
+    }
+    free_parts(m);
+    for (size_t k = 0; k < m->d_credit.size(); ++k) {
+        (void)hipSetDevice(m->dev[k]);
+        if (m->d_credit[k]) (void)hipFree(m->d_credit[k]);
+        if (m->ev_state[k]) (void)hipEventDestroy(m->ev_state[k]);
+        if (m->ev_copied[k]) (void)hipEventDestroy(m->ev_copied[k]);
+    }
+    for (kme_engine* e : m->eng)
+        if (e) kme_destroy(e);
+    if (m->router) kme_router_destroy(m->router);
+    delete m;
+    return KME_OK;
+}
+
+kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* devices, kme_multi** out) {
+    if (!cfg || !out || n == 0 || n > 1024 || !devices) return KME_E_INVALID;
+    // shards prove their orders against their share of each account's credit: FUNDED, no exact ledger
+    // (it couples every symbol, kme_create refuses it with credit_shards > 1)
+    if (cfg->mode != KME_MODE_FUNDED || (n > 1 && cfg->flags != 0)) return KME_E_INVALID;
+    kme_multi* m = new kme_multi();
+    m->cfg = *cfg;
+    m->cfg.credit_shards = n;
+    m->n = n;
+    if (const char* v = std::getenv("KME_MULTI_REBALANCE_EVERY")) m->rebalance_every = (uint32_t)std::max(0, std::atoi(v));
+    kme_status s = kme_router_create(n, (uint64_t)cfg->max_resting + cfg->max_epoch, &m->router);
+    for (uint32_t k = 0; k < n && s == KME_OK; ++k) {
+        kme_config c = m->cfg;
+        c.device = devices[k];
+        kme_engine* e = nullptr;
+        s = kme_create(&c, &e);
+        m->eng.push_back(e);
+        m->dev.push_back(devices[k]);
+    }
+    const size_t E = cfg->max_epoch, T = cfg->max_trades;
+    for (int slot = 0; slot < 2 && s == KME_OK; ++slot) {
+        m->part[slot].resize(n);
+        for (uint32_t k = 0; k < n && s == KME_OK; ++k) {
+            Part& p = m->part[slot][k];
+            auto get = [&](size_t bytes) -> void* {
+                void* q = page_alloc(bytes);
+                if (!q) { s = KME_E_CAPACITY; return nullptr; }
+                p.mem.push_back(q);
+                if (kme_host_register(m->eng[k], q, bytes) != KME_OK) s = KME_E_HIP;
+                return q;
+            };
+            p.in.action = (int32_t*)get(4 * E); p.in.oid = (int64_t*)get(8 * E); p.in.aid = (int64_t*)get(8 * E);
+            p.in.sid = (int64_t*)get(8 * E); p.in.price = (int32_t*)get(4 * E); p.in.size = (int32_t*)get(4 * E);
+            p.echo = (uint8_t*)get(E);
+            p.index = (uint32_t*)get(4 * E);
+            p.res.out_action = (int32_t*)get(4 * E); p.res.out_size = (int32_t*)get(4 * E);
+            p.res.out_prev = (int64_t*)get(8 * E); p.res.out_flags = (uint8_t*)get(E);
+            p.res.trade_off = (uint32_t*)get(4 * (E + 1));
+            p.res.trades = (kme_trade*)get(sizeof(kme_trade) * T);
+            p.res.trades_cap = (uint32_t)T;
+        }
+    }
+    if (s == KME_OK && n > 1) {
+        const size_t A = cfg->max_accounts;
+        for (uint32_t k = 0; k < n && s == KME_OK; ++k) {
+            int64_t* d = nullptr;
+            hipEvent_t a = nullptr, b = nullptr;
+            if (hipSetDevice(m->dev[k]) != hipSuccess || hipMalloc((void**)&d, (size_t)n * 2 * A * sizeof(int64_t)) != hipSuccess ||
+                hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess)
+                s = KME_E_HIP;
+            m->d_credit.push_back(d);
+            m->ev_state.push_back(a);
+            m->ev_copied.push_back(b);
+        }
+    }
+    if (s != KME_OK) {
+        kme_multi_destroy(m);
+        return s;
+    }
+    *out = m;
+    return KME_OK;
+}
+
+}  // extern "C"
+
+// The pooled credit split again over the shards, queued behind every engine's epochs in flight and
+// before the next epoch: each engine's (bound, demand) block after its last epoch, copied to every
+// other engine's device, then each engine's adjust (every engine computes the same split).
+static kme_status rebalance_enqueue(kme_multi* m) {
+    const uint32_t n = m->n;
+    const size_t A = m->cfg.max_accounts, blk = 2 * A;
+    for (uint32_t k = 0; k < n; ++k) {
+        hipStream_t st = kme::engine_stream(m->eng[k]);
+        if (hipSetDevice(m->dev[k]) != hipSuccess) return KME_E_HIP;
+        if (m->credit_used)   // the last round's copies out of this block have been made
+            for (uint32_t j = 0; j < n; ++j)
+                if (j != k && hipStreamWaitEvent(st, m->ev_copied[j], 0) != hipSuccess) return KME_E_HIP;
+        if (kme_status s = kme::credit_state_enqueue(m->eng[k], m->d_credit[k] + k * blk)) return s;
+        if (hipEventRecord(m->ev_state[k], st) != hipSuccess) return KME_E_HIP;
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        hipStream_t st = kme::engine_stream(m->eng[j]);
+        if (hipSetDevice(m->dev[j]) != hipSuccess) return KME_E_HIP;
+        for (uint32_t k = 0; k < n; ++k) {
+            if (k == j) continue;
+            if (hipStreamWaitEvent(st, m->ev_state[k], 0) != hipSuccess ||
+                hipMemcpyPeerAsync(m->d_credit[j] + k * blk, m->dev[j], m->d_credit[k] + k * blk, m->dev[k],
+                                   blk * sizeof(int64_t), st) != hipSuccess)
+                return KME_E_HIP;
+        }
+        if (kme_status s = kme::credit_adjust_enqueue(m->eng[j], m->d_credit[j], n, j, blk)) return s;
+        if (hipEventRecord(m->ev_copied[j], st) != hipSuccess) return KME_E_HIP;
+    }
+    m->credit_used = true;
+    return KME_OK;
+}
+
+extern "C" {
+
+kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
+    if (!m || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
+        !out->trades)
+        return KME_E_INVALID;
+    if (m->failed) return KME_E_FAILED;
+    if (n > m->cfg.max_epoch) return KME_E_CAPACITY;
+    if (m->inflight == 2) return KME_E_INVALID;
+    if (out->trades_cap < m->cfg.max_trades) return KME_E_INVALID;
+    if (m->n > 1 && m->rebalance_every && m->sub_count > 0 && ++m->since_rebalance >= m->rebalance_every) {
+        m->since_rebalance = 0;
+        if (kme_status s = rebalance_enqueue(m)) { m->failed = 1; return s; }
+    }
+    const int slot = (int)(m->sub_count & 1);
+    std::vector<Part>& parts = m->part[slot];
+    std::vector<kme_orders_buf> bufs(m->n);
+    std::vector<uint32_t> counts(m->n);
+    std::vector<uint8_t*> echo(m->n);
+    std::vector<uint32_t*> index(m->n);
+    for (uint32_t k = 0; k < m->n; ++k) {
+        bufs[k] = parts[k].in;
+        echo[k] = parts[k].echo;
+        index[k] = parts[k].index;
+    }
+    kme_status s = kme_router_split(m->router, in, n, bufs.data(), counts.data(), echo.data(), index.data());
+    if (s != KME_OK) return s;
+    // (a shard that receives more than max_epoch records cannot happen: a part is a subset of the epoch)
+    for (uint32_t k = 0; k < m->n; ++k) {
+        Part& p = parts[k];
+        p.count = counts[k];
+        const kme_orders pin{p.in.action, p.in.oid, p.in.aid, p.in.sid, p.in.price, p.in.size};
+        s = kme_submit_epoch_host(m->eng[k], &pin, p.count, &p.res);
+        if (s != KME_OK) {   // the shards before k hold a part of this epoch: nothing consistent remains
+            m->failed = 1;
+            return s;
+        }
+    }
+    m->slot_n[slot] = n;
+    m->slot_out[slot] = *out;
+    ++m->sub_count;
+    ++m->inflight;
+    return KME_OK;
+}
+
+kme_status kme_multi_poll(kme_multi* m, int* done) {
+    if (!m || !done) return KME_E_INVALID;
+    *done = 1;
+    for (kme_engine* e : m->eng) {
+        int d = 0;
+        if (kme_status s = kme_poll(e, &d)) return s;
+        if (!d) { *done = 0; return KME_OK; }
+    }
+    return KME_OK;
+}
+
+// Completes the oldest epoch: every shard's part, merged into input order.
+kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
+    if (!m) return KME_E_INVALID;
+    kme_epoch_status tot{};
+    tot.error_index = -1;
+    if (m->inflight == 0) {
+        tot.status = m->failed ? KME_E_FAILED : KME_OK;
+        if (st) *st = tot;
+        return (kme_status)tot.status;
+    }
+    const int slot = (int)((m->sub_count - (uint32_t)m->inflight) & 1);
+    --m->inflight;
+    std::vector<Part>& parts = m->part[slot];
+    const uint32_t n = m->slot_n[slot];
+    const kme_epoch_result& out = m->slot_out[slot];
+    std::vector<kme_epoch_status> sst(m->n);
+    for (uint32_t k = 0; k < m->n; ++k) (void)kme_wait(m->eng[k], &sst[k]);
+    // the first record (input order) a shard did not answer: its fault, or everything after a refusal
+    uint32_t limit = n;
+    int32_t lim_status = KME_OK, lim_detail = 0;
+    int64_t lim_index = -1;
+    for (uint32_t k = 0; k < m->n; ++k) {
+        const kme_epoch_status& s = sst[k];
+        tot.serial_fallback += s.serial_fallback;
+        if (s.status == KME_OK) continue;
+        const uint32_t ne = std::min(s.n_effective, parts[k].count);
+        const uint32_t at = ne < parts[k].count ? parts[k].index[ne] : n;
+        if (at < limit || (at == limit && lim_status == KME_OK)) {
+            limit = at;
+            lim_status = s.status;
+            lim_detail = s.detail;
+            lim_index = s.error_index >= 0 && (uint64_t)s.error_index < parts[k].count ? (int64_t)parts[k].index[s.error_index] : -1;
+        }
+    }
+    // OUT echoes and per-record trade counts (trade_off[i + 1] for now), each shard on its own thread
+    auto scatter = [&](uint32_t k) {
+        const Part& p = parts[k];
+        const uint32_t* to = p.res.trade_off;
+        for (uint32_t j = 0; j < p.count; ++j) {
+            if (!p.echo[j]) continue;
+            const uint32_t i = p.index[j];
+            if (i >= limit) break;
+            out.out_action[i] = p.res.out_action[j];
+            out.out_size[i] = p.res.out_size[j];
+            out.out_prev[i] = p.res.out_prev[j];
+            out.out_flags[i] = p.res.out_flags[j];
+            out.trade_off[i + 1] = to[j + 1] - to[j];
+        }
+    };
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < m->n; ++k) th.emplace_back(scatter, k);
+    scatter(0);
+    for (auto& t : th) t.join();
+    th.clear();
+    out.trade_off[0] = 0;
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < limit; ++i) {
+        acc += out.trade_off[i + 1];
+        if (acc > out.trades_cap) {   // the merged epoch's trades do not fit: its prefix that does
+            limit = i;
+            lim_status = KME_E_CAPACITY;
+            lim_detail = KME_D_CAP_TRADES;
+            lim_index = i;
+            acc -= out.trade_off[i + 1];
+            break;
+        }
+        out.trade_off[i + 1] = (uint32_t)acc;
+    }
+    auto gather = [&](uint32_t k) {
+        const Part& p = parts[k];
+        const uint32_t* to = p.res.trade_off;
+        for (uint32_t j = 0; j < p.count; ++j) {
+            if (!p.echo[j]) continue;
+            const uint32_t i = p.index[j];
+            if (i >= limit) break;
+            const uint32_t c = to[j + 1] - to[j];
+            if (c) std::memcpy(out.trades + out.trade_off[i], p.res.trades + to[j], (size_t)c * sizeof(kme_trade));
+        }
+    };
+    for (uint32_t k = 1; k < m->n; ++k) th.emplace_back(gather, k);
+    gather(0);
+    for (auto& t : th) t.join();
+    for (uint32_t k = 0; k < m->n; ++k) {
+        const Part& p = parts[k];
+        for (uint32_t j = 0; j < p.count; ++j) {   // counted once: partition 0 answers account records
+            if (!p.echo[j] || p.index[j] >= limit) continue;
+            const int32_t a = p.in.action[j];
+            tot.n_orders += (a == KME_BUY || a == KME_SELL || a == KME_CANCEL) ? 1 : 0;
+        }
+        if (sst[k].status == KME_OK) {
+            tot.n_rests += sst[k].n_rests;
+            tot.n_cancel_ok += sst[k].n_cancel_ok;
+        }
+    }
+    tot.n_inputs = n;
+    tot.n_trades = (uint32_t)acc;
+    tot.n_maker_visits = acc;
+    tot.n_effective = limit;
+    tot.status = lim_status;
+    tot.detail = lim_detail;
+    tot.error_index = lim_status == KME_OK ? -1 : lim_index;
+    // any fault leaves the shards out of step with one another (the others went past it): like the
+    // reference's dead stream thread, nothing further is accepted
+    if (lim_status != KME_OK) m->failed = 1;
+    if (st) *st = tot;
+    return (kme_status)tot.status;
+}
+
+kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out) {
+    if (!m || !out || k >= m->n) return KME_E_INVALID;
+    *out = m->eng[k];
+    return KME_OK;
+}
+
+// Checkpoint: every engine into path.g<generation>.<k>, then the manifest at `path` (written to
+// path.tmp and renamed: the commit of the set), then the previous generation's files are removed.
+kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* app, size_t app_bytes) {
+    if (!m || !path || (app_bytes && !app)) return KME_E_INVALID;
+    if (m->failed) return KME_E_FAILED;
+    if (m->inflight) return KME_E_INVALID;
+    const uint64_t gen = m->generation + 1;
+    const std::string base(path);
+    for (uint32_t k = 0; k < m->n; ++k) {
+        const std::string f = base + ".g" + std::to_string(gen) + "." + std::to_string(k);
+        if (kme_status s = kme_checkpoint_app(m->eng[k], f.c_str(), nullptr, 0)) return s;
+    }
+    MultiHeader h{};
+    std::memcpy(h.magic, kMultiMagic, sizeof h.magic);
+    h.n = m->n;
+    h.generation = gen;
+    h.app_bytes = app_bytes;
+    const std::string tmp = base + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return KME_E_INVALID;
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && (app_bytes == 0 || std::fwrite(app, 1, app_bytes, f) == app_bytes);
+    ok = std::fflush(f) == 0 && ok;
+    ok = std::fclose(f) == 0 && ok;
+    ok = ok && std::rename(tmp.c_str(), path) == 0;
+    if (!ok) return KME_E_INVALID;
+    for (uint32_t k = 0; k < m->n && m->generation; ++k)
+        std::remove((base + ".g" + std::to_string(m->generation) + "." + std::to_string(k)).c_str());
+    m->generation = gen;
+    return KME_OK;
+}
+
+kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size_t app_cap, size_t* app_bytes) {
+    if (!m || !path) return KME_E_INVALID;
+    if (m->failed) return KME_E_FAILED;
+    if (m->inflight) return KME_E_INVALID;
+    if (app_bytes) *app_bytes = 0;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return KME_E_INVALID;
+    MultiHeader h{};
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 &&
+              h.n == m->n && h.app_bytes < (1ull << 40);
+    std::vector<char> rec;
+    if (ok && h.app_bytes) {
+        rec.resize(h.app_bytes);
+        ok = std::fread(rec.data(), 1, rec.size(), f) == rec.size();
+    }
+    std::fclose(f);
+    if (!ok) return KME_E_INVALID;
+    if (app_bytes) *app_bytes = rec.size();
+    if (rec.size() > app_cap || (rec.size() && !app)) return KME_E_CAPACITY;
+    const std::string base(path);
+    for (uint32_t k = 0; k < m->n; ++k) {
+        const std::string fk = base + ".g" + std::to_string(h.generation) + "." + std::to_string(k);
+        if (kme_status s = kme_restore(m->eng[k], fk.c_str())) {
+            if (k > 0) m->failed = 1;   // some shards restored, others not
+            return s;
+        }
+    }
+    // the router's oid directory: every resting order's partition (a cancel of an order resting
+    // nowhere is rejected by whichever engine gets it, KP:290-291, so no other entry matters)
+    for (uint32_t k = 0; k < m->n; ++k) {
+        std::vector<int64_t> oids;
+        if (kme_status s = kme::resting_oids(m->eng[k], oids)) { m->failed = 1; return s; }
+        kme::router_seed(m->router, oids.data(), oids.size(), k);
+    }
+    m->generation = h.generation;
+    if (rec.size()) std::memcpy(app, rec.data(), rec.size());
+    return KME_OK;
+}
+
+}  // extern "C"

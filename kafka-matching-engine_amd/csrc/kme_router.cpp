@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "kme.h"
+#include "kme_internal.h"
 
 namespace {
 
@@ -112,6 +113,12 @@ struct kme_router {
     }
     uint32_t owner(int64_t oid) const { return (uint32_t)((mix64((uint64_t)oid ^ 0x5bd1e995ull) >> 40) % ndir); }
 };
+
+namespace kme {
+void router_seed(kme_router* r, const int64_t* oids, size_t n, uint32_t partition) {
+    for (size_t i = 0; i < n; ++i) r->dir[r->owner(oids[i])].put(oids[i], (uint16_t)partition);
+}
+}  // namespace kme
 
 extern "C" {
 

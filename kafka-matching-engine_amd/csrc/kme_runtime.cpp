@@ -7,6 +7,7 @@
 //   kme_destroy           MatchingEngine.close KP:129
 //   kme_snapshot_*        the contents of Books/Buckets/Orders and Balances/Positions
 #include <dlfcn.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -20,6 +21,7 @@
 #include "kme.h"
 #include "kme_device.h"
 #include "kme_launch.h"
+#include "kme_internal.h"
 
 using namespace kme;
 
@@ -98,6 +100,11 @@ struct kme_engine {
     bool hs_ready = false;
     hipStream_t in_stream = nullptr, out_stream = nullptr;
     hipEvent_t ev_in[2] = {};
+    // caller host memory registered through this engine (kme_host_register): exact ranges with a
+    // count; `owned` = this engine's hipHostRegister made it (another owner's registration of the same
+    // pages is used, never undone here)
+    struct HostReg { uintptr_t p; size_t bytes; int refs; bool owned; };
+    std::vector<HostReg> host_regs;
     bool host_epoch[2] = {};              // the epoch of this slot is a host epoch
     bool host_mapped[2] = {};             // its trades go out through the device mapping (k_export_trades)
     kme_epoch_result host_out[2] = {};    // the caller's result buffers of that epoch
@@ -344,7 +351,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
 kme_status kme_destroy(kme_engine* e) {
     if (!e) return KME_E_INVALID;
     (void)hipSetDevice(e->device);
+    // every queued copy and kernel of the engine finishes before its memory goes
+    if (e->in_stream) (void)hipStreamSynchronize(e->in_stream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->lane_stream) (void)hipStreamSynchronize(e->lane_stream);
+    if (e->out_stream) (void)hipStreamSynchronize(e->out_stream);
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
@@ -356,6 +367,8 @@ kme_status kme_destroy(kme_engine* e) {
     for (auto& ev : e->ev_in) if (ev) (void)hipEventDestroy(ev);
     if (e->in_stream) (void)hipStreamDestroy(e->in_stream);
     if (e->out_stream) (void)hipStreamDestroy(e->out_stream);
+    for (auto& r : e->host_regs)
+        if (r.owned) (void)hipHostUnregister((void*)r.p);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->lane_stream) (void)hipStreamDestroy(e->lane_stream);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -517,9 +530,10 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     e->last_busy = c[ci(C_BUSY)];
     e->last_light = c[ci(C_LIGHT)];
     e->last_cancel_heavy = c[ci(C_CANCEL_OK)] * 8 > (uint64_t)last_n;
-    if (host_overflow && c[ci(C_ERR)] == ~0ull) {   // the caller's trades buffer is too small for the epoch
+    if (host_overflow && c[ci(C_ERR)] == ~0ull) {
+        // (cannot happen: kme_submit_epoch_host takes only trades buffers of max_trades records, and the
+        // device never produces more; reported, the engine stays usable)
         s.status = KME_E_CAPACITY; s.detail = KME_D_CAP_TRADES; s.n_effective = 0;
-        e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_TRADES;
     } else if (c[ci(C_ERR)] != ~0ull) {
         s.status = (int32_t)(c[ci(C_ERR)] & 0xFF);
         s.detail = (int32_t)((c[ci(C_ERR)] >> 8) & 0xFF);
@@ -579,21 +593,48 @@ kme_status kme_poll(kme_engine* e, int* done) {
     return KME_E_HIP;
 }
 
+// Registration pins whole pages, so two buffers that share a page cannot be registered and
+// unregistered independently: the engine keeps the exact ranges it registered, counts repeats of the
+// same range, and refuses a range that shares a page with a different one (KME_E_INVALID; callers
+// allocate page-aligned buffers -- the JNI glue allocates the processor's buffers itself).
 kme_status kme_host_register(kme_engine* e, void* host, size_t bytes) {
     if (!e || !host || !bytes) return KME_E_INVALID;
+    const uintptr_t p = (uintptr_t)host, pg = 4096;
+    const uintptr_t lo = p & ~(pg - 1), hi = (p + bytes + pg - 1) & ~(pg - 1);
+    for (auto& r : e->host_regs) {
+        if (r.p == p && r.bytes == bytes) { ++r.refs; return KME_OK; }
+        const uintptr_t rlo = r.p & ~(pg - 1), rhi = (r.p + r.bytes + pg - 1) & ~(pg - 1);
+        if (lo < rhi && rlo < hi) return KME_E_INVALID;   // shares a page with another registered range
+    }
     HIP_TRY(hipSetDevice(e->device));
     const hipError_t r = hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
-    if (r == hipErrorHostMemoryAlreadyRegistered) { (void)hipGetLastError(); return KME_OK; }
-    HIP_TRY(r);
+    bool owned = true;
+    if (r == hipErrorHostMemoryAlreadyRegistered) {   // registered by its owner elsewhere: used, never undone here
+        (void)hipGetLastError();
+        owned = false;
+    } else {
+        HIP_TRY(r);
+    }
+    e->host_regs.push_back({p, bytes, 1, owned});
     return KME_OK;
 }
 
 kme_status kme_host_unregister(kme_engine* e, void* host) {
     if (!e || !host) return KME_E_INVALID;
     if (e->inflight) return KME_E_INVALID;
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipHostUnregister(host));
-    return KME_OK;
+    for (size_t k = 0; k < e->host_regs.size(); ++k) {
+        auto& r = e->host_regs[k];
+        if (r.p != (uintptr_t)host) continue;
+        if (--r.refs > 0) return KME_OK;
+        const bool owned = r.owned;
+        e->host_regs.erase(e->host_regs.begin() + (long)k);
+        if (owned) {
+            HIP_TRY(hipSetDevice(e->device));
+            HIP_TRY(hipHostUnregister(host));
+        }
+        return KME_OK;
+    }
+    return KME_E_INVALID;   // not registered through this engine
 }
 
 static kme_status host_slots(kme_engine* e) {
@@ -617,8 +658,11 @@ static kme_status host_slots(kme_engine* e) {
 
 kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
     if (!e || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
-        (!out->trades && out->trades_cap))
+        !out->trades)
         return KME_E_INVALID;
+    // the caller's trades buffer must hold an epoch's worth (max_trades): a smaller one could not take
+    // the results of an epoch the device has already committed
+    if (out->trades_cap < e->cfg.max_trades) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
     if (e->inflight == 2) return KME_E_INVALID;
@@ -699,7 +743,8 @@ struct kme_comm {
     ncclComm_t comm = nullptr;
     uint32_t n = 0, rank = 0;
     int device = 0;
-    int64_t* d_credit = nullptr;     // kme_credit_rebalance: n x (bound, demand) x accounts
+    int64_t* d_credit = nullptr;     // kme_credit_rebalance: n blocks of (bound, demand) x accounts + a status word
+    int64_t* h_status = nullptr;     // pinned: the ranks' status words (+ this rank's outgoing one)
     size_t credit_accounts = 0;
 };
 
@@ -733,6 +778,7 @@ kme_status kme_comm_destroy(kme_comm* c) {
     Rccl* r = rccl();
     (void)hipSetDevice(c->device);
     if (c->d_credit) (void)hipFree(c->d_credit);
+    if (c->h_status) (void)hipHostFree(c->h_status);
     if (r && c->comm) r->destroy(c->comm);
     delete c;
     return KME_OK;
@@ -766,34 +812,89 @@ kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_s
     if (e->inflight) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     HIP_TRY(hipSetDevice(e->device));
-    launch_credit_adjust(e->S, dev_all, n_shards, my_shard, e->stream);
+    launch_credit_adjust(e->S, dev_all, n_shards, my_shard, 2 * (size_t)e->cfg.max_accounts, e->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(e->stream));
     return KME_OK;
 }
 
+// A collective: every rank takes part in the all-gather whatever its own state, so no rank waits
+// for a peer that returned early.  Each rank's block is (bound, demand) per account plus a status
+// word; a rank that cannot re-split (an epoch in flight, a failed engine) sends zeros and its status,
+// and when any status is not OK no rank adjusts: that rank returns its own status, the others
+// KME_E_INVALID ("skipped on every rank").
 kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c) {
     if (!e || !c || e->cfg.mode != KME_MODE_FUNDED) return KME_E_INVALID;
-    if (e->inflight) return KME_E_INVALID;
-    if (e->failed) return KME_E_FAILED;
     Rccl* r = rccl();
-    if (!r) return KME_E_UNSUPPORTED;
+    if (!r) return KME_E_UNSUPPORTED;   // (a communicator exists only where RCCL loaded: the same on every rank)
     HIP_TRY(hipSetDevice(e->device));
-    const size_t A = e->cfg.max_accounts;
+    const size_t A = e->cfg.max_accounts, stride = 2 * A + 1;
     if (!c->d_credit || c->credit_accounts != A) {
         if (c->d_credit) HIP_TRY(hipFree(c->d_credit));
+        if (c->h_status) HIP_TRY(hipHostFree(c->h_status));
         c->d_credit = nullptr;
-        HIP_TRY(hipMalloc((void**)&c->d_credit, (size_t)c->n * 2 * A * sizeof(int64_t)));
+        c->h_status = nullptr;
+        HIP_TRY(hipMalloc((void**)&c->d_credit, (size_t)c->n * stride * sizeof(int64_t)));
+        HIP_TRY(hipHostMalloc((void**)&c->h_status, ((size_t)c->n + 1) * sizeof(int64_t), hipHostMallocDefault));
         c->credit_accounts = A;
     }
-    int64_t* mine = c->d_credit + (size_t)c->rank * 2 * A;
-    launch_credit_state(e->S, mine, e->stream);
+    const int64_t mine_st = e->failed ? KME_E_FAILED : e->inflight ? KME_E_INVALID : KME_OK;
+    int64_t* mine = c->d_credit + (size_t)c->rank * stride;
+    c->h_status[c->n] = mine_st;
+    if (mine_st == KME_OK) launch_credit_state(e->S, mine, e->stream);
+    else HIP_TRY(hipMemsetAsync(mine, 0, 2 * A * sizeof(int64_t), e->stream));
     HIP_TRY(hipGetLastError());
-    if (r->allgather(mine, c->d_credit, 2 * A * sizeof(int64_t), ncclUint8, c->comm, e->stream) != ncclSuccess)
+    HIP_TRY(hipMemcpyAsync(mine + 2 * A, &c->h_status[c->n], sizeof(int64_t), hipMemcpyHostToDevice, e->stream));
+    if (r->allgather(mine, c->d_credit, stride * sizeof(int64_t), ncclUint8, c->comm, e->stream) != ncclSuccess)
         return KME_E_HIP;
-    return kme_credit_adjust(e, c->d_credit, c->n, c->rank);
+    HIP_TRY(hipMemcpy2DAsync(c->h_status, sizeof(int64_t), c->d_credit + 2 * A, stride * sizeof(int64_t), sizeof(int64_t),
+                             c->n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    bool all_ok = true;
+    for (uint32_t k = 0; k < c->n; ++k) all_ok = all_ok && c->h_status[k] == KME_OK;
+    if (!all_ok) return mine_st != KME_OK ? (kme_status)mine_st : KME_E_INVALID;
+    launch_credit_adjust(e->S, c->d_credit, c->n, c->rank, stride, e->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return KME_OK;
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------------ internals for kme_multi (kme_internal.h)
+namespace kme {
+hipStream_t engine_stream(kme_engine* e) { return e->stream; }
+int engine_device(kme_engine* e) { return e->device; }
+const kme_config& engine_config(kme_engine* e) { return e->cfg; }
+kme_status credit_state_enqueue(kme_engine* e, int64_t* dev_out) {
+    HIP_TRY(hipSetDevice(e->device));
+    launch_credit_state(e->S, dev_out, e->stream);
+    HIP_TRY(hipGetLastError());
+    return KME_OK;
+}
+kme_status credit_adjust_enqueue(kme_engine* e, const int64_t* dev_all, uint32_t n, uint32_t me, size_t stride) {
+    HIP_TRY(hipSetDevice(e->device));
+    launch_credit_adjust(e->S, dev_all, n, me, stride, e->stream);
+    HIP_TRY(hipGetLastError());
+    return KME_OK;
+}
+kme_status resting_oids(kme_engine* e, std::vector<int64_t>& out) {
+    if (e->inflight) return KME_E_INVALID;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long ctr[C_NCTR * CTR_STRIDE];
+    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
+    std::vector<Node> pool(nslots);
+    if (nslots) HIP_TRY(hipMemcpy(pool.data(), e->S.pool, nslots * sizeof(Node), hipMemcpyDeviceToHost));
+    out.clear();
+    for (const Node& nd : pool)
+        if (nd.live) out.push_back(nd.oid);
+    return KME_OK;
+}
+}  // namespace kme
+
+extern "C" {
 #ifndef KME_SRC_HASH
 #define KME_SRC_HASH "unknown"
 #endif
@@ -801,7 +902,8 @@ const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
 namespace {
-constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '1'};
+constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '1'};    // format 1: no application record
+constexpr char kCkptMagic2[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '2'};
 struct CkptHeader {
     char magic[8];
     kme_config cfg;
@@ -836,8 +938,11 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
 }
 }  // namespace
 
-kme_status kme_checkpoint(kme_engine* e, const char* path) {
-    if (!e || !path) return KME_E_INVALID;
+// Format: header, the state blobs (u64 size + bytes each), then the application record (u64 size +
+// bytes; format 2).  Written to `path`.tmp, flushed to disk, then renamed over `path`: a crash while
+// writing leaves the previous checkpoint whole.
+kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes) {
+    if (!e || !path || (app_bytes && !app)) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (e->inflight) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
     HIP_TRY(hipSetDevice(e->device));
@@ -848,14 +953,15 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
     // changed nothing: the engine's state is the one before it)
     if (ctr[ci(C_ERR)] != ~0ull && (ctr[ci(C_ERR)] & 0xFF) != KME_E_UNFUNDED) return KME_E_FAILED;
     CkptHeader h{};
-    std::memcpy(h.magic, kCkptMagic, sizeof h.magic);
+    std::memcpy(h.magic, kCkptMagic2, sizeof h.magic);
     h.cfg = e->cfg;
     h.seq_base = e->seq_base;
     h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
     h.otab_used = ctr[ci(C_OTAB_USED)];
     h.bal_used = ctr[ci(C_BAL_USED)];
     h.pos_used = ctr[ci(C_POS_USED)];
-    FILE* f = std::fopen(path, "wb");
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return KME_E_INVALID;
     bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
     std::vector<char> host;
@@ -866,19 +972,30 @@ kme_status kme_checkpoint(kme_engine* e, const char* path) {
         const uint64_t n = b.bytes;
         ok = std::fwrite(&n, sizeof n, 1, f) == 1 && (n == 0 || std::fwrite(host.data(), 1, n, f) == n);
     }
+    const uint64_t an = app_bytes;
+    ok = ok && std::fwrite(&an, sizeof an, 1, f) == 1 && (an == 0 || std::fwrite(app, 1, an, f) == an);
+    ok = std::fflush(f) == 0 && ok;
+    ok = fsync(fileno(f)) == 0 && ok;
     ok = std::fclose(f) == 0 && ok;
+    ok = ok && std::rename(tmp.c_str(), path) == 0;
+    if (!ok) std::remove(tmp.c_str());
     return ok ? KME_OK : KME_E_INVALID;
 }
 
-kme_status kme_restore(kme_engine* e, const char* path) {
+kme_status kme_checkpoint(kme_engine* e, const char* path) { return kme_checkpoint_app(e, path, nullptr, 0); }
+
+kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t app_cap, size_t* app_bytes) {
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (e->inflight) return KME_E_INVALID;
+    if (app_bytes) *app_bytes = 0;
     HIP_TRY(hipSetDevice(e->device));
     FILE* f = std::fopen(path, "rb");
     if (!f) return KME_E_INVALID;
     CkptHeader h{};
-    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, sizeof h.magic) == 0;
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1;
+    const bool v2 = ok && std::memcmp(h.magic, kCkptMagic2, sizeof h.magic) == 0;
+    ok = ok && (v2 || std::memcmp(h.magic, kCkptMagic, sizeof h.magic) == 0);
     // the same store geometry (device, stream and timing choices may differ; max_epoch sizes the
     // oid table, whose blob size is checked below)
     ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
@@ -889,6 +1006,15 @@ kme_status kme_restore(kme_engine* e, const char* path) {
     // the whole file is read and checked before anything reaches the device: a mismatched or
     // truncated checkpoint leaves the engine untouched
     const std::vector<Blob> blobs = ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{};
+    if (ok && v2) {   // the record's size first (it follows the blobs): a buffer too small costs no read of the state
+        long off = (long)sizeof h;
+        for (const Blob& b : blobs) off += (long)(sizeof(uint64_t) + b.bytes);
+        uint64_t an = 0;
+        ok = std::fseek(f, off, SEEK_SET) == 0 && std::fread(&an, sizeof an, 1, f) == 1 && an < (1ull << 40);
+        if (ok && app_bytes) *app_bytes = (size_t)an;
+        if (ok && (an > app_cap || (an && !app))) { std::fclose(f); return KME_E_CAPACITY; }
+        ok = ok && std::fseek(f, (long)sizeof h, SEEK_SET) == 0;
+    }
     std::vector<std::vector<char>> host(blobs.size());
     for (size_t k = 0; ok && k < blobs.size(); ++k) {
         uint64_t n = 0;
@@ -897,9 +1023,22 @@ kme_status kme_restore(kme_engine* e, const char* path) {
         host[k].resize(n);
         ok = n == 0 || std::fread(host[k].data(), 1, n, f) == n;
     }
+    std::vector<char> rec;
+    if (ok && v2) {
+        uint64_t an = 0;
+        ok = std::fread(&an, sizeof an, 1, f) == 1 && an < (1ull << 40);
+        if (ok) {
+            rec.resize(an);
+            ok = an == 0 || std::fread(rec.data(), 1, an, f) == an;
+        }
+    }
     ok = ok && std::fgetc(f) == EOF;   // nothing after the last blob
     std::fclose(f);
-    if (!ok) return KME_E_INVALID;
+    if (!ok) {
+        if (app_bytes) *app_bytes = 0;
+        return KME_E_INVALID;
+    }
+    if (app_bytes) *app_bytes = rec.size();
     // from here on a failure leaves a mix of old and restored state: the engine is dead
     for (size_t k = 0; k < blobs.size(); ++k) {
         if (hipMemcpy(blobs[k].dev, host[k].data(), blobs[k].bytes, hipMemcpyHostToDevice) != hipSuccess) {
@@ -921,7 +1060,18 @@ kme_status kme_restore(kme_engine* e, const char* path) {
     }
     HIP_TRY(hipMemcpy(e->S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
     e->seq_base = h.seq_base;
+    if (rec.size()) std::memcpy(app, rec.data(), rec.size());
     return KME_OK;
+}
+
+kme_status kme_restore(kme_engine* e, const char* path) {
+    size_t n = 0;
+    kme_status s = kme_restore_app(e, path, nullptr, 0, &n);
+    if (s == KME_E_CAPACITY) {   // (an application record this caller does not want)
+        std::vector<char> sink(n);
+        s = kme_restore_app(e, path, sink.data(), sink.size(), &n);
+    }
+    return s;
 }
 
 kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,

@@ -68,13 +68,15 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_top_of_book_groups", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
+    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_checkpoint_app", "kme_restore_app", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
     "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_expand_rows_mt", "kme_build_id",
     "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
     "kme_credit_adjust", "kme_credit_rebalance",
+    "kme_multi_create", "kme_multi_destroy", "kme_multi_submit_epoch_host", "kme_multi_poll", "kme_multi_wait",
+    "kme_multi_checkpoint_app", "kme_multi_restore_app", "kme_multi_engine",
 ]
 
 _lib = None
@@ -120,6 +122,8 @@ def lib():
                                       C.POINTER(C.c_size_t)]),
         "kme_checkpoint": (st, [vp, C.c_char_p]),
         "kme_restore": (st, [vp, C.c_char_p]),
+        "kme_checkpoint_app": (st, [vp, C.c_char_p, vp, C.c_size_t]),
+        "kme_restore_app": (st, [vp, C.c_char_p, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
         "kme_shard_of": (u32, [i64, u32]),
@@ -153,6 +157,14 @@ def lib():
         "kme_credit_state": (st, [vp, vp]),
         "kme_credit_adjust": (st, [vp, vp, u32, u32]),
         "kme_credit_rebalance": (st, [vp, vp]),
+        "kme_multi_create": (st, [C.POINTER(kme_config), u32, vp, C.POINTER(vp)]),
+        "kme_multi_destroy": (st, [vp]),
+        "kme_multi_submit_epoch_host": (st, [vp, C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result)]),
+        "kme_multi_poll": (st, [vp, C.POINTER(C.c_int)]),
+        "kme_multi_wait": (st, [vp, C.POINTER(kme_epoch_status)]),
+        "kme_multi_checkpoint_app": (st, [vp, C.c_char_p, vp, C.c_size_t]),
+        "kme_multi_restore_app": (st, [vp, C.c_char_p, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
+        "kme_multi_engine": (st, [vp, u32, C.POINTER(vp)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -395,6 +407,27 @@ class Engine:
         rc = self._L.kme_restore(self._h, str(path).encode())
         if rc:
             raise KmeError(rc, "kme_restore")
+
+    def checkpoint_app(self, path: str, app: bytes):
+        """kme_checkpoint_app: the state plus an application record (bytes), written atomically."""
+        buf = C.create_string_buffer(bytes(app), max(1, len(app)))
+        rc = self._L.kme_checkpoint_app(self._h, str(path).encode(), buf, len(app))
+        if rc:
+            raise KmeError(rc, "kme_checkpoint_app")
+
+    def restore_app(self, path: str) -> bytes:
+        """kme_restore_app: restores the state and returns the application record."""
+        n = C.c_size_t(0)
+        rc = self._L.kme_restore_app(self._h, str(path).encode(), None, 0, C.byref(n))
+        if rc == 2:   # KME_E_CAPACITY: the record's size is known now
+            buf = C.create_string_buffer(max(1, n.value))
+            rc = self._L.kme_restore_app(self._h, str(path).encode(), buf, n.value, C.byref(n))
+            if rc:
+                raise KmeError(rc, "kme_restore_app")
+            return buf.raw[:n.value]
+        if rc:
+            raise KmeError(rc, "kme_restore_app")
+        return b""
 
     def tape_json_device_into(self, ptrs: dict, n: int, out_ptr: int, cap: int) -> int:
         """kme_tape_json_device into a caller device buffer; returns the text length (nothing is

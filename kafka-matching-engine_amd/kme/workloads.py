@@ -174,11 +174,12 @@ def exchange_test(n_events: int = 100_000, seed: int = 1, num_accounts: int = 10
             create_buy_sell(BUY)
         elif 335 < e <= 667:
             create_buy_sell(SELL)
-        else:  # createCancel (:97-104)
+        else:  # createCancel (:97-104): Math.random() is drawn even when there is no order (:99)
+            r = R.random()
             if not live:
                 create_order(CANCEL, 0, 0, 0, 0, 0)
             else:
-                j = math.floor(R.random() * len(live))
+                j = math.floor(r * len(live))
                 key = live[j]
                 create_order(CANCEL, key, orders[key], 0, 0, 0, True)
                 del orders[key]

@@ -38,5 +38,6 @@ struct JNINativeInterface_ {
     void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
     void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
     jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
+    jobject (*NewDirectByteBuffer)(JNIEnv* env, void* address, jlong capacity);
 };
 #endif

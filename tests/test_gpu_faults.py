@@ -332,3 +332,62 @@ def test_checkpoint_after_an_unfunded_refusal(kme_mod, oracle_mod, tmp_path):
         o.process(part)
     assert got == o.tape_text()
     assert b.snapshot_books() == o.dump_books()
+
+
+def test_fault_at_record_zero_of_an_unproven_epoch(kme_mod, oracle_mod):
+    """Advisor (round 3): at index 0 the error word orders by detail, and KME_D_UNPROVEN is the largest,
+    so a fault of record 0 itself is reported instead of the refusal.  That is the reference's outcome
+    (it throws at record 0 whatever the ledger holds): status DOMAIN at index 0, nothing takes
+    effect, and the engine is failed as after any domain fault."""
+    n_sym, n_acc = 16, 8
+    setup, big, topup = _unprovable(n_sym, n_acc)
+    bad = _inject(big, 0, (W.BUY, 99_999_999, 3, 5, 101, 3))            # record 0: FUNDED_RANGE
+    eng = kme_mod.Engine(_funded_cfg(kme_mod, n_sym + 1, accounts=n_acc))
+    eng.process(setup)
+    books = eng.snapshot_books()
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.process(bad)
+    assert kme_mod.STATUS[ke.value.status] == "DOMAIN" and ke.value.detail == 9
+    assert ke.value.index == 0 and ke.value.n_effective == 0
+    assert eng.snapshot_books() == books
+    with pytest.raises(kme_mod.KmeError) as ke2:
+        eng.process(topup)
+    assert kme_mod.STATUS[ke2.value.status] == "FAILED"
+
+
+def test_host_epoch_refuses_a_short_trades_buffer_and_overlapping_registrations(kme_mod):
+    """Advisor (round 3): a host epoch whose trades buffer holds fewer than max_trades records is
+    refused at submit (the device may commit more trades than it could take), the engine stays
+    usable; registering a range that shares a page with another registered range is refused, the
+    same range twice is counted, and only the registering engine undoes a registration."""
+    n_sym = 8
+    E = 1 << 12
+    cfg = _funded_cfg(kme_mod, n_sym + 1, accounts=16, E=E, P=1 << 14, max_trades=2 * E)
+    eng = kme_mod.Engine(cfg)
+    eng.process(W.funded_setup(16, range(1, n_sym + 1)))
+    stream = W.uniform(E, n_symbols=n_sym, n_accounts=16, seed=4)
+    cols = {k: np.ascontiguousarray(getattr(stream, k)) for k in ("action", "oid", "aid", "sid", "price", "size")}
+    short = kme_mod.new_result(E, 2 * E - 1)
+    with pytest.raises(kme_mod.KmeError) as ke:
+        eng.submit_host(cols, E, short)
+    assert kme_mod.STATUS[ke.value.status] == "INVALID"
+    full = kme_mod.new_result(E, 2 * E)
+    eng.submit_host(cols, E, full)
+    st = eng.wait()
+    assert st.status == 0 and full.trade_off[E] == st.n_trades
+    # registrations: page-granular ownership
+    raw = np.zeros(3 * 4096, np.uint8)
+    base = (-raw.ctypes.data) % 4096
+    a = raw[base:base + 100]
+    b = raw[base + 200:base + 300]                       # the same page as a
+    eng.host_register(a)
+    eng.host_register(a)                                 # counted
+    with pytest.raises(kme_mod.KmeError):
+        eng.host_register(b)
+    eng.host_unregister(a)
+    eng.host_unregister(a)
+    with pytest.raises(kme_mod.KmeError):
+        eng.host_unregister(a)                           # no longer registered by this engine
+    eng.host_register(b)                                 # the page is free again
+    eng.host_unregister(b)
+    eng.close()

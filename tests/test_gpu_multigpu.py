@@ -121,3 +121,77 @@ def test_credit_resplit_keeps_every_epoch_parallel(kme_mod, oracle_mod, rebalanc
     o = oracle_mod.Oracle()
     o.process(allin)
     assert "".join(chunks[i] for i in range(len(allin))) == o.tape_text()
+
+
+def test_rebalance_of_a_failed_engine_still_takes_part(kme_mod):
+    """Advisor (round 3): kme_credit_rebalance is a collective; a rank whose engine failed must still
+    join the all-gather (else its peers wait forever) and every rank must skip the adjust.  One rank
+    here: the call returns KME_E_FAILED instead of returning before the collective, and the
+    communicator still works afterwards (a market-data all-gather completes)."""
+    import os
+
+    import torch
+
+    trccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if os.path.exists(trccl):
+        os.environ.setdefault("KME_RCCL_LIB", trccl)
+    n_sym, n_acc = 8, 16
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    body = W.uniform(2000, n_symbols=n_sym, n_accounts=n_acc, seed=3)
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=1 << 13, max_resting=1 << 14,
+                                 max_accounts=n_acc)
+    eng = kme_mod.Engine(cfg)
+    eng.process(setup)
+    eng.process(body)
+    comm = eng.comm_init(1, 0, kme_mod.comm_unique_id())
+    comm.credit_rebalance()                                       # healthy: OK
+    with pytest.raises(kme_mod.KmeError):                        # REMOVE_SYMBOL of a non-empty book: fatal
+        eng.process(W.Orders.from_rows([(W.REMOVE_SYMBOL, 0, 0, 3, 0, 0)]))
+    with pytest.raises(kme_mod.KmeError) as ke:
+        comm.credit_rebalance()
+    assert kme_mod.STATUS[ke.value.status] == "FAILED"
+    groups = torch.arange(1, n_sym + 1, dtype=torch.int32, device="cuda")
+    allv = torch.zeros((n_sym, 4), dtype=torch.int32, device="cuda")
+    comm.market_data_allgather(groups.data_ptr(), n_sym, n_sym, allv.data_ptr())
+    torch.cuda.synchronize()
+    comm.close()
+
+
+def test_credit_state_marks_absent_accounts(kme_mod):
+    """Advisor (round 3): an account a shard does not hold reports demand -1, and the re-split gives
+    it nothing there: the pooled bound goes to the shards that hold it, none of it is lost."""
+    import torch
+
+    n_acc = 8
+    cfgs = []
+    engines = []
+    for k in range(2):
+        cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=5, max_epoch=1 << 10, max_resting=1 << 12,
+                                     max_accounts=n_acc)
+        cfg.credit_shards = 2
+        cfgs.append(cfg)
+        engines.append(kme_mod.Engine(cfg))
+    # account 3 exists on shard 0 only (its CREATE_BALANCE reached one shard), with 1000 of credit
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc) if a != 3]
+    rows += [(W.TRANSFER, 0, a, 0, 0, 1000) for a in range(n_acc) if a != 3]
+    both = W.Orders.from_rows(rows)
+    engines[0].process(W.Orders.concat([both, W.Orders.from_rows([(W.CREATE_BALANCE, 0, 3, 0, 0, 0),
+                                                                  (W.TRANSFER, 0, 3, 0, 0, 1000)])]))
+    engines[1].process(both)
+    state = torch.zeros((2, 2, n_acc), dtype=torch.int64, device="cuda")
+    for k, e in enumerate(engines):
+        e.credit_state(state[k].data_ptr())
+    torch.cuda.synchronize()
+    assert int(state[1, 1, 3]) == -1 and int(state[1, 0, 3]) == 0
+    assert int(state[0, 1, 3]) == 0 and int(state[0, 0, 3]) == 500            # floor(1000 / 2) booked
+    pooled = state[:, 0].sum(0).clone()
+    for k, e in enumerate(engines):
+        e.credit_adjust(state.data_ptr(), 2, k)
+    after = torch.zeros_like(state)
+    for k, e in enumerate(engines):
+        e.credit_state(after[k].data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(after[:, 0].sum(0), pooled)                          # nothing leaves the pool
+    assert int(after[0, 0, 3]) == 500 and int(after[1, 0, 3]) == 0
+    for e in engines:
+        e.close()

@@ -145,6 +145,7 @@ def test_order_fields_used_exist_with_compatible_types():
 
 _JNI_TYPES = {"int": "jint", "long": "jlong", "String": "jstring", "ByteBuffer": "jobject", "long[]": "jlongArray",
               "void": "void"}
+_JNI_RET = dict(_JNI_TYPES, ByteBuffer="jobject")
 
 
 def test_native_methods_match_the_jni_glue():
@@ -152,13 +153,13 @@ def test_native_methods_match_the_jni_glue():
     with open(JNI_C) as f:
         c = f.read()
     natives = re.findall(r"\bstatic\s+native\s+([\w\[\]]+)\s+(\w+)\s*\(([^)]*)\)\s*;", src)
-    assert {n for _, n, _ in natives} >= {"create", "destroy", "bind", "submit", "poll", "complete", "statusText",
-                                          "checkpoint", "restore"}
+    assert {n for _, n, _ in natives} >= {"create", "destroy", "buffer", "submit", "poll", "complete", "forwarded",
+                                          "statusText", "checkpoint", "restore"}
     for ret, name, params in natives:
         m = re.search(r"JNIEXPORT\s+(\w+)\s+JNICALL\s+Java_GpuMatchingEngine_" + name + r"\s*\(([^)]*)\)", c)
         assert m, f"native {name} has no Java_GpuMatchingEngine_{name} in kme_jni.c"
         jret, jparams = m.group(1), [p.strip() for p in m.group(2).split(",")]
-        assert jret == _JNI_TYPES[ret.replace("String", "String")] or (ret == "String" and jret == "jstring"), name
+        assert jret == _JNI_RET[ret], name
         assert jparams[0].startswith("JNIEnv") and jparams[1].startswith("jclass"), name
         jtypes = [p.split()[0] for p in jparams[2:]]
         jtypes_java = [_JNI_TYPES[p.split()[0]] for p in params.split(",") if p.strip()]
@@ -197,3 +198,89 @@ def test_java_source_is_balanced():
             depth += (ch == o) - (ch == c)
             assert depth >= 0
         assert depth == 0, o + c
+
+
+# kafka-streams 2.3.0's interfaces the commit hook implements (not vendored: their abstract methods)
+_STATE_STORE = {"name": "String", "init": "void", "flush": "void", "close": "void", "persistent": "boolean",
+                "isOpen": "boolean"}
+_STORE_BUILDER = {"withCachingEnabled", "withCachingDisabled", "withLoggingEnabled", "withLoggingDisabled", "build",
+                  "logConfig", "loggingEnabled", "name"}
+
+
+def _class_body(src: str, name: str) -> str:
+    m = re.search(r"class\s+" + name + r"\b[^{]*\{", src)
+    assert m, name
+    depth, i = 1, m.end()
+    while depth:
+        depth += (src[i] == "{") - (src[i] == "}")
+        i += 1
+    return src[m.end():i - 1]
+
+
+def _method_body(src: str, name: str) -> str:
+    m = re.search(r"\b" + name + r"\s*\([^)]*\)\s*(?:throws[^{]*)?\{", src)
+    assert m, name
+    depth, i = 1, m.end()
+    while depth:
+        depth += (src[i] == "{") - (src[i] == "}")
+        i += 1
+    return src[m.end():i - 1]
+
+
+def test_commit_hook_is_a_state_store_whose_flush_is_the_commit_point():
+    """Kafka Streams flushes a task's state stores before it commits the consumed offsets: the hook's
+    flush() must run the processor's commit point, which drains every epoch and checkpoints."""
+    src = _java()
+    assert re.search(r"import\s+org\.apache\.kafka\.streams\.processor\.StateStore\s*;", src)
+    assert re.search(r"import\s+org\.apache\.kafka\.streams\.state\.StoreBuilder\s*;", src)
+    hook = _class_body(src, "CommitHook")
+    assert re.search(r"class\s+CommitHook\s+implements\s+StateStore\b", src)
+    for m, ret in _STATE_STORE.items():
+        assert re.search(r"public\s+" + ret + r"\s+" + m + r"\s*\(", hook), f"StateStore.{m}"
+    assert re.search(r"public\s+void\s+init\s*\(\s*ProcessorContext\s+\w+\s*,\s*StateStore\s+\w+\s*\)", hook)
+    assert "context.register(root" in hook                     # a store registers itself at init
+    assert re.search(r"owner\.commitPoint\(\)", _method_body(hook, "flush"))
+    builder = _class_body(src, "CommitHookBuilder")
+    assert re.search(r"class\s+CommitHookBuilder\s+implements\s+StoreBuilder\s*<\s*CommitHook\s*>", src)
+    for m in _STORE_BUILDER:
+        assert re.search(r"\b" + m + r"\s*\(", builder), f"StoreBuilder.{m}"
+    assert re.search(r"public\s+static\s+StoreBuilder\s*<\s*CommitHook\s*>\s+commitHook\s*\(\s*\)", src)
+    cp = _method_body(src, "commitPoint")
+    # submit the partly filled epoch, complete the ones in flight WITHOUT forwarding, then checkpoint
+    assert "flush()" in cp and "completeOldest(false)" in cp
+    assert re.search(r"checkpoint\(h,\s*checkpointFile\.getPath\(\),\s*lastOffset\)", cp)
+    assert "forwardReady" not in cp and "context.forward" not in cp
+
+
+def test_restart_restores_and_skips_what_the_checkpoint_holds():
+    src = _java()
+    init = _method_body(src, "init")
+    assert "context.getStateStore(COMMIT_STORE)" in init
+    assert re.search(r"restore\(h,\s*checkpointFile\.getPath\(\),\s*\w+\)", init)
+    assert re.search(r"skipThrough\s*=", init)
+    assert "context.stateDir()" in init and "context.taskId()" in init
+    proc = _method_body(src, "process")
+    # restored rows go out first; re-delivered records at or below the checkpoint's offset are dropped
+    assert proc.index("forwardReady()") < proc.index("context.offset()")
+    assert re.search(r"if\s*\(\s*offset\s*<=\s*skipThrough\s*\)\s*return\s*;", proc)
+    assert re.search(r"lastOffset\s*=\s*offset\s*;", proc)
+    close = _method_body(src, "close")
+    assert "commitPoint()" in close and close.index("completeOldest(true)") < close.index("commitPoint()")
+    # no per-epoch commit request: every commit runs the commit point (a full checkpoint)
+    assert "context.commit()" not in src
+
+
+def test_default_configuration_covers_the_c3_universe():
+    """The default processor must take BASELINE C3's sids 1..65,536 (|sid| < max_symbols, kme.h)."""
+    src = _java()
+    m = re.search(r"public\s+GpuMatchingEngine\s*\(\s*\)\s*\{\s*(?://[^\n]*\s*)*this\(([^;]*)\);", _java_raw())
+    assert m
+    args = [a.strip() for a in m.group(1).replace("\n", " ").split(",")]
+    assert int(args[4]) >= 65537
+    assert "KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK" in args[3]
+    assert src.count("ledgerCapacity") >= 3
+
+
+def _java_raw():
+    with open(JAVA) as f:
+        return f.read()

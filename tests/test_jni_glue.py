@@ -3,10 +3,12 @@
 There is no JDK in this image, so libkme_jni_check.so is kme_jni.c built against
 tests/jni_stub/jni.h, and the JNIEnv it receives is a function table made here with ctypes: Java
 arrays and direct ByteBuffers are numpy arrays, exceptions are recorded.  The GPU tests drive the
-processor's own protocol -- bind two slots of direct buffers, submit an epoch per slot, poll,
-complete the oldest (kme_submit_epoch_host / kme_poll / kme_wait / kme_expand_rows) -- and compare
-the MatchOut rows with the oracle's tape record by record ("IN", maker fill, taker fill ..., "OUT";
-KP:97, 265-274, 124), including the rows of the records before a fault.
+processor's own protocol -- two slots of direct buffers over the glue's registered memory, an epoch
+submitted per slot, poll, complete the oldest (kme_submit_epoch_host / kme_poll / kme_wait /
+kme_expand_rows) -- and compare the MatchOut rows with the oracle's tape record by record ("IN",
+maker fill, taker fill ..., "OUT"; KP:97, 265-274, 124), including the rows of the records before a
+fault, and the commit / restart contract: a crash after a commit point, a restart
+from its checkpoint, re-delivery from the committed offset.
 """
 import ctypes as C
 import os
@@ -20,7 +22,8 @@ from kme import workloads as W
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
 CHECK_LIB = os.path.join(ROOT, "integration", "jni", "libkme_jni_check.so")
-SYMBOLS = ["create", "destroy", "bind", "submit", "poll", "complete", "statusText", "checkpoint", "restore"]
+SYMBOLS = ["create", "destroy", "buffer", "submit", "poll", "complete", "forwarded", "statusText", "checkpoint",
+           "restore"]
 ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
                       ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
 assert ROW_DTYPE.itemsize == 48
@@ -46,6 +49,7 @@ class FakeJni:
             ("ReleaseStringUTFChars", C.CFUNCTYPE(V, P, P, P), lambda env, s, p: None),
             ("GetDirectBufferAddress", C.CFUNCTYPE(P, P, P), lambda env, b: self.objs[b].ctypes.data),
             ("GetDirectBufferCapacity", C.CFUNCTYPE(L, P, P), lambda env, b: self.objs[b].nbytes),
+            ("NewDirectByteBuffer", C.CFUNCTYPE(P, P, P, L), self._new_direct),
         ]
 
         class Table(C.Structure):
@@ -66,6 +70,10 @@ class FakeJni:
 
     def _set_long(self, env, a, start, n, buf):
         self.objs[a][start:start + n] = np.ctypeslib.as_array(buf, shape=(n,))
+
+    def _new_direct(self, env, addr, cap):
+        """ByteBuffer over native memory: a uint8 view of it."""
+        return self._new(np.ctypeslib.as_array((C.c_uint8 * cap).from_address(addr)))
 
     def _utf(self, env, s, c):
         b = C.create_string_buffer(self.objs[s].encode())
@@ -89,11 +97,17 @@ def _lib():
         pytest.skip("integration/jni/libkme_jni_check.so not built (make -C kafka-matching-engine_amd/csrc)")
     lib = C.CDLL(CHECK_LIB)
     P, I, L = C.c_void_p, C.c_int32, C.c_int64
-    lib.Java_GpuMatchingEngine_create.argtypes = [P, P, I, I, I, L, I, I, I, I]
+    lib.Java_GpuMatchingEngine_create.argtypes = [P, P, I, I, I, L, I, I, I, I, I, L]
     lib.Java_GpuMatchingEngine_create.restype = L
     lib.Java_GpuMatchingEngine_destroy.argtypes = [P, P, L]
-    lib.Java_GpuMatchingEngine_bind.argtypes = [P, P, L, I] + [P] * 7
-    lib.Java_GpuMatchingEngine_bind.restype = I
+    lib.Java_GpuMatchingEngine_buffer.argtypes = [P, P, L, I, I]
+    lib.Java_GpuMatchingEngine_buffer.restype = P
+    lib.Java_GpuMatchingEngine_forwarded.argtypes = [P, P, L, I]
+    lib.Java_GpuMatchingEngine_forwarded.restype = None
+    lib.Java_GpuMatchingEngine_checkpoint.argtypes = [P, P, L, P, L]
+    lib.Java_GpuMatchingEngine_checkpoint.restype = I
+    lib.Java_GpuMatchingEngine_restore.argtypes = [P, P, L, P, P]
+    lib.Java_GpuMatchingEngine_restore.restype = I
     lib.Java_GpuMatchingEngine_submit.argtypes = [P, P, L, I, I]
     lib.Java_GpuMatchingEngine_submit.restype = I
     lib.Java_GpuMatchingEngine_poll.argtypes = [P, P, L]
@@ -118,8 +132,26 @@ def test_jni_glue_exports_and_cpu_paths():
     txt = lib.Java_GpuMatchingEngine_statusText(j.env, None, 4)
     assert "UNFUNDED" in j.objs[txt].upper() or "fund" in j.objs[txt].lower()
     # an invalid configuration throws IllegalStateException before touching the device
-    assert lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 0, 1 << 16, 1 << 16, 256, 0, 0) == 0
+    assert lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 0, 1 << 16, 1 << 16, 256, 0, 0, 1, 1 << 16) == 0
     assert j.thrown and "maxEpoch" in j.thrown[0]
+
+
+COLUMNS = (("action", np.int32), ("oid", np.int64), ("aid", np.int64), ("sid", np.int64), ("price", np.int32),
+           ("size", np.int32))
+
+
+def slot_views(lib, j, h):
+    """GpuMatchingEngine.init's buffer() calls: per slot the six columns and the rows, as views."""
+    cols, rows = [], []
+    for slot in range(2):
+        views = {}
+        for c, (name, dt) in enumerate(COLUMNS):
+            views[name] = j.objs[lib.Java_GpuMatchingEngine_buffer(j.env, None, h, slot, c)].view(dt)
+        cols.append(views)
+        rows.append(j.objs[lib.Java_GpuMatchingEngine_buffer(j.env, None, h, slot, 6)].view(ROW_DTYPE))
+    for v in cols[0].values():
+        assert v.ctypes.data % 4096 == 0            # page-aligned: no registration shares a page
+    return cols, rows
 
 
 class Proc:
@@ -128,18 +160,9 @@ class Proc:
 
     def __init__(self, lib, j, h, epoch, max_trades):
         self.lib, self.j, self.h, self.epoch = lib, j, h, epoch
-        self.cols, self.rows = [], []
-        for slot in range(2):
-            bufs, views = [], {}
-            for name, dt in (("action", np.int32), ("oid", np.int64), ("aid", np.int64), ("sid", np.int64),
-                             ("price", np.int32), ("size", np.int32)):
-                b, v = j.direct(epoch * np.dtype(dt).itemsize, dt)
-                bufs.append(b)
-                views[name] = v
-            rb, rv = j.direct(48 * (2 * epoch + 2 * max_trades), ROW_DTYPE)
-            assert lib.Java_GpuMatchingEngine_bind(j.env, None, h, slot, *bufs, rb) == 0
-            self.cols.append(views)
-            self.rows.append(rv)
+        self.cols, self.rows = slot_views(lib, j, h)
+        assert all(len(v) == epoch for v in self.cols[0].values())
+        assert len(self.rows[0]) == 2 * epoch + 2 * max_trades
         self.status = j.arr(np.zeros(4, np.int64))
         self.pending = []          # (slot, n) in submission order
 
@@ -154,7 +177,9 @@ class Proc:
         slot = self.pending.pop(0)
         m = self.lib.Java_GpuMatchingEngine_complete(self.j.env, None, self.h, slot, self.status)
         assert not self.j.thrown, self.j.thrown
-        return self.rows[slot][:m].copy(), self.j.objs[self.status].copy()
+        out = self.rows[slot][:m].copy(), self.j.objs[self.status].copy()
+        self.lib.Java_GpuMatchingEngine_forwarded(self.j.env, None, self.h, slot)
+        return out
 
 
 def _as_tape(rows, rec_dtype):
@@ -187,11 +212,11 @@ def test_jni_epochs_in_flight_equal_oracle_tape(oracle_mod, mode):
         setup = W.funded_setup(256, range(1, 65))
         orders = W.Orders.concat([setup, W.uniform(40_000, n_symbols=64, n_accounts=256, seed=11)])
         # default processor flags: the exact ledger, serial fallback where the proof fails
-        h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 1 << 13, 1 << 16, 1 << 15, 256, 3, 0)
+        h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 65, 1 << 13, 1 << 16, 1 << 15, 256, 3, 0, 1, 1 << 16)
         epoch, max_trades = 1 << 13, 1 << 15
     else:
         orders = W.exchange_test(6_000, seed=5)
-        h = lib.Java_GpuMatchingEngine_create(j.env, None, 0, 8, 1 << 12, 1 << 14, 1 << 14, 0, 0, 0)
+        h = lib.Java_GpuMatchingEngine_create(j.env, None, 0, 8, 1 << 12, 1 << 14, 1 << 14, 0, 0, 0, 1, 1 << 16)
         epoch, max_trades = 1 << 12, 1 << 14
     assert h and not j.thrown, j.thrown
     p = Proc(lib, j, h, epoch, max_trades)
@@ -228,7 +253,7 @@ def test_jni_forwards_the_records_before_a_fault(oracle_mod):
     body = W.uniform(3000, n_symbols=8, n_accounts=16, seed=2)
     bad = W.Orders.from_rows([(W.REMOVE_SYMBOL, 0, 0, 3, 0, 0)])
     orders = W.Orders.concat([body.slice(0, 2000), bad, body.slice(2000, 3000)])
-    h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 9, 1 << 13, 1 << 14, 1 << 14, 16, 0, 0)
+    h = lib.Java_GpuMatchingEngine_create(j.env, None, 1, 9, 1 << 13, 1 << 14, 1 << 14, 16, 0, 0, 1, 1 << 16)
     assert h
     p = Proc(lib, j, h, 1 << 13, 1 << 14)
     p.submit(0, setup)
@@ -243,3 +268,315 @@ def test_jni_forwards_the_records_before_a_fault(oracle_mod):
     o.process(orders.slice(0, 2000))
     _cmp_fields(_as_tape(rows, oracle_mod.REC_DTYPE), o.tape())
     lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
+
+
+class JavaProcessor:
+    """GpuMatchingEngine.java statement for statement (init / process / flush / completeOldest /
+    forwardReady / punctuate / commitPoint / close) over the JNI glue.  Each record carries its Kafka
+    offset (context.offset()); forwarded rows are collected in `out`; commit_point() is the commit
+    hook's StateStore.flush(), which Kafka Streams calls before it commits the consumed offsets."""
+
+    def __init__(self, lib, j, path, epoch, max_trades, create_args):
+        self.lib, self.j, self.path, self.epoch = lib, j, str(path), epoch
+        self.h = lib.Java_GpuMatchingEngine_create(j.env, None, *create_args)
+        assert self.h and not j.thrown, j.thrown
+        self.cols, self.rows = slot_views(lib, j, self.h)
+        self.count, self.busy, self.fill, self.oldest, self.inflight = [0, 0], [False, False], 0, 0, 0
+        self.ready, self.ready_rows = [], [0, 0]
+        self.ready_status = [j.arr(np.zeros(4, np.int64)) for _ in range(2)]
+        self.last_offset = self.skip_through = self.checkpointed = -1
+        self.out = []
+        if os.path.exists(self.path):
+            r = j.arr(np.zeros(6, np.int64))
+            rc = lib.Java_GpuMatchingEngine_restore(j.env, None, self.h, _jstr(j, self.path), r)
+            assert rc == 0, rc
+            o = j.objs[r]
+            self.skip_through = self.checkpointed = self.last_offset = int(o[0])
+            for k in range(int(o[1])):
+                s = int(o[2 + 2 * k])
+                self.ready_rows[s] = int(o[3 + 2 * k])
+                j.objs[self.ready_status[s]][:] = 0
+                self.busy[s] = True
+                self.ready.append(s)
+
+    def process(self, offset, rec):
+        self.forward_ready()
+        if offset <= self.skip_through:
+            return
+        while self.busy[self.fill]:
+            if self.ready:
+                self.forward_ready()
+            else:
+                self.complete_oldest(True)
+        n = self.count[self.fill]
+        for name, v in self.cols[self.fill].items():
+            v[n] = rec[name]
+        self.count[self.fill] = n + 1
+        self.last_offset = offset
+        if self.count[self.fill] == self.epoch:
+            self.flush()
+
+    def flush(self):
+        if self.count[self.fill] == 0:
+            return
+        while self.inflight == 2:
+            self.complete_oldest(True)
+        rc = self.lib.Java_GpuMatchingEngine_submit(self.j.env, None, self.h, self.fill, self.count[self.fill])
+        assert rc == 0, rc
+        if self.inflight == 0:
+            self.oldest = self.fill
+        self.busy[self.fill] = True
+        self.inflight += 1
+        self.fill ^= 1
+
+    def complete_oldest(self, forward):
+        s = self.oldest
+        self.ready_rows[s] = self.lib.Java_GpuMatchingEngine_complete(self.j.env, None, self.h, s, self.ready_status[s])
+        assert not self.j.thrown, self.j.thrown
+        self.ready.append(s)
+        self.inflight -= 1
+        self.oldest = s ^ 1
+        if forward:
+            self.forward_ready()
+
+    def forward_ready(self):
+        while self.ready:
+            s = self.ready.pop(0)
+            self.out.append(self.rows[s][:self.ready_rows[s]].copy())
+            self.lib.Java_GpuMatchingEngine_forwarded(self.j.env, None, self.h, s)
+            self.busy[s] = False
+            self.count[s] = 0
+            assert self.j.objs[self.ready_status[s]][0] == 0
+
+    def punctuate(self):
+        self.forward_ready()
+        while self.inflight > 0:
+            p = self.lib.Java_GpuMatchingEngine_poll(self.j.env, None, self.h)
+            assert p >= 0
+            if p == 0:
+                break
+            self.complete_oldest(True)
+        if self.inflight < 2 and self.count[self.fill] > 0 and not self.busy[self.fill]:
+            self.flush()
+
+    def commit_point(self):
+        if self.h == 0 or self.last_offset == self.checkpointed:
+            return
+        self.flush()
+        while self.inflight > 0:
+            self.complete_oldest(False)
+        rc = self.lib.Java_GpuMatchingEngine_checkpoint(self.j.env, None, self.h, _jstr(self.j, self.path), self.last_offset)
+        assert rc == 0, rc
+        self.checkpointed = self.last_offset
+
+    def close(self):
+        self.forward_ready()
+        self.flush()
+        while self.inflight > 0:
+            self.complete_oldest(True)
+        self.commit_point()
+        self.lib.Java_GpuMatchingEngine_destroy(self.j.env, None, self.h)
+        self.h = 0
+
+    def crash(self):
+        """The JVM dies: nothing more is forwarded, nothing flushed (the native memory goes with it)."""
+        self.lib.Java_GpuMatchingEngine_destroy(self.j.env, None, self.h)
+        self.h = 0
+
+    def rows_out(self):
+        return np.concatenate(self.out) if self.out else np.zeros(0, ROW_DTYPE)
+
+
+def _jstr(j, s):
+    return j._new(s)
+
+
+def _records(orders, k):
+    return {f: getattr(orders, f)[k] for f in ("action", "oid", "aid", "sid", "price", "size")}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,redeliver", [("funded", "committed"), ("funded", "previous"), ("exact", "committed")])
+def test_crash_after_commit_restarts_without_losing_output(oracle_mod, tmp_path, mode, redeliver):
+    """The commit / restart contract (KP:29-49, 125).  Records are taken with their
+    Kafka offsets; two commit points (the commit hook's flush, which Kafka Streams runs before it
+    commits the offsets) leave epochs completed but not forwarded and one partly filled; more records
+    are taken, some forwarded, some buffered, then the process dies.  A new processor restores the
+    checkpoint and Kafka re-delivers from the committed offset ("committed"), or from the commit
+    before it when the last offset commit did not land ("previous": the restored checkpoint is ahead
+    of Kafka, those records are skipped).  The rows forwarded before the commit point plus everything
+    forwarded after the restart are the oracle's uninterrupted tape; what was forwarded between the
+    commit point and the crash comes again, and only that (at least once).  The books (and the exact
+    ledger) at the end equal the oracle's."""
+    lib = _lib()
+    j = FakeJni()
+    if mode == "funded":
+        setup = W.funded_setup(256, range(1, 65))
+        orders = W.Orders.concat([setup, W.uniform(60_000, n_symbols=64, n_accounts=256, seed=23)])
+        epoch, max_trades = 1 << 12, 1 << 14
+        args = (1, 65, epoch, 1 << 16, max_trades, 256, 3, 0, 1, 1 << 16)   # the default flags: exact ledger + fallback
+    else:
+        orders = W.exchange_test(12_000, seed=9)
+        epoch, max_trades = 1 << 11, 1 << 13
+        args = (0, 8, epoch, 1 << 14, max_trades, 0, 0, 0, 1, 1 << 16)
+    n = len(orders)
+    ckpt = tmp_path / "kme-0_0.ckpt"
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    c0, c1, crash_at = int(n * 0.3) + 17, int(n * 0.55) + 5, int(n * 0.8) + 3
+    committed = {}
+    for k in range(crash_at):
+        p.process(k, _records(orders, k))
+        if k % 1500 == 700:
+            p.punctuate()
+        if k in (c0, c1):
+            p.commit_point()
+            committed[k] = sum(len(x) for x in p.out)     # rows forwarded before the commit point
+            assert p.ready or p.count[p.fill] == 0
+    first = p.rows_out()
+    p.crash()
+    q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    assert q.skip_through == c1
+    start = (c1 if redeliver == "committed" else c0) + 1
+    for k in range(start, n):
+        q.process(k, _records(orders, k))
+        if k % 2000 == 1000:
+            q.punctuate()
+    # the books and ledger at the end, read through the engine the glue holds (its first field)
+    eng = C.c_void_p.from_address(q.h).value
+    import kme
+    L = kme.lib()
+    q.forward_ready()
+    q.flush()
+    while q.inflight:
+        q.complete_oldest(True)
+    books = _snapshot(L, L.kme_snapshot_books, eng)
+    ledger = _snapshot(L, L.kme_snapshot_ledger, eng)
+    q.close()
+    second = q.rows_out()
+    F = committed[c1]
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    got = np.concatenate([first[:F], second])
+    _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
+    dup = first[F:]
+    assert len(dup) > 0                                        # something was forwarded after the commit point
+    _cmp_fields(_as_tape(second[:len(dup)], oracle_mod.REC_DTYPE), _as_tape(dup, oracle_mod.REC_DTYPE))
+    assert books == o.dump_books()
+    assert ledger == o.dump_ledger()
+
+
+def _snapshot(L, fn, eng):
+    p = C.c_void_p()
+    n = C.c_size_t(0)
+    assert fn(C.c_void_p(eng), C.byref(p), C.byref(n)) == 0
+    try:
+        return C.string_at(p, n.value).decode()
+    finally:
+        L.kme_free(p)
+
+
+@pytest.mark.gpu
+def test_checkpoint_of_another_processor_is_refused(kme_mod, tmp_path):
+    """restore() takes only checkpoints with the processor's record (a bare kme_checkpoint file is
+    refused), and a file of another geometry leaves the fresh engine untouched."""
+    lib = _lib()
+    j = FakeJni()
+    args = (1, 9, 1 << 10, 1 << 12, 1 << 12, 16, 0, 0, 1, 1 << 12)
+    h = lib.Java_GpuMatchingEngine_create(j.env, None, *args)
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=9, max_epoch=1 << 10,
+                                                max_resting=1 << 12, max_trades=1 << 12, max_accounts=16,
+                                                ledger_capacity=1 << 12))
+    bare = tmp_path / "bare.ckpt"
+    eng.checkpoint(str(bare))
+    r = j.arr(np.zeros(6, np.int64))
+    assert lib.Java_GpuMatchingEngine_restore(j.env, None, h, _jstr(j, str(bare)), r) == 1     # KME_E_INVALID
+    other = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=17, max_epoch=1 << 10,
+                                                  max_resting=1 << 12, max_trades=1 << 12, max_accounts=16))
+    odd = tmp_path / "odd.ckpt"
+    other.checkpoint_app(str(odd), b"x" * 40)
+    assert lib.Java_GpuMatchingEngine_restore(j.env, None, h, _jstr(j, str(odd)), r) == 1
+    assert other.restore_app(str(odd)) == b"x" * 40
+    lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
+    eng.close()
+    other.close()
+
+
+def _drive(p, orders, start=0, end=None, punct=1500):
+    end = len(orders) if end is None else end
+    for k in range(start, end):
+        p.process(k, _records(orders, k))
+        if k % punct == punct // 2:
+            p.punctuate()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crash", [False, True])
+def test_multi_gpu_drop_in_equals_the_single_partition_tape(oracle_mod, tmp_path, crash):
+    """Round-3 verdict: the drop-in over N engines (kme_multi: the router's symbol split, one engine per
+    shard, credit re-split before every epoch, results merged into input order through the router's
+    index).  Four shard engines on GPU 0 (nDevices = -4) behind one processor: its MatchOut rows equal
+    the oracle's single-partition tape (topic.js:17-18, KP:52) -- and across a crash and restart from
+    the commit point (every shard's checkpoint, the router's directory rebuilt from the resting
+    orders) as for one engine."""
+    lib = _lib()
+    j = FakeJni()
+    setup = W.funded_setup(256, range(1, 129))
+    orders = W.Orders.concat([setup, W.uniform(60_000, n_symbols=128, n_accounts=256, seed=31)])
+    epoch, max_trades = 1 << 12, 1 << 14
+    args = (1, 129, epoch, 1 << 16, max_trades, 256, 0, 0, -4, 1 << 12)   # FUNDED, flags 0, 4 shards on GPU 0
+    ckpt = tmp_path / "multi.ckpt"
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    n = len(orders)
+    if not crash:
+        _drive(p, orders)
+        p.close()
+        got = p.rows_out()
+    else:
+        c1, crash_at = int(n * 0.5) + 11, int(n * 0.7) + 5
+        _drive(p, orders, 0, c1 + 1)
+        p.commit_point()
+        F = sum(len(x) for x in p.out)
+        _drive(p, orders, c1 + 1, crash_at)
+        first = p.rows_out()
+        p.crash()
+        q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+        assert q.skip_through == c1
+        _drive(q, orders, c1 + 1, n)
+        q.close()
+        got = np.concatenate([first[:F], q.rows_out()])
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rebalance", [True, False])
+def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, rebalance):
+    """Every account funded with 1.25x its single-engine need over the whole stream, booked as a
+    quarter on each of four shards.  The drop-in re-splits the pooled credit before every epoch, so
+    every epoch stays provable and the tape is the oracle's; with re-splitting off
+    (KME_MULTI_REBALANCE_EVERY=0) some shard's share runs dry and the processor fails (UNFUNDED)."""
+    monkeypatch.setenv("KME_MULTI_REBALANCE_EVERY", "1" if rebalance else "0")
+    lib = _lib()
+    j = FakeJni()
+    n_sym, n_acc, E = 2048, 1024, 1 << 14
+    body = W.uniform(8 * E, n_symbols=n_sym, n_accounts=n_acc, seed=77)
+    risk = np.where(body.action == W.BUY, body.size.astype(np.int64) * body.price,
+                    np.where(body.action == W.SELL, body.size.astype(np.int64) * (100 - body.price.astype(np.int64)), 0))
+    credit = np.floor(np.bincount(body.aid, weights=risk, minlength=n_acc) * 1.25).astype(np.int64)
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
+    rows += [(W.TRANSFER, 0, a, 0, 0, int(credit[a])) for a in range(n_acc)]
+    rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
+    orders = W.Orders.concat([W.Orders.from_rows(rows), body])
+    args = (1, n_sym + 1, E, 1 << 20, 4 * E, n_acc, 0, 0, -4, 1 << 12)
+    p = JavaProcessor(lib, j, tmp_path / "m.ckpt", E, 4 * E, args)
+    if not rebalance:
+        with pytest.raises(AssertionError):        # a shard's epoch refused: status UNFUNDED in the rows' epoch
+            _drive(p, orders, punct=1 << 30)
+            p.close()
+        return
+    _drive(p, orders, punct=1 << 30)
+    p.close()
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    _cmp_fields(_as_tape(p.rows_out(), oracle_mod.REC_DTYPE), o.tape())

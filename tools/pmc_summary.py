@@ -54,6 +54,21 @@ def derived(res):
     return out
 
 
+def build_id_of(d):
+    """kme_build_id() of the library the profiled bench runs loaded: bench.py prints it in its line
+    (one per pass log, <d>/p*.log); None when the passes disagree or none printed one."""
+    ids = set()
+    for f in glob.glob(os.path.join(d, "p*.log")) + glob.glob(os.path.join(d, "*.p*.log")):
+        with open(f) as fh:
+            for line in fh:
+                if line.startswith("{") and '"build_id"' in line:
+                    try:
+                        ids.add(json.loads(line)["build_id"])
+                    except (ValueError, KeyError):
+                        pass
+    return ids.pop() if len(ids) == 1 else None
+
+
 def main():
     d, kre, out = sys.argv[1], sys.argv[2], sys.argv[3]
     skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
@@ -62,7 +77,7 @@ def main():
         if os.path.isdir(sub):
             for k, v in counters(sub, kre).items():
                 allv[k] = v
-    res = {"kernel_regex": kre, "source": os.path.relpath(d)}
+    res = {"kernel_regex": kre, "source": os.path.relpath(d), "build_id": build_id_of(d)}
     # several kernels may match (k_match and k_match_lanes both run once per epoch): the figure per
     # epoch ("per launch" of the match phase) is the sum of each kernel's mean per dispatch
     for k, kerns in sorted(allv.items()):
