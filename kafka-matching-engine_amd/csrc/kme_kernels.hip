@@ -3863,6 +3863,7 @@ __global__ void k_init_state(DevState S) {
         S.grp[k] = gs;
     }
     if (k < (uint32_t)S.A && S.acct_since) S.acct_since[k] = INT64_MAX;
+    if (k == 0) S.ctr[ci(C_ERR)] = ~0ull;   // no epoch yet: nothing faulted (a fresh engine can be checkpointed)
 }
 
 // Per-epoch counters: error = none, the epoch's statistics = 0 (pool bump and table usage persist).
