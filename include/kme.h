@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 5
+#define KME_ABI_VERSION 6
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -83,12 +83,14 @@ enum kme_mode { KME_MODE_EXACT = 0, KME_MODE_FUNDED = 1 };
 
 /* kme_config.flags
  * KME_FLAG_EXACT_LEDGER (FUNDED, SURVEY §8 row f next-2): after the parallel matching of each
- *   epoch, one wavefront replays the epoch's ledger effects in arrival order -- createBalance /
- *   transfer (KP:131-146), checkBalance's reservation and position adjustment (KP:167-182), both
- *   fillOrder calls per trade (KP:276-287) and postRemoveAdjustments (KP:325-333), with the
- *   value-keyed position writes of KP:434-436 -- into device Balances / Positions tables, so the
- *   final ledger stores are bit-exact too (kme_snapshot_ledger).  The replay is a serial chain:
- *   it costs far more than the matching it follows. */
+ *   epoch its ledger effects -- createBalance / transfer (KP:131-146), checkBalance's reservation
+ *   and position adjustment (KP:167-182), both fillOrder calls per trade (KP:276-287) and
+ *   postRemoveAdjustments (KP:325-333), with the value-keyed position writes of KP:434-436 -- are
+ *   applied to device Balances / Positions tables exactly as the reference's arrival order would,
+ *   so the final ledger stores are bit-exact too (kme_snapshot_ledger).  Balances are per-account
+ *   sums and positions per (account, symbol) chains, applied in parallel; chains a value-keyed write
+ *   couples are replayed together in arrival order; an epoch with too many such couplings takes the
+ *   serial replay (kme_epoch_status.ledger_serial).  env KME_LEDGER_SERIAL=1: always serial. */
 #define KME_FLAG_EXACT_LEDGER 1u
 /* KME_FLAG_SERIAL_FALLBACK (FUNDED, requires KME_FLAG_EXACT_LEDGER; SURVEY §8 row f next-2, the
  *   validate-and-replay relaxation): an epoch whose funded proof fails -- some checkBalance
@@ -173,6 +175,10 @@ typedef struct kme_epoch_status {
     uint32_t serial_fallback;   /* epochs (device sub-epochs of kme_submit_epoch) that ran serially
                                    under KME_FLAG_SERIAL_FALLBACK */
     uint32_t n_effective;       /* records of the submission that took effect (= n_inputs when OK) */
+    uint32_t ledger_repaired;   /* KME_FLAG_EXACT_LEDGER: position chains the parallel ledger pass replayed
+                                   in arrival order because a value-keyed write (KP:434-436) reached them */
+    uint32_t ledger_serial;     /* KME_FLAG_EXACT_LEDGER: epochs whose ledger the serial replay applied
+                                   (too many such couplings, or the parallel pass is off) */
 } kme_epoch_status;
 
 typedef struct kme_engine kme_engine;

@@ -89,6 +89,24 @@ KDEV_HOST_INLINE uint32_t tt_ordp(uint32_t ord, int32_t price, bool sneg) {
 
 struct PosEntry { int64_t k0, k1, v0, v1; };   // Positions: UUID(aid,sid) -> UUID(amount,available)
 
+// kme_ledger.hip: one position chain of an epoch (the ops on Positions key (aid, sid)), stored at the
+// sorted position of its first op (aid -1 there: that op is not a chain's first)
+struct LChain {
+    int64_t sid;
+    int64_t ia, iv;                // the entry at the epoch's start (ipres)
+    int64_t fa, fv;                // after the chain's last effect (fpres)
+    int64_t delta;                 // the balance change of its effects
+    uint32_t last_seq;             // arrival number of its last effect
+    uint32_t dirty;                // a value write into it precedes one of its reads (k_ldetect)
+    uint32_t late;                 // 1 + arrival number of the latest value write after its last effect
+    uint32_t rix;                  // 1 + index in k_lrepair's set
+    int32_t aid, islot;            // islot: the entry's table slot at the start (-1: absent)
+    uint8_t ipres, fpres, _p[6];
+};
+static_assert(sizeof(LChain) == 80, "LChain");
+// the ledger pass's counters (DevState::lctr, one line each)
+enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_N = 8 };
+
 // Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
 // counters never contend for one L2 line.
 enum Ctr : int {
@@ -106,6 +124,8 @@ enum Ctr : int {
     C_SIZE0,           // persistent: nonzero once a BUY/SELL of size 0 was submitted (a book may then hold
                        // size-0 makers, and k_match's fast segments -- which read a level's emptiness off
                        // its quantity -- stay off)
+    C_LREPAIRED,       // exact ledger: position chains the parallel pass replayed for value-key couplings
+    C_LSERIAL,         // exact ledger: nonzero = the serial replay applied this epoch's ledger
     C_NCTR = 20
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
@@ -169,6 +189,30 @@ struct DevState {
     KG unsigned long long* tsh;       // TSHARDS x CTR_STRIDE words (TShardWord in each line)
     KG unsigned long long* ctr;       // C_NCTR x CTR_STRIDE words
     KG unsigned long long* dbg;     // diagnostic stamps (KME_STAMPS builds), G x 16 words
+    // FUNDED + exact ledger, applied in parallel (kme_ledger.hip; lpar = 0: the serial replay)
+    int32_t lpar, lpasses;
+    uint32_t lr_cap, le_cap, lx_cap, _lpad;
+    uint64_t lvk_mask;
+    KG uint32_t* lcnt;                // per record: its ops, then their offset
+    KG uint32_t* lscan;               // scan scratch
+    KG uint32_t* lk0;                 // per op (arrival order): sort key aid * 256 + hash8(sid)
+    KG uint32_t* lv0;                 //   and its arrival number
+    KG uint32_t* lkey[2];
+    KG uint32_t* lval[2];
+    KG uint32_t* lghist;
+    KG uint32_t* lop;                 // per arrival number: record | kind << 30
+    KG int64_t* lsid;                 //   and its chain's sid
+    KG LChain* lchain;                // per sorted op
+    KG long4* lvw;                    // per arrival number: a value write (key, value)
+    KG uint32_t* lvw_meta;            //   kind | writer chain << 2
+    KG int32_t* lvw_tgt;              //   the chain it writes into (-1: none)
+    KG uint32_t* lseg;                // per account: its first sorted op
+    KG int64_t* ldelta;               // per account: the epoch's balance change
+    KG ulonglong4* lvk;               // value-key table: hash, 1 + latest arrival, key
+    KG uint32_t* lx;                  // couplings (arrival numbers of the value writes)
+    KG uint32_t* ldirty;              // the chains they write into
+    KG uint32_t* lrscr;               // k_lrepair scratch
+    KG unsigned long long* lctr;      // LC_N x CTR_STRIDE words
 };
 
 struct EpochIO {

@@ -26,27 +26,12 @@
 
 #include "kme.h"
 #include "kme_device.h"
+#include "kme_jarith.h"
 #include "kme_launch.h"
 
 namespace kme {
 
-#define KDEV __device__ __forceinline__
-#define KC __attribute__((address_space(4)))   // constant address space: scalar loads
 
-// ------------------------------------------------------------------ Java arithmetic (wraps)
-KDEV int32_t jiadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
-KDEV int32_t jisub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
-KDEV int32_t jimul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
-KDEV int32_t jineg(int32_t a) { return (int32_t)(0u - (uint32_t)a); }
-KDEV int64_t jladd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
-KDEV int64_t jlsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
-KDEV int64_t jlmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
-KDEV int64_t jlneg(int64_t a) { return (int64_t)(0ull - (uint64_t)a); }
-KDEV int64_t lmax(int64_t a, int64_t b) { return a >= b ? a : b; }
-KDEV int64_t lmin(int64_t a, int64_t b) { return a <= b ? a : b; }
-KDEV int32_t imin(int32_t a, int32_t b) { return a <= b ? a : b; }
-
-KDEV int lane_id() { return (int)(threadIdx.x & 63); }
 
 // Diagnostic build only (-DKME_STAMPS): s_memtime stamps accumulated per category in SGPRs and
 // written to DevState::dbg at the end of k_match (cdna_hip_programming.md §7 "In-kernel stamps").
@@ -86,38 +71,6 @@ KDEV unsigned long long bcast64(unsigned long long v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
     return ((unsigned long long)hi << 32) | lo;
-}
-
-KDEV uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
-
-KDEV uint64_t err_code(int status, int detail, int64_t idx) {
-    uint64_t ix = idx < 0 ? 0xFFFFFFFFFFFFull : (uint64_t)idx;
-    return (ix << 16) | ((uint64_t)(detail & 0xFF) << 8) | (uint64_t)(status & 0xFF);
-}
-KDEV void raise_thread(unsigned long long* ctr, int status, int detail, int64_t idx) {
-    atomicMin(&ctr[ci(C_ERR)], (unsigned long long)err_code(status, detail, idx));
-}
-KDEV void raise_wave(unsigned long long* ctr, int status, int detail, int64_t idx) {
-    // every lane issues the (idempotent) atomicMin: a lane-0 branch here, inside the matching
-    // loops, makes the compiler treat their exits as divergent (uniform state moves to VGPRs)
-    atomicMin(&ctr[ci(C_ERR)], (unsigned long long)err_code(status, detail, idx));
-}
-KDEV bool failed(const unsigned long long* ctr) {
-    return __hip_atomic_load(&ctr[ci(C_ERR)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ~0ull;
-}
-// The records of the epoch that still take effect: every record before the first fault raised so
-// far (the reference forwards and commits each record before the one that throws, KP:97, 124-125);
-// none after a fault of the epoch as a whole (no index: the funded proof, trade capacity).
-KDEV uint32_t err_limit(const unsigned long long* ctr, uint32_t n) {
-    const unsigned long long c = __hip_atomic_load(&ctr[ci(C_ERR)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c == ~0ull) return n;
-    const unsigned long long ix = c >> 16;
-    if (ix == 0xFFFFFFFFFFFFull) return 0;
-    return ix < n ? (uint32_t)ix : n;
 }
 
 // ------------------------------------------------------------------ the book bit scans (KP:359-416)
@@ -670,23 +623,28 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
 constexpr int RADIX_DIGITS = 1 << RADIX_BITS;
 constexpr int RADIX_PER_T = RADIX_DIGITS / 256;   // digits per thread of a 256-thread block
 
-KDEV uint32_t radix_key(const DevState& S, int pass, int src, uint32_t k) {
-    if (pass == 0) { const int32_t g = S.route_grp[k]; return g < 0 ? (uint32_t)S.G : (uint32_t)g; }
-    return (src ? S.rkeys[1] : S.rkeys[0])[k];
+KDEV uint32_t radix_key(const RadixIO& R, int pass, int src, uint32_t k) {
+    if (pass == 0) { const int32_t g = R.key0[k]; return g < 0 ? R.none : (uint32_t)g; }
+    return R.keys[src][k];
+}
+KDEV uint32_t radix_n(const RadixIO& R) {
+    if (!R.n_dev) return R.n;
+    const uint32_t d = (uint32_t)*R.n_dev;
+    return d < R.n ? d : R.n;
 }
 
-__global__ void __launch_bounds__(256) k_radix_hist(DevState S, EpochIO io, int pass, int src) {
+__global__ void __launch_bounds__(256) k_radix_hist(RadixIO R, int pass, int src) {
     __shared__ uint32_t h[RADIX_DIGITS];
     const int t = threadIdx.x;
     for (int q = 0; q < RADIX_PER_T; ++q) h[t + 256 * q] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * RADIX_TILE;
+    const uint32_t base = blockIdx.x * RADIX_TILE, n = radix_n(R);
     for (int j = 0; j < RADIX_TILE / 256; ++j) {
         const uint32_t k = base + j * 256 + t;
-        if (k < io.n) atomicAdd(&h[(radix_key(S, pass, src, k) >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1)], 1u);
+        if (k < n) atomicAdd(&h[(radix_key(R, pass, src, k) >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1)], 1u);
     }
     __syncthreads();
-    for (int q = 0; q < RADIX_PER_T; ++q) S.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
+    for (int q = 0; q < RADIX_PER_T; ++q) R.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
 }
 
 KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
@@ -698,7 +656,7 @@ KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
 // round, lane) and counts its digits in its own LDS row round by round (match-any over the digit
 // bits; the first lane of each digit adds the run), so the only block barriers are the few
 // between the counting, the per-digit offsets and the placement.
-__global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, int pass, int src) {
+__global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int src) {
     static_assert(RADIX_DIGITS == 512, "two digits per thread");
     static_assert(RADIX_TILE % 256 == 0, "whole rounds");
     __shared__ uint32_t wh[4][RADIX_DIGITS];     // wavefront w's count of digit d, then its first local slot
@@ -706,7 +664,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
     __shared__ uint32_t lkey[RADIX_TILE], lval[RADIX_TILE];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t base = blockIdx.x * RADIX_TILE;
+    const uint32_t base = blockIdx.x * RADIX_TILE, n = radix_n(R);
     const int dst = src ^ 1;
     const int shift = RADIX_BITS * pass;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -717,9 +675,9 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
     for (int j = 0; j < RJ; ++j) {
         const uint32_t k = base + w * WCH + j * 64 + lane;
         keys[j] = 0; vals[j] = 0;
-        if (k < io.n) {
-            keys[j] = radix_key(S, pass, src, k);
-            vals[j] = pass == 0 ? k : (src ? S.rvals[1] : S.rvals[0])[k];
+        if (k < n) {
+            keys[j] = radix_key(R, pass, src, k);
+            vals[j] = pass == 0 ? (R.val0 ? R.val0[k] : k) : R.vals[src][k];
         }
     }
 #pragma unroll
@@ -729,7 +687,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-        const bool valid = base + w * WCH + j * 64 + lane < io.n;
+        const bool valid = base + w * WCH + j * 64 + lane < n;
         const uint32_t d = (keys[j] >> shift) & (RADIX_DIGITS - 1);
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < RADIX_BITS; ++b) {
@@ -756,25 +714,26 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
         uint32_t tot;
         const uint32_t ex = block_excl_scan_256(t0 + t1, wsum, tot);
         uint32_t r0 = ex, r1 = ex + t0;
-        gdelta[2 * t] = S.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - r0;
-        gdelta[2 * t + 1] = S.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - r1;
+        gdelta[2 * t] = R.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - r0;
+        gdelta[2 * t + 1] = R.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - r1;
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) { wh[ww][2 * t] = r0; wh[ww][2 * t + 1] = r1; r0 += c0[ww]; r1 += c1[ww]; }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-        if (base + w * WCH + j * 64 + lane < io.n) {
+        if (base + w * WCH + j * 64 + lane < n) {
             const uint32_t pos = wh[w][(keys[j] >> shift) & (RADIX_DIGITS - 1)] + wr[j];
             lkey[pos] = keys[j];
             lval[pos] = vals[j];
         }
     }
     __syncthreads();
-    const uint32_t cnt = io.n - base < (uint32_t)RADIX_TILE ? io.n - base : (uint32_t)RADIX_TILE;
-    KG uint32_t* okeys = dst ? S.rkeys[1] : S.rkeys[0];
-    KG uint32_t* ovals = dst ? S.rvals[1] : S.rvals[0];
-    const bool last = pass == S.passes - 1 && S.rank;
+    if (base >= n) return;
+    const uint32_t cnt = n - base < (uint32_t)RADIX_TILE ? n - base : (uint32_t)RADIX_TILE;
+    KG uint32_t* okeys = R.keys[dst];
+    KG uint32_t* ovals = R.vals[dst];
+    const bool last = pass == R.passes - 1 && R.rank;
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
         const uint32_t e = j * 256 + t;
@@ -783,7 +742,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(DevState S, EpochIO io, i
             const uint32_t pos = gdelta[(key >> shift) & (RADIX_DIGITS - 1)] + e;
             okeys[pos] = key;
             ovals[pos] = val;
-            if (last) S.rank[val] = (int32_t)pos;
+            if (last) R.rank[val] = (int32_t)pos;
         }
     }
 }
@@ -3633,6 +3592,8 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
     if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;   // a serial epoch kept the exact ledger itself
+    if (S.lpar && S.lctr[ci(LC_FALLBACK)] == 0) return;     // kme_ledger.hip applied it in parallel
+    if (lane_id() == 0) S.ctr[ci(C_LSERIAL)] = 1;
     Core c(S, io);
     const int lane = lane_id();
     for (uint32_t k0 = 0; k0 < io.n && !c.dead; k0 += 64) {
@@ -3871,7 +3832,8 @@ __global__ void k_init_state(DevState S) {
 __global__ void k_epoch_reset(DevState S) {
     const int k = threadIdx.x;
     if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
-    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY || k == C_LIGHT)
+    else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY || k == C_LIGHT ||
+             k == C_LREPAIRED || k == C_LSERIAL)
         S.ctr[ci(k)] = 0ull;
 }
 
@@ -3920,17 +3882,37 @@ static void launch_scan2(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t
     hipLaunchKernelGGL(k_tile_sums, dim3(nb), dim3(256), 0, st, in, L, sums);
     hipLaunchKernelGGL(k_scan_tiles, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end);
 }
-int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
-    const uint32_t ntiles = cdiv(io.n > 0 ? io.n : 1, RADIX_TILE);
+// Stable LSD radix sort of (key, value) pairs, R.passes digit passes; the result is in keys / vals
+// [R.passes & 1].
+void launch_radix(const RadixIO& R, hipStream_t st) {
+    const uint32_t ntiles = cdiv(R.n > 0 ? R.n : 1, RADIX_TILE);
     int src = 0;
-    for (int pass = 0; pass < S.passes; ++pass) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(256), 0, st, S, io, pass, src);
+    for (int pass = 0; pass < R.passes; ++pass) {
+        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
         const uint32_t L = RADIX_DIGITS * ntiles;
-        launch_scan2(S.ghist, S.ghist, L, S.ghist + L, nullptr, 0, st);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(256), 0, st, S, io, pass, src);
+        launch_scan2(R.ghist, R.ghist, L, R.ghist + L, nullptr, 0, st);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         src ^= 1;
     }
+}
+void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st) {
+    launch_scan2(in, out, L, sums, total, 0, st);
+}
+int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
+    RadixIO R{};
+    R.key0 = S.route_grp;
+    R.val0 = nullptr;
+    R.keys[0] = S.rkeys[0]; R.keys[1] = S.rkeys[1];
+    R.vals[0] = S.rvals[0]; R.vals[1] = S.rvals[1];
+    R.ghist = S.ghist;
+    R.rank = S.rank;
+    R.none = (uint32_t)S.G;
+    R.n = io.n;
+    R.n_dev = nullptr;
+    R.passes = S.passes;
+    launch_radix(R, st);
+    const int src = S.passes & 1;
     const uint32_t nthreads = (io.n + 1) > (uint32_t)S.G + 2 ? io.n + 1 : (uint32_t)S.G + 2;
     hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src);
     return src;

@@ -16,6 +16,28 @@ constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT
 constexpr int kLaneTradeChunk = 8;    // trade scratch slots a k_match_lanes lane reserves at a time
 constexpr int kOsLanesMaxLight = 512;  // light_max up to which light groups' OUT echo goes step-major
 
+// A stable LSD radix sort of (key, value) u32 pairs, RADIX_BITS-bit digits (the partition's kernels).
+// Pass 0 reads key0 (negative -> `none`) and val0 (nullptr: the element's index); the result is in
+// keys / vals [passes & 1].  n_dev: the count on the device (at most n), else n.
+struct RadixIO {
+    const KG int32_t* key0;
+    const KG uint32_t* val0;
+    KG uint32_t* keys[2];
+    KG uint32_t* vals[2];
+    KG uint32_t* ghist;              // RADIX_DIGITS x tiles + the scan's scratch
+    KG int32_t* rank;                // the last pass: rank[value] = position (nullptr: none)
+    uint32_t none;
+    uint32_t n;
+    const KG unsigned long long* n_dev;
+    int passes;
+};
+void launch_radix(const RadixIO& R, hipStream_t st);
+void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st);
+// FUNDED + exact ledger: the epoch's ledger effects in parallel (kme_ledger.hip); the serial replay
+// (launch_ledger_replay) runs after it and does the work only when this path fell back
+void launch_ledger_parallel(const DevState& S, const DevState* S_dev, const EpochIO& io, const EpochIO* io_dev,
+                            uint32_t max_trades, hipStream_t st);
+
 // FUNDED pipeline
 void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);

@@ -1,0 +1,691 @@
+// kme_ledger.hip -- FUNDED + KME_FLAG_EXACT_LEDGER (SURVEY §8 row f next-2): the epoch's ledger
+// effects applied in parallel, bit-exact with the reference's arrival-order updates.
+//
+// Reference (KProcessor.java, "KP"): checkBalance KP:167-182, fillOrder KP:276-287 (twice per trade,
+// executeTrade KP:265-274), postRemoveAdjustments KP:325-333, createBalance / transfer KP:131-146,
+// and the position store's value-keyed writes KP:434-436 (hazard H2).
+//
+// After the parallel matching every outcome of the epoch is fixed (accept / reject, every trade):
+// the funded proof (k_check_funded) guarantees each checkBalance passes.  What remains are the
+// ledger's values, and they decompose:
+//
+//   * Balances: every effect is an addition (checkBalance's -risk, a fill's size * price, a refund,
+//     a transfer), so an account's final balance is its start plus the sum of its deltas in any
+//     order (Java long wrap-around is a group).  One wavefront per account sums them.
+//   * Positions: the entry keyed (aid, sid) -- a "chain" -- is read by the account's checkBalance,
+//     fillOrder and postRemoveAdjustments on that symbol, and written back under its own key only by
+//     checkBalance (KP:179-180) and the first fill (KP:280).  Every other write goes under the
+//     position's VALUE as key (setPosition(UUID, ...) / positions.delete(position), KP:283-284, 332,
+//     434-436): a "value write" to the key (amount, available).  One lane applies a chain's ops in
+//     arrival order and records its value writes.
+//   * A value write whose key is another chain of this epoch, read after the write, couples the two
+//     chains: the reference clobbers that real position.  k_ldetect finds them; k_lrepair replays the
+//     chains involved in arrival order on one wavefront, growing the set until no new coupling appears.
+//     More than a few hundred couplings (streams over few accounts and symbols, where almost every
+//     position value is also some live key) send the epoch to the serial replay (k_ledger_replay).
+//     Value writes to keys no chain of the epoch reads commit last-writer-wins (latest arrival).
+//
+// Ops are compacted in arrival order, one per (record, chain) -- a BUY/SELL's checkBalance with its
+// taker fills (and any maker fill on the same key) is one op on (aid, sid), each other maker fill one
+// op on the maker's key, an accepted cancel one op -- and sorted (stable LSD radix, the partition's
+// kernels) by aid * 256 + hash8(sid): an account's ops are contiguous and a chain's are in arrival
+// order.  Every effect carries its arrival number seq = i + 2 trade_off[i] for record i (its check or
+// cancel), + 2k + 1 for trade k's maker fill, + 2k + 2 for its taker fill -- the executeTrade order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kme.h"
+#include "kme_device.h"
+#include "kme_jarith.h"
+#include "kme_launch.h"
+
+namespace kme {
+
+namespace {
+
+constexpr int LB_BUCKET_BITS = 8;                 // hash8(sid): 256 buckets per account
+constexpr uint32_t L_OP_REC = 0u, L_OP_MAKER = 1u, L_OP_CANCEL = 2u;
+constexpr uint32_t VW_PUT = 1u, VW_DEL = 2u;
+
+KDEV uint32_t hash8(int64_t sid) { return (uint32_t)(mix64((uint64_t)sid ^ 0x632be59bd9b4e019ull) >> 56); }
+KDEV uint32_t lkey_of(int64_t aid, int64_t sid) { return (uint32_t)aid << LB_BUCKET_BITS | hash8(sid); }
+
+KDEV unsigned long long* lc(const DevState& S, int k) { return &S.lctr[ci(k)]; }
+KDEV void lfallback(const DevState& S) { atomicOr(lc(S, LC_FALLBACK), 1ull); }
+KDEV bool lfell(const DevState& S) {
+    return __hip_atomic_load(lc(S, LC_FALLBACK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+// not this path's epoch: a fault (nothing of it is replayed), or a serial epoch (k_serial kept the ledger)
+KDEV bool lskip(const DevState& S) { return failed(S.ctr) || S.ctr[ci(C_FALLBACK)] != 0; }
+KDEV uint32_t lops(const DevState& S) { return (uint32_t)S.lctr[ci(LC_OPS)]; }
+KDEV uint32_t lseqs(const DevState& S, const EpochIO& io) { return io.n + 2 * (uint32_t)S.ctr[ci(C_TRADES)]; }
+
+// ---------------------------------------------------------------- stores (Core's layout, shared)
+KDEV uint32_t ld_state(const KG uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+KDEV uint32_t pos_hash(const DevState& S, int64_t k0, int64_t k1) {
+    return (uint32_t)mix64((uint64_t)k0 * 0x9e3779b97f4a7c15ull ^ mix64((uint64_t)k1)) & S.pos_mask;
+}
+// positions.get(UUID(k0, k1)): the slot of a live entry, or -1
+KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
+    uint32_t h = pos_hash(S, k0, k1);
+    for (uint32_t p = 0; p <= S.pos_mask; ++p) {
+        const uint32_t st = ld_state(&S.pos_state[h]);
+        if (st == 0) return -1;
+        if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) return (int32_t)h;
+        h = (h + 1) & S.pos_mask;
+    }
+    return -1;
+}
+// positions.put by the one thread that commits this key: update in place, or claim a free slot (the
+// probe chain's first tombstone, else its empty end) by CAS to the transient state 3, write the
+// entry, publish state 1.  A prober meeting state 3 passes it (another key: every key has one
+// committing thread).  false = no room.
+KDEV bool pos_upsert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1) {
+    for (int attempt = 0; attempt < 4096; ++attempt) {
+        uint32_t h = pos_hash(S, k0, k1);
+        int32_t tomb = -1;
+        uint32_t p = 0;
+        for (; p <= S.pos_mask; ++p) {
+            const uint32_t st = ld_state(&S.pos_state[h]);
+            if (st == 0) break;
+            if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) {
+                S.pos[h].v0 = v0;
+                S.pos[h].v1 = v1;
+                return true;
+            }
+            if (st == 2 && tomb < 0) tomb = (int32_t)h;
+            h = (h + 1) & S.pos_mask;
+        }
+        if (p > S.pos_mask && tomb < 0) return false;
+        const uint32_t at = tomb >= 0 ? (uint32_t)tomb : h, expect = tomb >= 0 ? 2u : 0u;
+        if (atomicCAS((unsigned int*)&S.pos_state[at], expect, 3u) != expect) continue;   // taken meanwhile
+        S.pos[at].k0 = k0; S.pos[at].k1 = k1; S.pos[at].v0 = v0; S.pos[at].v1 = v1;
+        __threadfence();
+        __hip_atomic_store(&S.pos_state[at], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (expect == 0) atomicAdd(&S.ctr[ci(C_POS_USED)], 1ull);
+        return true;
+    }
+    return false;
+}
+KDEV int32_t bal_lookup(const DevState& S, int64_t aid) {
+    uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
+    for (uint32_t p = 0; p <= S.bal_mask; ++p) {
+        const uint32_t st = ld_state(&S.bal_state[h]);
+        if (st == 0) return -1;
+        if (st == 1 && S.bal_key[h] == aid) return (int32_t)h;
+        h = (h + 1) & S.bal_mask;
+    }
+    return -1;
+}
+// createBalance's put (KP:134), same protocol (balances are never deleted: no tombstones)
+KDEV bool bal_create(const DevState& S, int64_t aid) {
+    for (int attempt = 0; attempt < 4096; ++attempt) {
+        uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
+        uint32_t p = 0;
+        for (; p <= S.bal_mask; ++p) {
+            const uint32_t st = ld_state(&S.bal_state[h]);
+            if (st == 0) break;
+            if (st == 1 && S.bal_key[h] == aid) return true;
+            h = (h + 1) & S.bal_mask;
+        }
+        if (p > S.bal_mask) return false;
+        if (atomicCAS((unsigned int*)&S.bal_state[h], 0u, 3u) != 0u) continue;
+        S.bal_key[h] = aid;
+        S.bal_val[h] = 0;
+        __threadfence();
+        __hip_atomic_store(&S.bal_state[h], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&S.ctr[ci(C_BAL_USED)], 1ull);
+        return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------- the effects
+struct PState {
+    int64_t a, v;      // amount, available (KP:418-424)
+    bool present;
+};
+struct VWrite {        // a value write (H2): key = the position read, and the new value
+    int64_t k0, k1, v0, v1;
+    uint32_t kind;     // 0 none, VW_PUT, VW_DEL
+};
+
+// checkBalance (KP:167-182) of an accepted order: the reservation, and when adj != 0 the position's
+// available under its own key (KP:179-180; adj != 0 implies the position exists)
+KDEV int64_t eff_check(PState& P, bool is_buy, int32_t size, int32_t price) {
+    const int32_t s = jimul(size, is_buy ? 1 : -1);
+    const int64_t available = P.present ? P.v : 0;
+    const int64_t adj = is_buy ? lmax(lmin(available, 0), (int64_t)jineg(s)) : lmin(lmax(available, 0), (int64_t)jineg(s));
+    if (adj != 0) P.v = jlsub(available, adj);
+    return jlneg(jlmul(jladd((int64_t)s, adj), (int64_t)(is_buy ? price : jisub(price, 100))));
+}
+// fillOrder (KP:276-287): absent -> created under (aid, sid); present -> the new value written under
+// the old VALUE as key (that key deleted when the amount returns to 0); the entry read stays as is
+KDEV int64_t eff_fill(PState& P, bool bought, int32_t fsize, int32_t price, VWrite& w) {
+    const int32_t s = jimul(fsize, bought ? 1 : -1);
+    w.kind = 0;
+    if (!P.present) {
+        P.present = true;
+        P.a = s;
+        P.v = s;
+    } else {
+        const int64_t np = jladd(P.a, (int64_t)s);
+        w.k0 = P.a;
+        w.k1 = P.v;
+        if (np == 0) {
+            w.kind = VW_DEL;
+        } else {
+            w.kind = VW_PUT;
+            w.v0 = np;
+            w.v1 = jladd(P.v, (int64_t)s);
+        }
+    }
+    return (int64_t)jimul(s, price);
+}
+// postRemoveAdjustments (KP:325-333): the refund; adj != 0 writes (amount, available + adj) under the
+// position's value as key
+KDEV int64_t eff_cancel(PState& P, bool is_buy, int32_t size, int32_t price, VWrite& w) {
+    const int32_t s = jimul(size, is_buy ? 1 : -1);
+    const int64_t blocked = P.present ? jlsub(P.a, P.v) : 0;
+    const int64_t adj = is_buy ? lmax(lmin(blocked, 0), (int64_t)jineg(s)) : lmin(lmax(blocked, 0), (int64_t)jineg(s));
+    w.kind = 0;
+    if (adj != 0) {
+        w.kind = VW_PUT;
+        w.k0 = P.a;
+        w.k1 = P.v;
+        w.v0 = P.a;
+        w.v1 = jladd(P.v, adj);
+    }
+    return jlmul(jladd((int64_t)s, adj), (int64_t)(is_buy ? price : jisub(price, 100)));
+}
+// a value write to the chain's own key changes the chain itself
+KDEV void write_into(PState& P, const VWrite& w) {
+    if (w.kind == VW_DEL) {
+        P.present = false;
+    } else if (w.kind == VW_PUT) {
+        P.present = true;
+        P.a = w.v0;
+        P.v = w.v1;
+    }
+}
+
+// The effect with arrival number `es` of the op at `seq` (its check / cancel: es == seq; trade k's
+// maker fill: i + 2k + 1; its taker fill: i + 2k + 2) on chain (aid, sid); returns the balance delta.
+KDEV int64_t apply_effect(const DevState& S, const EpochIO& io, uint32_t seq, uint32_t es, int64_t aid, int64_t sid,
+                          PState& P, VWrite& w) {
+    const uint32_t meta = S.lop[seq];
+    const uint32_t kind = meta >> 30, i = meta & 0x3FFFFFFFu;
+    w.kind = 0;
+    int64_t d;
+    if (kind == L_OP_CANCEL) {
+        const int4 o = S.vic[i];
+        d = eff_cancel(P, (o.x >> 8) == BUY, o.y, o.x & 0xFF, w);
+    } else if (kind == L_OP_REC && es == seq) {
+        d = eff_check(P, io.action[i] == BUY, io.size[i], io.price[i]);
+    } else {
+        const uint32_t q = (es - i - 1) / 2;   // (maker fill: es - i odd; taker fill: even)
+        const TradeRec tr = io.trades[q];
+        const bool taker_buy = io.action[i] == BUY;
+        if (((es - i) & 1u) == 1u) d = eff_fill(P, !taker_buy, tr.size, 0, w);                               // KP:266-267
+        else d = eff_fill(P, taker_buy, tr.size, jisub(io.price[i], tr.mprice), w);                          // KP:268-269
+    }
+    if (w.kind && w.k0 == aid && w.k1 == sid) write_into(P, w);
+    return d;
+}
+// The effects of one op, in order: f(es).
+template <class F>
+KDEV void for_effects(const DevState& S, const EpochIO& io, uint32_t seq, int64_t aid, int64_t sid, F&& f) {
+    const uint32_t meta = S.lop[seq];
+    f(seq);
+    if ((meta >> 30) != L_OP_REC) return;
+    const uint32_t i = meta & 0x3FFFFFFFu;
+    for (uint32_t q = io.trade_off[i]; q < io.trade_off[i + 1]; ++q) {
+        const TradeRec tr = io.trades[q];
+        if (tr.maid == aid && tr.msid == sid) f(i + 2 * q + 1);   // a maker fill on this same key
+        f(i + 2 * q + 2);
+    }
+}
+
+// The sorted ops: keys (aid * 256 + hash8(sid)) and values (seq) of the last radix pass.
+KDEV const KG uint32_t* skeys(const DevState& S) { return S.lkey[S.lpasses & 1]; }
+KDEV const KG uint32_t* svals(const DevState& S) { return S.lval[S.lpasses & 1]; }
+KDEV uint32_t lower_bound(const KG uint32_t* k, uint32_t lo, uint32_t hi, uint32_t key) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (k[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+// The chain (head position) of key (k0, k1) among this epoch's ops, or -1.
+KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
+    if (k0 < 0 || k0 >= S.A) return -1;
+    const KG uint32_t* K = skeys(S);
+    const KG uint32_t* V = svals(S);
+    const uint32_t key = lkey_of(k0, k1);
+    const uint32_t hi = S.lseg[k0 + 1];
+    for (uint32_t p = lower_bound(K, S.lseg[k0], hi, key); p < hi && K[p] == key; ++p)
+        if (S.lsid[V[p]] == k1) return (int32_t)p;
+    return -1;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- 1. the ops in arrival order
+__global__ void __launch_bounds__(256) k_lcount(DevState S, EpochIO io) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= io.n) return;
+    uint32_t c = 0;
+    if (!lskip(S)) {
+        const int32_t a = io.action[i], out = io.out_action[i];
+        if ((a == BUY || a == SELL) && out == a) {
+            c = 1;
+            const int64_t aid = io.aid[i], sid = io.sid[i];
+            for (uint32_t q = io.trade_off[i]; q < io.trade_off[i + 1]; ++q) {
+                const TradeRec tr = io.trades[q];
+                c += (tr.maid == aid && tr.msid == sid) ? 0u : 1u;
+            }
+        } else if (a == CANCEL && out == CANCEL) {
+            c = 1;
+        }
+    }
+    S.lcnt[i] = c;
+}
+// At the scanned offsets: sort key aid * 256 + hash8(sid) and value seq; per seq the op's record and
+// kind (lop) and its chain's sid (lsid).
+__global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= io.n || lskip(S)) return;
+    const int32_t a = io.action[i], out = io.out_action[i];
+    uint32_t o = S.lcnt[i];
+    const uint32_t t0 = io.trade_off[i], seq = i + 2 * t0;
+    if ((a == BUY || a == SELL) && out == a) {
+        const int64_t aid = io.aid[i], sid = io.sid[i];
+        S.lk0[o] = lkey_of(aid, sid); S.lv0[o] = seq; ++o;
+        S.lop[seq] = L_OP_REC << 30 | i;
+        S.lsid[seq] = sid;
+        for (uint32_t q = t0; q < io.trade_off[i + 1]; ++q) {
+            const TradeRec tr = io.trades[q];
+            if (tr.maid == aid && tr.msid == sid) continue;
+            const uint32_t ms = i + 2 * q + 1;
+            S.lk0[o] = lkey_of(tr.maid, tr.msid); S.lv0[o] = ms; ++o;
+            S.lop[ms] = L_OP_MAKER << 30 | i;
+            S.lsid[ms] = tr.msid;
+        }
+    } else if (a == CANCEL && out == CANCEL) {
+        const int4 v = S.vic[i];
+        const int64_t vsid = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
+        S.lk0[o] = lkey_of(io.aid[i], vsid); S.lv0[o] = seq;
+        S.lop[seq] = L_OP_CANCEL << 30 | i;
+        S.lsid[seq] = vsid;
+    }
+}
+
+// ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
+__global__ void __launch_bounds__(256) k_lseg(DevState S) {
+    const uint32_t n = lops(S);
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > n || n == 0) return;      // (no ops: lseg stays zero)
+    const KG uint32_t* K = skeys(S);
+    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> LB_BUCKET_BITS);
+    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> LB_BUCKET_BITS);
+    for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
+}
+
+// ---------------------------------------------------------------- 3. chains: one wavefront per account
+// Lane l takes the account's buckets 4l .. 4l + 3; a chain is the ops of one sid inside a bucket run
+// (in arrival order: the sort is stable).  Its start state is the Positions entry (aid, sid); its
+// record (LChain) sits at the position of its first op, which is also its name.
+__global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
+    const uint32_t a = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (a >= (uint32_t)S.A || lskip(S) || lops(S) == 0) return;
+    const uint32_t lo = S.lseg[a], hi = S.lseg[a + 1];
+    if (lo == hi) return;
+    const KG uint32_t* K = skeys(S);
+    const KG uint32_t* V = svals(S);
+    const uint32_t kb = a << LB_BUCKET_BITS;
+    const uint32_t ls = lower_bound(K, lo, hi, kb + 4 * lane), le = lower_bound(K, ls, hi, kb + 4 * lane + 4);
+    int64_t dsum = 0;
+    for (uint32_t j = ls; j < le; ++j) {
+        const uint32_t bj = K[j], sj = V[j];
+        const int64_t sid = S.lsid[sj];
+        bool head = true;   // the first op of its sid in this bucket run?
+        for (uint32_t p = j; p > ls && K[p - 1] == bj; --p)
+            if (S.lsid[V[p - 1]] == sid) { head = false; break; }
+        KG LChain& c = S.lchain[j];
+        if (!head) { c.aid = -1; continue; }
+        const int32_t slot = pos_lookup(S, a, sid);
+        PState P;
+        P.present = slot >= 0;
+        P.a = P.present ? S.pos[slot].v0 : 0;
+        P.v = P.present ? S.pos[slot].v1 : 0;
+        c.sid = sid; c.aid = (int32_t)a; c.islot = slot;
+        c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
+        int64_t cd = 0;
+        uint32_t last = 0;
+        for (uint32_t p = j; p < le && K[p] == bj; ++p) {
+            const uint32_t sq = V[p];
+            if (p != j && S.lsid[sq] != sid) continue;
+            for_effects(S, io, sq, (int64_t)a, sid, [&](uint32_t es) {
+                VWrite w;
+                cd = jladd(cd, apply_effect(S, io, sq, es, (int64_t)a, sid, P, w));
+                last = es;
+                if (w.kind) {
+                    S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                    S.lvw_meta[es] = w.kind | (j << 2);
+                }
+            });
+        }
+        c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
+        c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0;
+        dsum = jladd(dsum, cd);
+    }
+    // the account's balance delta: a wavefront sum (wrap-around, order-free)
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)dsum, off, 64);
+        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)dsum >> 32), off, 64);
+        dsum = jladd(dsum, (int64_t)(((uint64_t)hi32 << 32) | lo32));
+    }
+    if (lane == 0) S.ldelta[a] = dsum;
+}
+
+// ---------------------------------------------------------------- 4. couplings between chains
+// A value write into a chain of this epoch that the chain reads afterwards (seq < its last effect).
+__global__ void __launch_bounds__(256) k_ldetect(DevState S, EpochIO io) {
+    if (lskip(S) || lops(S) == 0) return;
+    const uint32_t ns = lseqs(S, io);
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+        const uint32_t meta = S.lvw_meta[s];
+        if (!(meta & 3u)) continue;
+        const long4 w = S.lvw[s];
+        const int32_t c = find_chain(S, w.x, w.y);
+        S.lvw_tgt[s] = c;
+        if (c < 0 || (uint32_t)c == (meta >> 2) || s > S.lchain[c].last_seq) continue;
+        const unsigned long long x = atomicAdd(lc(S, LC_CROSS), 1ull);
+        if (x < S.lx_cap) S.lx[x] = s;
+        if (atomicExch(&S.lchain[c].dirty, 1u) == 0u) {
+            const unsigned long long d = atomicAdd(lc(S, LC_DIRTY), 1ull);
+            if (d < S.lr_cap) S.ldirty[d] = (uint32_t)c;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- 5. the coupled chains, in arrival order
+// One thread (the chains involved are few): the effects of the chains in the set R and the value
+// writes into them from chains outside R, sorted by arrival number and applied in that order; a value
+// write of an R chain into a chain outside R that reads it later adds that chain to R and starts over.
+// Converged: the chains' final states, balance deltas and value writes are replaced.  Too many chains
+// or effects: the epoch goes to the serial replay.
+struct LEvent { uint32_t seq, r, op, ext; };   // ext: 1 = a value write from outside R into chain r
+__global__ void __launch_bounds__(64) k_lrepair(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
+    const DevState& S = *Sp;
+    const EpochIO& io = *iop;
+    if (threadIdx.x != 0 || lskip(S) || lops(S) == 0) return;
+    const uint32_t nd = (uint32_t)S.lctr[ci(LC_DIRTY)], nx = (uint32_t)S.lctr[ci(LC_CROSS)];
+    if (nd == 0) return;
+    if (nd > S.lr_cap || nx > S.lx_cap) { lfallback(S); return; }
+    KG uint32_t* R = S.lrscr;                                   // chain heads of the set
+    KG LEvent* ev = reinterpret_cast<KG LEvent*>(S.lrscr + S.lr_cap);
+    KG int64_t* st = reinterpret_cast<KG int64_t*>(ev + S.le_cap);   // per R chain: a, v, present, delta
+    KG long4* nw = reinterpret_cast<KG long4*>(st + 4 * (size_t)S.lr_cap);   // per event: the new value write
+    KG uint32_t* nk = reinterpret_cast<KG uint32_t*>(nw + S.le_cap);
+    uint32_t nr = 0;
+    for (uint32_t d = 0; d < nd; ++d) { R[nr] = S.ldirty[d]; S.lchain[R[nr]].rix = nr + 1; ++nr; }
+    const KG uint32_t* K = skeys(S);
+    const KG uint32_t* V = svals(S);
+    for (uint32_t round = 0; round < 32; ++round) {
+        // the events
+        uint32_t ne = 0;
+        bool over = false;
+        for (uint32_t r = 0; r < nr && !over; ++r) {
+            const uint32_t head = R[r];
+            const int64_t aid = S.lchain[head].aid, sid = S.lchain[head].sid;
+            const uint32_t hi = S.lseg[aid + 1];
+            for (uint32_t p = head; p < hi && K[p] == K[head] && !over; ++p) {
+                const uint32_t sq = V[p];
+                if (S.lsid[sq] != sid) continue;
+                for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
+                    if (ne == S.le_cap) { over = true; return; }
+                    ev[ne++] = LEvent{es, r, sq, 0};
+                });
+            }
+        }
+        for (uint32_t x = 0; x < nx && !over; ++x) {
+            const uint32_t s = S.lx[x];
+            const int32_t c = S.lvw_tgt[s];
+            const uint32_t src = S.lvw_meta[s] >> 2;
+            if (c < 0 || S.lchain[c].rix == 0 || S.lchain[src].rix != 0) continue;   // into R, from outside R
+            if (ne == S.le_cap) { over = true; break; }
+            ev[ne++] = LEvent{s, S.lchain[c].rix - 1, 0, 1};
+        }
+        if (over) { lfallback(S); break; }
+        // arrival order (shell sort: a few thousand events at most)
+        for (uint32_t gap = ne / 2; gap > 0; gap /= 2)
+            for (uint32_t i = gap; i < ne; ++i) {
+                const LEvent t = ev[i];
+                uint32_t j = i;
+                for (; j >= gap && ev[j - gap].seq > t.seq; j -= gap) ev[j] = ev[j - gap];
+                ev[j] = t;
+            }
+        for (uint32_t r = 0; r < nr; ++r) {
+            const KG LChain& c = S.lchain[R[r]];
+            st[4 * r] = c.ia; st[4 * r + 1] = c.iv; st[4 * r + 2] = c.ipres; st[4 * r + 3] = 0;
+        }
+        bool grown = false;
+        for (uint32_t e = 0; e < ne && !grown; ++e) {
+            const LEvent E = ev[e];
+            PState P{st[4 * E.r], st[4 * E.r + 1], st[4 * E.r + 2] != 0};
+            VWrite w;
+            if (E.ext) {
+                const long4 x = S.lvw[E.seq];
+                w = VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[E.seq] & 3u};
+                write_into(P, w);
+            } else {
+                const KG LChain& c = S.lchain[R[E.r]];
+                st[4 * E.r + 3] = jladd(st[4 * E.r + 3], apply_effect(S, io, E.op, E.seq, c.aid, c.sid, P, w));
+                nw[e] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                nk[e] = w.kind;
+                if (w.kind && !(w.k0 == c.aid && w.k1 == c.sid)) {
+                    const int32_t t = find_chain(S, w.k0, w.k1);
+                    if (t >= 0 && S.lchain[t].rix != 0) {          // into a chain of R: applied in order
+                        const uint32_t tr = S.lchain[t].rix - 1;
+                        PState Q{st[4 * tr], st[4 * tr + 1], st[4 * tr + 2] != 0};
+                        write_into(Q, w);
+                        st[4 * tr] = Q.a; st[4 * tr + 1] = Q.v; st[4 * tr + 2] = Q.present;
+                    } else if (t >= 0 && E.seq < S.lchain[t].last_seq) {   // a new coupling
+                        if (nr == S.lr_cap) { lfallback(S); return; }
+                        R[nr] = (uint32_t)t;
+                        S.lchain[t].rix = ++nr;
+                        grown = true;
+                    }
+                }
+            }
+            st[4 * E.r] = P.a; st[4 * E.r + 1] = P.v; st[4 * E.r + 2] = P.present;
+        }
+        if (grown) continue;
+        // converged: the chains' results and value writes replace the first pass's
+        for (uint32_t e = 0; e < ne; ++e) {
+            if (ev[e].ext) continue;
+            S.lvw[ev[e].seq] = nw[e];
+            S.lvw_meta[ev[e].seq] = nk[e] | (R[ev[e].r] << 2);
+            if (nk[e]) {
+                const long4 x = nw[e];
+                S.lvw_tgt[ev[e].seq] = find_chain(S, x.x, x.y);
+            }
+        }
+        for (uint32_t r = 0; r < nr; ++r) {
+            KG LChain& c = S.lchain[R[r]];
+            c.fa = st[4 * r]; c.fv = st[4 * r + 1]; c.fpres = st[4 * r + 2] != 0;
+            S.ldelta[c.aid] = jladd(S.ldelta[c.aid], jlsub(st[4 * r + 3], c.delta));
+            c.delta = st[4 * r + 3];
+            c.rix = 0;
+        }
+        atomicAdd(lc(S, LC_REPAIRED), (unsigned long long)nr);
+        S.ctr[ci(C_LREPAIRED)] = nr;
+        return;
+    }
+    lfallback(S);   // (no convergence in 32 rounds)
+}
+
+// ---------------------------------------------------------------- 6. commit
+// Value writes: into a chain of the epoch after its last read -> the chain's final value (latest
+// wins, `late`); into a chain it reads later -> already applied; into no chain -> last-writer-wins
+// per key through a per-epoch table keyed by a 64-bit hash of the key (the winner then stores the
+// key, and a second pass checks every writer's key against it: a hash collision of two different keys
+// sends the epoch to the serial replay).
+KDEV uint64_t vkey_hash(int64_t k0, int64_t k1) { return mix64((uint64_t)k0 * 0xc2b2ae3d27d4eb4full ^ mix64((uint64_t)k1 + 1)) | 1ull; }
+KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert) {
+    uint64_t p = h & S.lvk_mask;
+    for (uint32_t probes = 0; probes < 4096; ++probes) {
+        KG unsigned long long* e = reinterpret_cast<KG unsigned long long*>(&S.lvk[p]);
+        const unsigned long long cur = insert ? atomicCAS(e, 0ull, (unsigned long long)h)
+                                              : __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == h || (insert && cur == 0)) return (int64_t)p;
+        if (cur == 0) return -1;
+        p = (p + 1) & S.lvk_mask;
+    }
+    return -1;
+}
+__global__ void __launch_bounds__(256) k_lvw_classify(DevState S, EpochIO io) {
+    if (lskip(S) || lops(S) == 0 || lfell(S)) return;
+    const uint32_t ns = lseqs(S, io);
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+        const uint32_t meta = S.lvw_meta[s];
+        if (!(meta & 3u)) continue;
+        const int32_t c = S.lvw_tgt[s];
+        if (c >= 0) {
+            if ((uint32_t)c != (meta >> 2) && s > S.lchain[c].last_seq) atomicMax(&S.lchain[c].late, s + 1);
+            continue;
+        }
+        const long4 w = S.lvw[s];
+        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), true);
+        if (p < 0) { lfallback(S); return; }
+        atomicMax(reinterpret_cast<KG unsigned long long*>(&S.lvk[p]) + 1, (unsigned long long)s + 1);
+    }
+}
+__global__ void __launch_bounds__(256) k_lvw_claim(DevState S, EpochIO io, int check) {
+    if (lskip(S) || lops(S) == 0 || lfell(S)) return;
+    const uint32_t ns = lseqs(S, io);
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+        if (!(S.lvw_meta[s] & 3u) || S.lvw_tgt[s] >= 0) continue;
+        const long4 w = S.lvw[s];
+        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), false);
+        if (p < 0) { lfallback(S); return; }
+        KG ulonglong4& e = S.lvk[p];
+        if (!check) {
+            if (e.y == (unsigned long long)s + 1) { e.z = (unsigned long long)w.x; e.w = (unsigned long long)w.y; }
+        } else if ((int64_t)e.z != w.x || (int64_t)e.w != w.y) {
+            lfallback(S);   // two keys with one hash
+        }
+    }
+}
+// Account records (createBalance / transfer, KP:131-146): outcomes fixed by k_ledger_funded.
+__global__ void __launch_bounds__(256) k_lacct(DevState S, EpochIO io) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= io.n || lskip(S) || lfell(S) || S.ctr[ci(C_ACCT_OPS)] == 0) return;
+    const int32_t a = io.action[i];
+    if (io.out_action[i] != a) return;
+    if (a == CREATE_BALANCE) {
+        if (!bal_create(S, io.aid[i])) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+    } else if (a == TRANSFER) {
+        atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[io.aid[i]]), (unsigned long long)(int64_t)io.size[i]);
+    }
+}
+__global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io) {
+    if (lskip(S) || lops(S) == 0 || lfell(S)) return;
+    const uint32_t ns = lseqs(S, io), no = lops(S);
+    const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    // the winning value write of each key no chain reads
+    for (uint32_t s = t0; s < ns; s += stride) {
+        const uint32_t meta = S.lvw_meta[s];
+        if (!(meta & 3u) || S.lvw_tgt[s] >= 0) continue;
+        const long4 w = S.lvw[s];
+        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), false);
+        if (p < 0 || S.lvk[p].y != (unsigned long long)s + 1) continue;
+        if ((meta & 3u) == VW_DEL) {
+            const int32_t h = pos_lookup(S, w.x, w.y);
+            if (h >= 0) __hip_atomic_store(&S.pos_state[h], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (!pos_upsert(S, w.x, w.y, w.z, w.w)) {
+            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+        }
+    }
+    // every chain's final entry (its own last state, or a later value write into it)
+    for (uint32_t p = t0; p < no; p += stride) {
+        const KG LChain& c = S.lchain[p];
+        if (c.aid < 0) continue;
+        bool fp = c.fpres != 0;
+        int64_t fa = c.fa, fv = c.fv;
+        if (c.late) {
+            const uint32_t s = c.late - 1;
+            const long4 w = S.lvw[s];
+            fp = (S.lvw_meta[s] & 3u) == VW_PUT;
+            fa = w.z;
+            fv = w.w;
+        }
+        if (fp == (c.ipres != 0) && (!fp || (fa == c.ia && fv == c.iv))) continue;
+        if (c.ipres) {
+            if (fp) { S.pos[c.islot].v0 = fa; S.pos[c.islot].v1 = fv; }
+            else __hip_atomic_store(&S.pos_state[c.islot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (fp && !pos_upsert(S, (int64_t)c.aid, c.sid, fa, fv)) {
+            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= S.A || lskip(S) || lfell(S)) return;
+    const int64_t d = S.ldelta[a];
+    if (d == 0) return;
+    const int32_t h = bal_lookup(S, a);
+    if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); return; }   // (cannot happen)
+    S.bal_val[h] = jladd(S.bal_val[h], d);
+    if (a == 0) {   // the tables' load (one thread), as Core's inserts check it
+        if (S.ctr[ci(C_POS_USED)] * 4 > ((unsigned long long)S.pos_mask + 1) * 3 ||
+            S.ctr[ci(C_BAL_USED)] * 2 > (unsigned long long)S.bal_mask + 1)
+            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+    }
+}
+
+// ---------------------------------------------------------------- launcher
+void launch_ledger_parallel(const DevState& S, const DevState* S_dev, const EpochIO& io, const EpochIO* io_dev,
+                            uint32_t max_trades, hipStream_t st) {
+    const uint32_t n = io.n;
+    auto cdiv = [](uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); };
+    const uint64_t nseq = (uint64_t)n + 2ull * max_trades;
+    (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
+    (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nseq, st);
+    (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
+    (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
+    (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_lcount, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
+    // offsets (in place) and the op count (LC_OPS, low word)
+    launch_excl_scan(S.lcnt, S.lcnt, n, S.lscan, reinterpret_cast<uint32_t*>(S.lctr + ci(LC_OPS)), st);
+    hipLaunchKernelGGL(k_lgen, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
+    RadixIO R{};
+    R.key0 = reinterpret_cast<const KG int32_t*>(S.lk0);
+    R.val0 = S.lv0;
+    R.keys[0] = S.lkey[0]; R.keys[1] = S.lkey[1];
+    R.vals[0] = S.lval[0]; R.vals[1] = S.lval[1];
+    R.ghist = S.lghist;
+    R.rank = nullptr;
+    R.none = 0;
+    R.n = n + max_trades;
+    R.n_dev = S.lctr + ci(LC_OPS);
+    R.passes = S.lpasses;
+    launch_radix(R, st);
+    hipLaunchKernelGGL(k_lseg, dim3(cdiv(n + max_trades + 1ull, 256)), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lchains, dim3(cdiv((uint32_t)S.A, 4)), dim3(256), 0, st, S, io);
+    const uint32_t gs = std::min<uint32_t>(cdiv(nseq, 256), 4096);
+    hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lrepair, dim3(1), dim3(64), 0, st, S_dev, io_dev);
+    hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 0);
+    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 1);
+    hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lbalances, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
+}
+
+}  // namespace kme

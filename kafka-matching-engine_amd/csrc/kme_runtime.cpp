@@ -272,6 +272,38 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.acct_demand, cfg->max_accounts);
         if (S.ledger_replay) ALLOC(S.vic, E);
     }
+    if (S.ledger_replay) {   // the parallel ledger pass (kme_ledger.hip); KME_LEDGER_SERIAL=1: the serial replay only
+        const uint64_t nops = (uint64_t)E + cfg->max_trades, nseq = (uint64_t)E + 2ull * cfg->max_trades;
+        const char* ls = std::getenv("KME_LEDGER_SERIAL");
+        S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && nseq < (1ull << 30) ? 1 : 0;
+        if (S.lpar) {
+            int bits = 0;
+            while ((1ull << bits) < ((uint64_t)cfg->max_accounts << 8)) ++bits;
+            S.lpasses = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+            S.lr_cap = 512;
+            S.le_cap = 16384;
+            S.lx_cap = 65536;
+            const uint64_t vk = pow2_at_least(std::min<uint64_t>(2 * nseq, 1ull << 22));
+            S.lvk_mask = vk - 1;
+            const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE - 1) / RADIX_TILE);
+            ALLOC(S.lcnt, E);
+            ALLOC(S.lscan, E / 4096 + 64);
+            ALLOC(S.lk0, nops); ALLOC(S.lv0, nops);
+            ALLOC(S.lkey[0], nops); ALLOC(S.lkey[1], nops);
+            ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
+            ALLOC(S.lghist, lh + lh / 4096 + 4096);
+            ALLOC(S.lop, nseq); ALLOC(S.lsid, nseq);
+            ALLOC(S.lchain, nops);
+            ALLOC(S.lvw, nseq); ALLOC(S.lvw_meta, nseq); ALLOC(S.lvw_tgt, nseq);
+            ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
+            ALLOC(S.ldelta, cfg->max_accounts);
+            ALLOC(S.lvk, vk);
+            ALLOC(S.lx, S.lx_cap);
+            ALLOC(S.ldirty, S.lr_cap);
+            ALLOC(S.lrscr, (4ull * S.lr_cap + 16ull * S.le_cap + 32ull * S.lr_cap + 32ull * S.le_cap + 4ull * S.le_cap) / 4);
+            ALLOC(S.lctr, (size_t)LC_N * CTR_STRIDE);
+        }
+    }
     if (exact_ledger) {
         const uint64_t lc = pow2_at_least(std::max<uint64_t>(2 * std::max<uint64_t>(cfg->ledger_capacity, 1024), 2048));
         if (lc > (1ull << 31)) { kme_destroy(e); return KME_E_INVALID; }
@@ -467,7 +499,8 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         }
         if (S.ledger_replay) {
             phase_begin(e, PH_REPLAY);
-            launch_ledger_replay(e->d_S, e->d_io, st);
+            if (S.lpar) launch_ledger_parallel(S, e->d_S, io, e->d_io, e->cfg.max_trades, st);
+            launch_ledger_replay(e->d_S, e->d_io, st);   // (works only when the parallel pass fell back)
             phase_end(e, PH_REPLAY);
         }
     } else {
@@ -526,6 +559,8 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     s.n_maker_visits = c[ci(C_TRADES)];               // every maker visit is one trade (KP:238-242)
     s.n_cancel_ok = c[ci(C_CANCEL_OK)];
     s.serial_fallback = c[ci(C_FALLBACK)] ? 1u : 0u;
+    s.ledger_repaired = (uint32_t)c[ci(C_LREPAIRED)];
+    s.ledger_serial = c[ci(C_LSERIAL)] ? 1u : 0u;
     s.n_effective = last_n;
     e->last_busy = c[ci(C_BUSY)];
     e->last_light = c[ci(C_LIGHT)];
@@ -1168,6 +1203,8 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme
         total.n_maker_visits += es.n_maker_visits;
         total.n_cancel_ok += es.n_cancel_ok;
         total.serial_fallback += es.serial_fallback;   // sub-epochs that ran serially
+        total.ledger_repaired += es.ledger_repaired;
+        total.ledger_serial += es.ledger_serial;
         if (rc != KME_OK) {
             // the results of the records before the fault (the reference forwarded and committed
             // them, KP:97, 124-125): out arrays, trade offsets and their trades

@@ -26,7 +26,7 @@ MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
           7: "FAILED"}
-ABI_VERSION = 5
+ABI_VERSION = 6
 FLAG_EXACT_LEDGER = 1
 FLAG_SERIAL_FALLBACK = 2   # FUNDED: an epoch whose funded proof fails runs serially (needs FLAG_EXACT_LEDGER)
 
@@ -57,7 +57,8 @@ class kme_epoch_status(C.Structure):
     _fields_ = [("status", C.c_int32), ("detail", C.c_int32), ("error_index", C.c_int64),
                 ("n_inputs", C.c_uint32), ("n_trades", C.c_uint32), ("n_orders", C.c_uint64),
                 ("n_rests", C.c_uint64), ("n_maker_visits", C.c_uint64), ("n_cancel_ok", C.c_uint64),
-                ("serial_fallback", C.c_uint32), ("n_effective", C.c_uint32)]
+                ("serial_fallback", C.c_uint32), ("n_effective", C.c_uint32), ("ledger_repaired", C.c_uint32),
+                ("ledger_serial", C.c_uint32)]
 
 
 FORWARD_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t)

@@ -1,0 +1,115 @@
+"""The exact ledger in parallel (kme_ledger.hip; SURVEY.md §8 row f next-2, KP:167-182, 276-287,
+325-333, 434-436): FUNDED matching with KME_FLAG_EXACT_LEDGER, Balances and Positions compared with
+the oracle after every epoch, in the three regimes of the parallel pass --
+
+* sparse keys (the C3 shape: many accounts x many symbols): chains independent, no repair;
+* value-keyed writes into live chains (hazard H2: a fill's setPosition(UUID, ...) under the old
+  position VALUE as key, which is also some account's real (aid, sid) key): the coupled chains are
+  replayed in arrival order (kme_epoch_status.ledger_repaired > 0), still bit-exact;
+* so many couplings that the epoch goes to the serial replay (ledger_serial = 1).
+
+Every stream also runs with KME_LEDGER_SERIAL=1 (the serial replay only): same tape, books, ledger.
+"""
+import numpy as np
+import pytest
+
+from kme import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, flags, serial_env, monkeypatch, check_every=True):
+    monkeypatch.setenv("KME_LEDGER_SERIAL", "1" if serial_env else "0")
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=E,
+                                                max_resting=1 << 21, max_trades=2 * E + (1 << 12), max_accounts=n_acc,
+                                                ledger_capacity=1 << 20, flags=flags))
+    o = oracle_mod.Oracle()
+    stats = []
+    parts = [setup] + [body.slice(a, min(len(body), a + E)) for a in range(0, len(body), E)]
+    for k, part in enumerate(parts):
+        r = eng.process(part)
+        got = r.tape_json(part)
+        o.process(part)
+        want = o.tape_text()
+        o.clear_tape()
+        assert got == want, f"epoch {k}: tape"
+        if check_every or k == len(parts) - 1:
+            assert eng.snapshot_ledger() == o.dump_ledger(), f"epoch {k}: ledger"
+        stats.append((int(r.status.ledger_repaired), int(r.status.ledger_serial)))
+    assert eng.snapshot_books() == o.dump_books()
+    ledger = eng.snapshot_ledger()
+    eng.close()
+    return stats, ledger
+
+
+def test_sparse_chains_in_parallel(kme_mod, oracle_mod, monkeypatch):
+    """The C3 shape scaled down: 8,192 symbols x 16,384 accounts, 2^17-record epochs."""
+    n_sym, n_acc, E = 8192, 16384, 1 << 17
+    body = W.uniform(4 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2001)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, led = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    assert all(s == 0 for _, s in stats[1:]), stats          # the parallel pass took every order epoch
+    _, led_serial = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, True,
+                         monkeypatch, check_every=False)
+    assert led == led_serial
+
+
+def test_value_keyed_writes_into_live_chains_are_replayed(kme_mod, oracle_mod, monkeypatch):
+    """64 accounts x 63 symbols with sizes around 50: a position's value (amount, available) ~ (50, 50)
+    is also the key of account 50's position on symbol 50, which the epoch reads -- the reference
+    clobbers it (KP:284, 434-436).  Short epochs keep each one's couplings to a few dozen chains, which
+    the repair replays in arrival order."""
+    n_sym, n_acc, E = 63, 64, 256
+    body = W.uniform(60 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2002)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, led = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    repaired = [r for r, s in stats if s == 0 and r > 0]
+    assert repaired, stats                                       # couplings replayed by the parallel pass
+    _, led_serial = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, True,
+                         monkeypatch, check_every=False)
+    assert led == led_serial
+
+
+def test_dense_couplings_take_the_serial_replay(kme_mod, oracle_mod, monkeypatch):
+    """The same universe in 2^15-record epochs: thousands of couplings per epoch, beyond the repair's
+    capacity -- those epochs take the serial replay, and the ledger is still the oracle's."""
+    n_sym, n_acc, E = 63, 64, 1 << 15
+    body = W.uniform(3 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2003)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, _ = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    assert any(s for _, s in stats[1:]), stats
+
+
+@pytest.mark.parametrize("kind", ["uniform", "cancel_replace"])
+def test_parallel_ledger_with_cancels_and_fallback_epochs(kme_mod, oracle_mod, monkeypatch, kind):
+    """Refunds (postRemoveAdjustments, value writes when a position blocks part of the order) and
+    KME_FLAG_SERIAL_FALLBACK epochs mixed with parallel ones: accounts topped up every third epoch, so
+    some epochs' proof fails and k_serial applies them (its own ledger), the others take the parallel
+    pass; the ledger equals the oracle's after each."""
+    n_sym, n_acc, ep = 512, 2048, 1 << 14
+    rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
+    rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
+    setup = W.Orders.from_rows(rows)
+    stream = (W.uniform(9 * ep, n_symbols=n_sym, n_accounts=n_acc, seed=2004) if kind == "uniform"
+              else W.cancel_replace(9 * ep, n_symbols=n_sym, n_accounts=n_acc, seed=2005))
+    topup = W.Orders.from_rows([(W.TRANSFER, 0, a, 0, 0, 120_000 if kind == "uniform" else 2_000_000_000)
+                                for a in range(n_acc)])
+    chunks = [setup]
+    for c in range(0, len(stream), 3 * ep):
+        chunks.append(topup)
+        chunks += [stream.slice(c + k, c + k + ep) for k in range(0, 3 * ep, ep)]
+    monkeypatch.setenv("KME_LEDGER_SERIAL", "0")
+    eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=ep,
+                                                max_resting=1 << 20, max_trades=4 * ep, max_accounts=n_acc,
+                                                ledger_capacity=1 << 18,
+                                                flags=kme_mod.FLAG_EXACT_LEDGER | kme_mod.FLAG_SERIAL_FALLBACK))
+    o = oracle_mod.Oracle()
+    for ch in chunks:
+        r = eng.process(ch)
+        got = r.tape_json(ch)
+        o.process(ch)
+        assert got == o.tape_text()
+        o.clear_tape()
+        assert eng.snapshot_ledger() == o.dump_ledger()
+    assert eng.snapshot_books() == o.dump_books()
+    eng.close()
