@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
             });
         }
         c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
-        c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0;
+        c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
         dsum = jladd(dsum, cd);
     }
     // the account's balance delta: a wavefront sum (wrap-around, order-free)
