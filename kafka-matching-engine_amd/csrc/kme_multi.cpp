@@ -43,6 +43,8 @@ struct Part {
     std::vector<void*> mem;
 };
 
+enum : int { kSlotIdle = 0, kSlotQueued, kSlotCollected, kSlotDone };
+
 constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '1'};
 struct MultiHeader {
     char magic[8];
@@ -62,6 +64,9 @@ struct kme_multi {
     std::vector<Part> part[2];             // per slot, per shard
     uint32_t slot_n[2] = {};
     kme_epoch_result slot_out[2] = {};
+    int slot_mode[2] = {};                 // kSlot*: the slot's epoch is queued on the shards, collected, or done
+    std::vector<kme_epoch_status> sst[2];  // per slot: the shards' statuses once collected
+    kme_epoch_status done[2] = {};         // per slot: the merged status of an epoch that ran at submit
     int inflight = 0;
     uint32_t sub_count = 0;
     int failed = 0;
@@ -129,6 +134,7 @@ kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* de
     const size_t E = cfg->max_epoch, T = cfg->max_trades;
     for (int slot = 0; slot < 2 && s == KME_OK; ++slot) {
         m->part[slot].resize(n);
+        m->sst[slot].resize(n);
         for (uint32_t k = 0; k < n && s == KME_OK; ++k) {
             Part& p = m->part[slot][k];
             auto get = [&](size_t bytes) -> void* {
@@ -205,21 +211,9 @@ static kme_status rebalance_enqueue(kme_multi* m) {
     return KME_OK;
 }
 
-extern "C" {
-
-kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
-    if (!m || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
-        !out->trades)
-        return KME_E_INVALID;
-    if (m->failed) return KME_E_FAILED;
-    if (n > m->cfg.max_epoch) return KME_E_CAPACITY;
-    if (m->inflight == 2) return KME_E_INVALID;
-    if (out->trades_cap < m->cfg.max_trades) return KME_E_INVALID;
-    if (m->n > 1 && m->rebalance_every && m->sub_count > 0 && ++m->since_rebalance >= m->rebalance_every) {
-        m->since_rebalance = 0;
-        if (kme_status s = rebalance_enqueue(m)) { m->failed = 1; return s; }
-    }
-    const int slot = (int)(m->sub_count & 1);
+// Routes records [a, a + n) of the caller's epoch to the shards (slot's part buffers) and queues
+// every shard's part as a host epoch.
+static kme_status split_submit(kme_multi* m, int slot, const kme_orders* in, uint32_t a, uint32_t n) {
     std::vector<Part>& parts = m->part[slot];
     std::vector<kme_orders_buf> bufs(m->n);
     std::vector<uint32_t> counts(m->n);
@@ -230,9 +224,10 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
         echo[k] = parts[k].echo;
         index[k] = parts[k].index;
     }
-    kme_status s = kme_router_split(m->router, in, n, bufs.data(), counts.data(), echo.data(), index.data());
+    const kme_orders sub{in->action + a, in->oid + a, in->aid + a, in->sid + a, in->price + a, in->size + a};
+    kme_status s = kme_router_split(m->router, &sub, n, bufs.data(), counts.data(), echo.data(), index.data());
     if (s != KME_OK) return s;
-    // (a shard that receives more than max_epoch records cannot happen: a part is a subset of the epoch)
+    // (a part is a subset of the epoch: it fits max_epoch)
     for (uint32_t k = 0; k < m->n; ++k) {
         Part& p = parts[k];
         p.count = counts[k];
@@ -243,41 +238,22 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
             return s;
         }
     }
-    m->slot_n[slot] = n;
-    m->slot_out[slot] = *out;
-    ++m->sub_count;
-    ++m->inflight;
     return KME_OK;
 }
 
-kme_status kme_multi_poll(kme_multi* m, int* done) {
-    if (!m || !done) return KME_E_INVALID;
-    *done = 1;
-    for (kme_engine* e : m->eng) {
-        int d = 0;
-        if (kme_status s = kme_poll(e, &d)) return s;
-        if (!d) { *done = 0; return KME_OK; }
-    }
-    return KME_OK;
+// Every shard's part of the slot's epoch completed (kme_wait, oldest first on each engine).
+static void collect(kme_multi* m, int slot) {
+    for (uint32_t k = 0; k < m->n; ++k) (void)kme_wait(m->eng[k], &m->sst[slot][k]);
+    m->slot_mode[slot] = kSlotCollected;
 }
 
-// Completes the oldest epoch: every shard's part, merged into input order.
-kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
-    if (!m) return KME_E_INVALID;
+// The shards' results of records [a, a + n) merged into the caller's arrays at record a and trade
+// `tbase` (out->trade_off[a] == tbase already); the status is relative to record a.
+static kme_epoch_status merge(kme_multi* m, int slot, uint32_t n, const kme_epoch_result& out, uint32_t a, uint32_t tbase) {
+    std::vector<Part>& parts = m->part[slot];
+    const std::vector<kme_epoch_status>& sst = m->sst[slot];
     kme_epoch_status tot{};
     tot.error_index = -1;
-    if (m->inflight == 0) {
-        tot.status = m->failed ? KME_E_FAILED : KME_OK;
-        if (st) *st = tot;
-        return (kme_status)tot.status;
-    }
-    const int slot = (int)((m->sub_count - (uint32_t)m->inflight) & 1);
-    --m->inflight;
-    std::vector<Part>& parts = m->part[slot];
-    const uint32_t n = m->slot_n[slot];
-    const kme_epoch_result& out = m->slot_out[slot];
-    std::vector<kme_epoch_status> sst(m->n);
-    for (uint32_t k = 0; k < m->n; ++k) (void)kme_wait(m->eng[k], &sst[k]);
     // the first record (input order) a shard did not answer: its fault, or everything after a refusal
     uint32_t limit = n;
     int32_t lim_status = KME_OK, lim_detail = 0;
@@ -295,7 +271,7 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
             lim_index = s.error_index >= 0 && (uint64_t)s.error_index < parts[k].count ? (int64_t)parts[k].index[s.error_index] : -1;
         }
     }
-    // OUT echoes and per-record trade counts (trade_off[i + 1] for now), each shard on its own thread
+    // OUT echoes and per-record trade counts (trade_off[a + i + 1] for now), each shard on its own thread
     auto scatter = [&](uint32_t k) {
         const Part& p = parts[k];
         const uint32_t* to = p.res.trade_off;
@@ -303,11 +279,11 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
             if (!p.echo[j]) continue;
             const uint32_t i = p.index[j];
             if (i >= limit) break;
-            out.out_action[i] = p.res.out_action[j];
-            out.out_size[i] = p.res.out_size[j];
-            out.out_prev[i] = p.res.out_prev[j];
-            out.out_flags[i] = p.res.out_flags[j];
-            out.trade_off[i + 1] = to[j + 1] - to[j];
+            out.out_action[a + i] = p.res.out_action[j];
+            out.out_size[a + i] = p.res.out_size[j];
+            out.out_prev[a + i] = p.res.out_prev[j];
+            out.out_flags[a + i] = p.res.out_flags[j];
+            out.trade_off[a + i + 1] = to[j + 1] - to[j];
         }
     };
     std::vector<std::thread> th;
@@ -315,19 +291,18 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
     scatter(0);
     for (auto& t : th) t.join();
     th.clear();
-    out.trade_off[0] = 0;
     uint64_t acc = 0;
     for (uint32_t i = 0; i < limit; ++i) {
-        acc += out.trade_off[i + 1];
-        if (acc > out.trades_cap) {   // the merged epoch's trades do not fit: its prefix that does
+        acc += out.trade_off[a + i + 1];
+        if (tbase + acc > out.trades_cap) {   // the merged epoch's trades do not fit: its prefix that does
             limit = i;
             lim_status = KME_E_CAPACITY;
             lim_detail = KME_D_CAP_TRADES;
             lim_index = i;
-            acc -= out.trade_off[i + 1];
+            acc -= out.trade_off[a + i + 1];
             break;
         }
-        out.trade_off[i + 1] = (uint32_t)acc;
+        out.trade_off[a + i + 1] = (uint32_t)(tbase + acc);
     }
     auto gather = [&](uint32_t k) {
         const Part& p = parts[k];
@@ -337,7 +312,7 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
             const uint32_t i = p.index[j];
             if (i >= limit) break;
             const uint32_t c = to[j + 1] - to[j];
-            if (c) std::memcpy(out.trades + out.trade_off[i], p.res.trades + to[j], (size_t)c * sizeof(kme_trade));
+            if (c) std::memcpy(out.trades + out.trade_off[a + i], p.res.trades + to[j], (size_t)c * sizeof(kme_trade));
         }
     };
     for (uint32_t k = 1; k < m->n; ++k) th.emplace_back(gather, k);
@@ -347,8 +322,8 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
         const Part& p = parts[k];
         for (uint32_t j = 0; j < p.count; ++j) {   // counted once: partition 0 answers account records
             if (!p.echo[j] || p.index[j] >= limit) continue;
-            const int32_t a = p.in.action[j];
-            tot.n_orders += (a == KME_BUY || a == KME_SELL || a == KME_CANCEL) ? 1 : 0;
+            const int32_t act = p.in.action[j];
+            tot.n_orders += (act == KME_BUY || act == KME_SELL || act == KME_CANCEL) ? 1 : 0;
         }
         if (sst[k].status == KME_OK) {
             tot.n_rests += sst[k].n_rests;
@@ -362,9 +337,121 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
     tot.status = lim_status;
     tot.detail = lim_detail;
     tot.error_index = lim_status == KME_OK ? -1 : lim_index;
-    // any fault leaves the shards out of step with one another (the others went past it): like the
-    // reference's dead stream thread, nothing further is accepted
-    if (lim_status != KME_OK) m->failed = 1;
+    return tot;
+}
+
+extern "C" {
+
+// An epoch of orders only is split and queued (asynchronous, as kme_submit_epoch_host).  An epoch
+// with account records runs now, in runs split at them (as kme_submit_epoch splits host epochs): the
+// funded proof books a transfer's credit from the next epoch on, so orders of an account funded in
+// the same epoch would not be provable; the epoch in flight before it is collected first.
+kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
+    if (!m || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
+        !out->trades)
+        return KME_E_INVALID;
+    if (m->failed) return KME_E_FAILED;
+    if (n > m->cfg.max_epoch) return KME_E_CAPACITY;
+    if (m->inflight == 2) return KME_E_INVALID;
+    if (out->trades_cap < m->cfg.max_trades) return KME_E_INVALID;
+    auto is_acct = [&](uint32_t i) { return in->action[i] == KME_CREATE_BALANCE || in->action[i] == KME_TRANSFER; };
+    bool mixed = false;
+    for (uint32_t i = 0; i < n && !mixed; ++i) mixed = is_acct(i);
+    const int slot = (int)(m->sub_count & 1);
+    auto rebalance = [&]() -> kme_status {
+        if (m->n > 1 && m->rebalance_every && m->sub_count > 0 && ++m->since_rebalance >= m->rebalance_every) {
+            m->since_rebalance = 0;
+            if (kme_status s = rebalance_enqueue(m)) { m->failed = 1; return s; }
+        }
+        return KME_OK;
+    };
+    if (!mixed) {
+        if (kme_status s = rebalance()) return s;
+        if (kme_status s = split_submit(m, slot, in, 0, n)) return s;
+        m->slot_mode[slot] = kSlotQueued;
+    } else {
+        if (m->inflight) {
+            const int other = slot ^ 1;
+            if (m->slot_mode[other] == kSlotQueued) collect(m, other);
+        }
+        kme_epoch_status tot{};
+        tot.error_index = -1;
+        tot.n_inputs = n;
+        out->trade_off[0] = 0;
+        uint32_t a = 0, tbase = 0;
+        while (a < n) {
+            const bool kind = is_acct(a);
+            uint32_t b = a;
+            while (b < n && is_acct(b) == kind) ++b;
+            if (!kind)
+                if (kme_status s = rebalance()) return s;
+            if (kme_status s = split_submit(m, slot, in, a, b - a)) return s;
+            collect(m, slot);
+            const kme_epoch_status r = merge(m, slot, b - a, *out, a, tbase);
+            tot.n_orders += r.n_orders; tot.n_rests += r.n_rests; tot.n_cancel_ok += r.n_cancel_ok;
+            tot.serial_fallback += r.serial_fallback;
+            tbase += r.n_trades;
+            if (r.status != KME_OK) {
+                tot.status = r.status;
+                tot.detail = r.detail;
+                tot.error_index = r.error_index >= 0 ? a + r.error_index : -1;
+                tot.n_effective = a + r.n_effective;
+                break;
+            }
+            a = b;
+            tot.n_effective = a;
+        }
+        tot.n_trades = tbase;
+        tot.n_maker_visits = tbase;
+        if (tot.status != KME_OK) m->failed = 1;
+        m->done[slot] = tot;
+        m->slot_mode[slot] = kSlotDone;
+    }
+    m->slot_n[slot] = n;
+    m->slot_out[slot] = *out;
+    ++m->sub_count;
+    ++m->inflight;
+    return KME_OK;
+}
+
+kme_status kme_multi_poll(kme_multi* m, int* done) {
+    if (!m || !done) return KME_E_INVALID;
+    *done = 1;
+    if (m->inflight == 0) return KME_OK;
+    const int slot = (int)((m->sub_count - (uint32_t)m->inflight) & 1);
+    if (m->slot_mode[slot] != kSlotQueued) return KME_OK;
+    for (kme_engine* e : m->eng) {   // (an engine's oldest epoch in flight is this slot's part)
+        int d = 0;
+        if (kme_status s = kme_poll(e, &d)) return s;
+        if (!d) { *done = 0; return KME_OK; }
+    }
+    return KME_OK;
+}
+
+// Completes the oldest epoch: every shard's part, merged into input order.
+kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
+    if (!m) return KME_E_INVALID;
+    if (m->inflight == 0) {
+        kme_epoch_status tot{};
+        tot.error_index = -1;
+        tot.status = m->failed ? KME_E_FAILED : KME_OK;
+        if (st) *st = tot;
+        return (kme_status)tot.status;
+    }
+    const int slot = (int)((m->sub_count - (uint32_t)m->inflight) & 1);
+    --m->inflight;
+    kme_epoch_status tot;
+    if (m->slot_mode[slot] == kSlotDone) {
+        tot = m->done[slot];
+    } else {
+        if (m->slot_mode[slot] == kSlotQueued) collect(m, slot);
+        m->slot_out[slot].trade_off[0] = 0;
+        tot = merge(m, slot, m->slot_n[slot], m->slot_out[slot], 0, 0);
+        // any fault leaves the shards out of step with one another (the others went past it): like
+        // the reference's dead stream thread, nothing further is accepted
+        if (tot.status != KME_OK) m->failed = 1;
+    }
+    m->slot_mode[slot] = kSlotIdle;
     if (st) *st = tot;
     return (kme_status)tot.status;
 }
