@@ -322,12 +322,8 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
             if (funded) {
                 const int32_t price = io.price[i], size = io.size[i];
                 const int64_t aid = io.aid[i];
-                if (price < 0 || price > 100 || size < 0) {
-                    raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
-                } else if (aid >= 0 && aid < S.A && !KME_DIAG_EMAP_NONEED) {
-                    const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
-                    atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
-                }
+                if (price < 0 || price > 100 || size < 0) raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
+                // (the per-account need: k_need, on a side stream beside k_route and the partition)
                 // k_route's work for the order, done here while its fields are in registers (the
                 // streaming stores overlap this kernel's atomics): symbol group, the packed record
                 // with the order's oid-table position, or the books.get == null reject (KP:202-203).
@@ -359,6 +355,38 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
         if (no) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)no);
         if (na) atomicAdd(&S.ctr[ci(C_ACCT_OPS)], (unsigned long long)na);
         if (ni) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)ni);
+    }
+}
+
+// FUNDED per-account reservation need of the epoch: sum over its BUY/SELL of the larger end of
+// checkBalance's risk (KP:172-176).  Memory-side atomics on a 8-byte-per-account array; the kernel
+// runs on a side stream concurrently with k_route and the partition (nothing there reads it), joined
+// before the matching.
+__global__ void __launch_bounds__(256) k_need(DevState S, EpochIO io) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
+        const int32_t a = io.action[i];
+        if (a != BUY && a != SELL) continue;
+        const int32_t price = io.price[i], size = io.size[i];
+        const int64_t aid = io.aid[i];
+        if (price < 0 || price > 100 || size < 0 || aid < 0 || aid >= S.A || KME_DIAG_EMAP_NONEED) continue;
+        const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
+        atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
+    }
+}
+
+// With account records in the epoch (k_ledger_funded has applied them), a BUY/SELL's acct_ok is
+// decided again (k_emap read the accounts as they stood before the epoch): runs after the join.
+__global__ void __launch_bounds__(256) k_acct_refresh(DevState S, EpochIO io) {
+    if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
+        const int32_t a = io.action[i];
+        if (a != BUY && a != SELL) continue;
+        const int32_t g = S.route_grp[i];
+        if (g < 0) continue;
+        const int64_t aid = io.aid[i];
+        const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
+        KG int32_t* w0 = reinterpret_cast<KG int32_t*>(&S.prec[2 * (size_t)i]);
+        *w0 = (*w0 & ~(1 << 16)) | ((acct_ok ? 1 : 0) << 16);
     }
 }
 
@@ -534,16 +562,8 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     int64_t tgt = -1;
     S.rest_slot[i] = (a == BUY || a == SELL) ? RS_PENDING : -1;
     io.n_trades[i] = 0;
-    if (funded && (a == BUY || a == SELL)) {   // routed by k_emap
+    if (funded && (a == BUY || a == SELL)) {   // routed by k_emap (acct_ok again: k_acct_refresh)
         if (S.fallback) S.cancel_tgt[i] = -1;
-        if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
-        // the epoch has account records (k_ledger_funded has applied them): acct_ok again
-        const int32_t g = S.route_grp[i];
-        if (g < 0) return;
-        const int64_t aid = io.aid[i];
-        const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
-        KG int32_t* w0 = reinterpret_cast<KG int32_t*>(&S.prec[2 * (size_t)i]);
-        *w0 = (*w0 & ~(1 << 16)) | ((acct_ok ? 1 : 0) << 16);
         return;
     }
     bool direct = false, ok = false, acct_ok = false;
@@ -3855,6 +3875,14 @@ void launch_epoch_reset(const DevState& S, hipStream_t st) {
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st) {
     const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
     hipLaunchKernelGGL(k_emap, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);
+}
+void launch_need(const DevState& S, const EpochIO& io, hipStream_t st) {
+    const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
+    hipLaunchKernelGGL(k_need, dim3(nb), dim3(256), 0, st, S, io);
+}
+void launch_acct_refresh(const DevState& S, const EpochIO& io, hipStream_t st) {
+    const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
+    hipLaunchKernelGGL(k_acct_refresh, dim3(nb), dim3(256), 0, st, S, io);
 }
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_funded, dim3(1), dim3(64), 0, st, S, io);

@@ -552,10 +552,13 @@ def test_multi_gpu_drop_in_equals_the_single_partition_tape(oracle_mod, tmp_path
 @pytest.mark.gpu
 @pytest.mark.parametrize("rebalance", [True, False])
 def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, rebalance):
-    """Every account funded with 1.25x its single-engine need over the whole stream, booked as a
+    """Every account funded with 1.5x its single-engine need over the whole stream, booked as a
     quarter on each of four shards.  The drop-in re-splits the pooled credit before every epoch, so
     every epoch stays provable and the tape is the oracle's; with re-splitting off
-    (KME_MULTI_REBALANCE_EVERY=0) some shard's share runs dry and the processor fails (UNFUNDED)."""
+    (KME_MULTI_REBALANCE_EVERY=0) some shard's share runs dry and the processor fails (UNFUNDED).
+    (A numpy model of the proof over this stream: the static split fails from epoch 6 at 1.5x, the
+    re-split holds at 1.5x; at 1.25x the 2^14-record epochs leave too few orders per account and
+    shard for the demand weights to follow, and a few pairs run dry.)"""
     monkeypatch.setenv("KME_MULTI_REBALANCE_EVERY", "1" if rebalance else "0")
     lib = _lib()
     j = FakeJni()
@@ -563,7 +566,7 @@ def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, r
     body = W.uniform(8 * E, n_symbols=n_sym, n_accounts=n_acc, seed=77)
     risk = np.where(body.action == W.BUY, body.size.astype(np.int64) * body.price,
                     np.where(body.action == W.SELL, body.size.astype(np.int64) * (100 - body.price.astype(np.int64)), 0))
-    credit = np.floor(np.bincount(body.aid, weights=risk, minlength=n_acc) * 1.25).astype(np.int64)
+    credit = np.floor(np.bincount(body.aid, weights=risk, minlength=n_acc) * 1.5).astype(np.int64)
     rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
     rows += [(W.TRANSFER, 0, a, 0, 0, int(credit[a])) for a in range(n_acc)]
     rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
