@@ -536,7 +536,7 @@ def main():
         build_id = kme.lib().kme_build_id().decode()
         traffic, pmc_derived, pmc_src = None, None, "PMC passes cover the default single-GPU configurations only"
         pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
-        # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round.sh),
+        # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round4.sh),
         # and counts only when it profiled this very build
         if world == 1 and not args.symbols and not args.mix and E == (1 << 22) and not flags:
             traffic, pmc_derived, pmc_src = pmc_for_build(pmc, build_id)

@@ -15,9 +15,10 @@
 // Work is O(records) in three parallel passes over a thread pool of the caller's call: (1) each
 // thread takes a contiguous range -- a symbol record's partition from a per-sid cache, and which
 // directory shard owns each BUY/SELL/CANCEL oid (a hash); (2) the records of each directory shard
-// are bucketed in arrival order (a counting sort over (range, shard)); (3) each thread owns one
-// directory shard and applies its records in arrival order -- a BUY/SELL records its partition, a
-// CANCEL takes it -- with the probe slots of the records a few ahead prefetched.  The directory slots
+// are bucketed in arrival order as 16-byte items (oid, input index, partition or cancel; a counting
+// sort over (range, shard)); (3) each thread owns one directory shard and streams its items -- a
+// BUY/SELL records its partition, a CANCEL takes it -- with the probe slots a few items ahead
+// prefetched.  The directory slots
 // are 16 bytes (oid + 1, partition: one cache line per probe) in 2 MiB-aligned memory advised for
 // huge pages (the directory outgrows every cache: each probe is a DRAM access, and with 4 KiB pages a
 // TLB miss too).  kme_router_split then counts and scatters each range's records per partition.
@@ -62,6 +63,13 @@ inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
+
+// one BUY/SELL/CANCEL for its directory shard: all pass (3) reads, so that its pass streams
+struct Item {
+    int64_t oid;
+    uint32_t i;        // input index
+    int32_t p;         // BUY/SELL: its partition; CANCEL: -1
+};
 
 struct Slot {
     uint64_t key;      // oid + 1 (0 = empty)
@@ -152,7 +160,7 @@ struct kme_router {
     int32_t* sym_part;                           // |sid| -> partition + 1 (0 = not computed), |sid| < 2^24
     // per call scratch
     std::vector<uint8_t> own;
-    std::vector<uint32_t> idx;
+    std::vector<Item> items;
     std::vector<int32_t> dest;
     bool oom = false;
 
@@ -230,19 +238,15 @@ static kme_status route(kme_router* r, const kme_orders* in, uint32_t n, int32_t
         }
     }
     start[D] = (uint32_t)acc;
-    r->idx.resize(acc);
-    uint32_t* idx = r->idx.data();
+    r->items.resize(acc);
+    Item* items = r->items.data();
     parallel(T, [&](uint32_t t) {
         uint32_t a, b;
         range(t, a, b);
         std::vector<uint32_t> o(&off[(size_t)t * D], &off[(size_t)t * D] + D);
-        o.push_back(0);                                      // (slot D: records with no directory work)
-        uint32_t sink;
         for (uint32_t i = a; i < b; ++i) {
             const uint32_t w = own[i];
-            uint32_t* dst = w < D ? &idx[o[w]] : &sink;
-            *dst = i;
-            o[w] += w < D;
+            if (w < D) items[o[w]++] = Item{in->oid[i], i, in->action[i] == A_CANCEL ? -1 : dest[i]};
         }
     });
     // (3) each directory shard applies its records in arrival order (a BUY/SELL records its
@@ -253,28 +257,26 @@ static kme_status route(kme_router* r, const kme_orders* in, uint32_t n, int32_t
         constexpr uint32_t AHEAD = 16;
         const uint32_t a = start[d], b = start[d + 1];
         for (uint32_t k = a; k < b; ++k) {
-            if (k + AHEAD < b) dir.prefetch(in->oid[idx[k + AHEAD]]);
-            const uint32_t i = idx[k];
-            const int64_t oid = in->oid[i];
-            const bool cancel = in->action[i] == A_CANCEL;
-            if (__builtin_expect(oid == -1, 0)) {
-                if (cancel) dest[i] = dir.has_m1 ? (int32_t)dir.m1_val : 0;
-                else { dir.has_m1 = true; dir.m1_val = (uint32_t)dest[i]; }
+            if (k + AHEAD < b) dir.prefetch(items[k + AHEAD].oid);
+            const Item it = items[k];
+            if (__builtin_expect(it.oid == -1, 0)) {
+                if (it.p < 0) dest[it.i] = dir.has_m1 ? (int32_t)dir.m1_val : 0;
+                else { dir.has_m1 = true; dir.m1_val = (uint32_t)it.p; }
                 continue;
             }
             if (__builtin_expect(2 * (dir.used + 1) > dir.mask + 1, 0) && !dir.grow()) {
                 oom.store(true, std::memory_order_relaxed);
                 return;
             }
-            Slot& sl = dir.probe(oid);
-            const uint64_t key = (uint64_t)oid + 1;
+            Slot& sl = dir.probe(it.oid);
+            const uint64_t key = (uint64_t)it.oid + 1;
             const bool found = sl.key == key;
-            if (cancel) {
-                dest[i] = found ? (int32_t)sl.val : 0;
+            if (it.p < 0) {
+                dest[it.i] = found ? (int32_t)sl.val : 0;
             } else {
                 dir.used += !found;
                 sl.key = key;
-                sl.val = (uint32_t)dest[i];
+                sl.val = (uint32_t)it.p;
             }
         }
     });

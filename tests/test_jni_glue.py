@@ -95,6 +95,10 @@ class FakeJni:
 def _lib():
     if not os.path.exists(CHECK_LIB):
         pytest.skip("integration/jni/libkme_jni_check.so not built (make -C kafka-matching-engine_amd/csrc)")
+    # libkme through kme.lib() first: it imports torch, so the glue's libkme binds torch's HIP
+    # runtime (a glue loaded first maps a second HIP runtime, and torch then sees no GPU)
+    import kme
+    kme.lib()
     lib = C.CDLL(CHECK_LIB)
     P, I, L = C.c_void_p, C.c_int32, C.c_int64
     lib.Java_GpuMatchingEngine_create.argtypes = [P, P, I, I, I, L, I, I, I, I, I, L]
