@@ -415,6 +415,7 @@ def main():
 
     lat, match_ms, bytes_alg, n_orders, n_trades = [], [], [], 0, 0
     mix = {"inputs": 0, "trades": 0, "rests": 0, "maker_visits": 0, "cancels_ok": 0}
+    ledger = {"epochs_parallel": 0, "epochs_serial_replay": 0, "chains_repaired": 0, "epochs_serial_fallback": 0}
     # --pipeline: two epochs in flight (kme.h), epoch k + 1 queued before epoch k is waited for, so
     # the GPU never idles on the host's turnaround between epochs (--serialize reads the
     # engine-owned results of each epoch, so it runs them one at a time)
@@ -446,6 +447,11 @@ def main():
         for name, v in (("inputs", st.n_inputs), ("trades", st.n_trades), ("rests", st.n_rests),
                      ("maker_visits", st.n_maker_visits), ("cancels_ok", st.n_cancel_ok)):
             mix[name] += int(v)
+        if flags & 1:   # the exact ledger: which pass kept each epoch's Balances / Positions
+            ledger["epochs_serial_fallback"] += int(st.serial_fallback != 0)
+            ledger["epochs_serial_replay"] += int(st.ledger_serial != 0)
+            ledger["epochs_parallel"] += int(st.serial_fallback == 0 and st.ledger_serial == 0)
+            ledger["chains_repaired"] += int(st.ledger_repaired)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -572,6 +578,7 @@ def main():
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
             "host_path": host_path,
+            "exact_ledger": ledger if flags & 1 else None,
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             # cancels that removed a resting order (KP:289-323) / cancels in the timed epochs

@@ -97,15 +97,15 @@ struct LChain {
     int64_t fa, fv;                // after the chain's last effect (fpres)
     int64_t delta;                 // the balance change of its effects
     uint32_t last_seq;             // arrival number of its last effect
-    uint32_t dirty;                // a value write into it precedes one of its reads (k_ldetect)
+    uint32_t dirty;                // in the repair rounds' run list (a value write into it preceded one of its reads)
     uint32_t late;                 // 1 + arrival number of the latest value write after its last effect
-    uint32_t rix;                  // 1 + index in k_lrepair's set
+    uint32_t rix;                  // 1 + the coupling list index of its first incoming value write (this round)
     int32_t aid, islot;            // islot: the entry's table slot at the start (-1: absent)
     uint8_t ipres, fpres, _p[6];
 };
 static_assert(sizeof(LChain) == 80, "LChain");
 // the ledger pass's counters (DevState::lctr, one line each)
-enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_N = 8 };
+enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
 
 // Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
 // counters never contend for one L2 line.
@@ -191,7 +191,7 @@ struct DevState {
     KG unsigned long long* dbg;     // diagnostic stamps (KME_STAMPS builds), G x 16 words
     // FUNDED + exact ledger, applied in parallel (kme_ledger.hip; lpar = 0: the serial replay)
     int32_t lpar, lpasses;
-    uint32_t lr_cap, le_cap, lx_cap, _lpad;
+    uint32_t lr_cap, lx_cap, lc_cap, lrounds;
     uint64_t lvk_mask;
     KG uint32_t* lcnt;                // per record: its ops, then their offset
     KG uint32_t* lscan;               // scan scratch
@@ -209,9 +209,11 @@ struct DevState {
     KG uint32_t* lseg;                // per account: its first sorted op
     KG int64_t* ldelta;               // per account: the epoch's balance change
     KG ulonglong4* lvk;               // value-key table: hash, 1 + latest arrival, key
-    KG uint32_t* lx;                  // couplings (arrival numbers of the value writes)
-    KG uint32_t* ldirty;              // the chains they write into
-    KG uint32_t* lrscr;               // k_lrepair scratch
+    KG uint32_t* lx;                  // couplings: arrival numbers of value writes into chains that read later
+    KG uint32_t* lxn;                 //   per coupling: 1 + the next one into the same chain (this round)
+    KG uint8_t* lxmark;               // per arrival number: listed in lx
+    KG uint32_t* lrun;                // the repair rounds' run list (chain heads)
+    KG uint32_t* lchg;                // the value writes a repair round changed
     KG unsigned long long* lctr;      // LC_N x CTR_STRIDE words
 };
 

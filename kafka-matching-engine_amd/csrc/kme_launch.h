@@ -35,8 +35,7 @@ void launch_radix(const RadixIO& R, hipStream_t st);
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st);
 // FUNDED + exact ledger: the epoch's ledger effects in parallel (kme_ledger.hip); the serial replay
 // (launch_ledger_replay) runs after it and does the work only when this path fell back
-void launch_ledger_parallel(const DevState& S, const DevState* S_dev, const EpochIO& io, const EpochIO* io_dev,
-                            uint32_t max_trades, hipStream_t st);
+void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_trades, hipStream_t st);
 
 // FUNDED pipeline
 void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch

@@ -19,10 +19,12 @@
 //     434-436): a "value write" to the key (amount, available).  One lane applies a chain's ops in
 //     arrival order and records its value writes.
 //   * A value write whose key is another chain of this epoch, read after the write, couples the two
-//     chains: the reference clobbers that real position.  k_ldetect finds them; k_lrepair replays the
-//     chains involved in arrival order on one wavefront, growing the set until no new coupling appears.
-//     More than a few hundred couplings (streams over few accounts and symbols, where almost every
-//     position value is also some live key) send the epoch to the serial replay (k_ledger_replay).
+//     chains: the reference clobbers that real position.  k_ldetect finds them; repair rounds re-run
+//     the coupled chains in parallel, each with its incoming value writes merged in arrival order,
+//     until a fixed point (k_lr_link / k_lr_run / k_lr_detect).  At C3 (65,536 accounts x 65,536
+//     symbols) thousands of position values per epoch are also live keys -- (amount, available) ~
+//     (50, 50) is account 50's position on symbol 50.  No fixed point within S.lrounds rounds, or
+//     past a capacity, sends the epoch to the serial replay (k_ledger_replay).
 //     Value writes to keys no chain of the epoch reads commit last-writer-wins (latest arrival).
 //
 // Ops are compacted in arrival order, one per (record, chain) -- a BUY/SELL's checkBalance with its
@@ -392,6 +394,15 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
 
 // ---------------------------------------------------------------- 4. couplings between chains
 // A value write into a chain of this epoch that the chain reads afterwards (seq < its last effect).
+KDEV bool coupling(const DevState& S, uint32_t s, uint32_t meta, int32_t c) {
+    return (meta & 3u) && c >= 0 && (uint32_t)c != (meta >> 2) && s < S.lchain[c].last_seq;
+}
+KDEV void list_coupling(const DevState& S, uint32_t s) {
+    if (S.lxmark[s]) return;                     // (one writer per s: no race)
+    S.lxmark[s] = 1;
+    const unsigned long long x = atomicAdd(lc(S, LC_CROSS), 1ull);
+    if (x < S.lx_cap) S.lx[x] = s; else lfallback(S);
+}
 __global__ void __launch_bounds__(256) k_ldetect(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0) return;
     const uint32_t ns = lseqs(S, io);
@@ -401,131 +412,123 @@ __global__ void __launch_bounds__(256) k_ldetect(DevState S, EpochIO io) {
         const long4 w = S.lvw[s];
         const int32_t c = find_chain(S, w.x, w.y);
         S.lvw_tgt[s] = c;
-        if (c < 0 || (uint32_t)c == (meta >> 2) || s > S.lchain[c].last_seq) continue;
-        const unsigned long long x = atomicAdd(lc(S, LC_CROSS), 1ull);
-        if (x < S.lx_cap) S.lx[x] = s;
-        if (atomicExch(&S.lchain[c].dirty, 1u) == 0u) {
-            const unsigned long long d = atomicAdd(lc(S, LC_DIRTY), 1ull);
-            if (d < S.lr_cap) S.ldirty[d] = (uint32_t)c;
-        }
+        if (coupling(S, s, meta, c)) list_coupling(S, s);
     }
 }
 
-// ---------------------------------------------------------------- 5. the coupled chains, in arrival order
-// One thread (the chains involved are few): the effects of the chains in the set R and the value
-// writes into them from chains outside R, sorted by arrival number and applied in that order; a value
-// write of an R chain into a chain outside R that reads it later adds that chain to R and starts over.
-// Converged: the chains' final states, balance deltas and value writes are replaced.  Too many chains
-// or effects: the epoch goes to the serial replay.
-struct LEvent { uint32_t seq, r, op, ext; };   // ext: 1 = a value write from outside R into chain r
-__global__ void __launch_bounds__(64) k_lrepair(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
-    const DevState& S = *Sp;
-    const EpochIO& io = *iop;
-    if (threadIdx.x != 0 || lskip(S) || lops(S) == 0) return;
-    const uint32_t nd = (uint32_t)S.lctr[ci(LC_DIRTY)], nx = (uint32_t)S.lctr[ci(LC_CROSS)];
-    if (nd == 0) return;
-    if (nd > S.lr_cap || nx > S.lx_cap) { lfallback(S); return; }
-    KG uint32_t* R = S.lrscr;                                   // chain heads of the set
-    KG LEvent* ev = reinterpret_cast<KG LEvent*>(S.lrscr + S.lr_cap);
-    KG int64_t* st = reinterpret_cast<KG int64_t*>(ev + S.le_cap);   // per R chain: a, v, present, delta
-    KG long4* nw = reinterpret_cast<KG long4*>(st + 4 * (size_t)S.lr_cap);   // per event: the new value write
-    KG uint32_t* nk = reinterpret_cast<KG uint32_t*>(nw + S.le_cap);
-    uint32_t nr = 0;
-    for (uint32_t d = 0; d < nd; ++d) { R[nr] = S.ldirty[d]; S.lchain[R[nr]].rix = nr + 1; ++nr; }
+// ---------------------------------------------------------------- 5. repair rounds
+// The coupled chains re-run in parallel, each with the value writes into it merged into its own
+// effects in arrival order, until nothing changes (a fixed point: a value write only affects later
+// effects, so after round r every effect whose causal chain of couplings is at most r deep is
+// final).  Round: (a) k_lr_link threads each chain's incoming couplings into a list and adds the
+// chain to the run list (which only grows: a chain whose coupling went away re-runs without it);
+// (b) k_lr_run re-runs every chain of the run list from its start state -- new final state, balance
+// delta (the difference goes to the account's sum) and value writes, the changed ones listed; (c)
+// k_lr_detect re-targets the changed value writes and lists new couplings; no change = converged
+// (LC_DONE: the later rounds' launches return at once).  Not converged in S.lrounds rounds, or past a
+// capacity: the epoch goes to the serial replay.
+KDEV bool lr_active(const DevState& S) {
+    return !lskip(S) && lops(S) != 0 && S.lctr[ci(LC_DONE)] == 0 && !lfell(S);
+}
+__global__ void __launch_bounds__(256) k_lr_link(DevState S) {
+    if (!lr_active(S)) return;
+    const uint32_t nx = (uint32_t)S.lctr[ci(LC_CROSS)];
+    const uint32_t x0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x0 == 0) S.lctr[ci(LC_CHG)] = 0;         // (the run kernel's list, filled after this launch)
+    for (uint32_t x = x0; x < nx; x += gridDim.x * blockDim.x) {
+        const uint32_t s = S.lx[x];
+        const int32_t c = S.lvw_tgt[s];
+        if (!coupling(S, s, S.lvw_meta[s], c)) continue;
+        S.lxn[x] = atomicExch(&S.lchain[c].rix, x + 1);
+        if (atomicExch(&S.lchain[c].dirty, 1u) == 0u) {
+            const unsigned long long d = atomicAdd(lc(S, LC_DIRTY), 1ull);
+            if (d < S.lr_cap) S.lrun[d] = (uint32_t)c; else lfallback(S);
+        }
+    }
+}
+constexpr int LR_IN = 32;   // incoming value writes one chain takes in a round (more: the serial replay)
+__global__ void __launch_bounds__(256) k_lr_run(DevState S, EpochIO io) {
+    if (!lr_active(S)) return;
+    const uint32_t nd = (uint32_t)min(S.lctr[ci(LC_DIRTY)], (unsigned long long)S.lr_cap);
     const KG uint32_t* K = skeys(S);
     const KG uint32_t* V = svals(S);
-    for (uint32_t round = 0; round < 32; ++round) {
-        // the events
-        uint32_t ne = 0;
-        bool over = false;
-        for (uint32_t r = 0; r < nr && !over; ++r) {
-            const uint32_t head = R[r];
-            const int64_t aid = S.lchain[head].aid, sid = S.lchain[head].sid;
-            const uint32_t hi = S.lseg[aid + 1];
-            for (uint32_t p = head; p < hi && K[p] == K[head] && !over; ++p) {
-                const uint32_t sq = V[p];
-                if (S.lsid[sq] != sid) continue;
-                for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
-                    if (ne == S.le_cap) { over = true; return; }
-                    ev[ne++] = LEvent{es, r, sq, 0};
-                });
-            }
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nd; d += gridDim.x * blockDim.x) {
+        const uint32_t head = S.lrun[d];
+        KG LChain& c = S.lchain[head];
+        // the incoming value writes, in arrival order
+        uint32_t in[LR_IN];
+        int nin = 0;
+        for (uint32_t x = c.rix; x != 0; x = S.lxn[x - 1]) {
+            if (nin == LR_IN) { lfallback(S); return; }
+            const uint32_t s = S.lx[x - 1];
+            int k = nin++;
+            for (; k > 0 && in[k - 1] > s; --k) in[k] = in[k - 1];
+            in[k] = s;
         }
-        for (uint32_t x = 0; x < nx && !over; ++x) {
-            const uint32_t s = S.lx[x];
-            const int32_t c = S.lvw_tgt[s];
-            const uint32_t src = S.lvw_meta[s] >> 2;
-            if (c < 0 || S.lchain[c].rix == 0 || S.lchain[src].rix != 0) continue;   // into R, from outside R
-            if (ne == S.le_cap) { over = true; break; }
-            ev[ne++] = LEvent{s, S.lchain[c].rix - 1, 0, 1};
-        }
-        if (over) { lfallback(S); break; }
-        // arrival order (shell sort: a few thousand events at most)
-        for (uint32_t gap = ne / 2; gap > 0; gap /= 2)
-            for (uint32_t i = gap; i < ne; ++i) {
-                const LEvent t = ev[i];
-                uint32_t j = i;
-                for (; j >= gap && ev[j - gap].seq > t.seq; j -= gap) ev[j] = ev[j - gap];
-                ev[j] = t;
-            }
-        for (uint32_t r = 0; r < nr; ++r) {
-            const KG LChain& c = S.lchain[R[r]];
-            st[4 * r] = c.ia; st[4 * r + 1] = c.iv; st[4 * r + 2] = c.ipres; st[4 * r + 3] = 0;
-        }
-        bool grown = false;
-        for (uint32_t e = 0; e < ne && !grown; ++e) {
-            const LEvent E = ev[e];
-            PState P{st[4 * E.r], st[4 * E.r + 1], st[4 * E.r + 2] != 0};
-            VWrite w;
-            if (E.ext) {
-                const long4 x = S.lvw[E.seq];
-                w = VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[E.seq] & 3u};
-                write_into(P, w);
-            } else {
-                const KG LChain& c = S.lchain[R[E.r]];
-                st[4 * E.r + 3] = jladd(st[4 * E.r + 3], apply_effect(S, io, E.op, E.seq, c.aid, c.sid, P, w));
-                nw[e] = make_long4(w.k0, w.k1, w.v0, w.v1);
-                nk[e] = w.kind;
-                if (w.kind && !(w.k0 == c.aid && w.k1 == c.sid)) {
-                    const int32_t t = find_chain(S, w.k0, w.k1);
-                    if (t >= 0 && S.lchain[t].rix != 0) {          // into a chain of R: applied in order
-                        const uint32_t tr = S.lchain[t].rix - 1;
-                        PState Q{st[4 * tr], st[4 * tr + 1], st[4 * tr + 2] != 0};
-                        write_into(Q, w);
-                        st[4 * tr] = Q.a; st[4 * tr + 1] = Q.v; st[4 * tr + 2] = Q.present;
-                    } else if (t >= 0 && E.seq < S.lchain[t].last_seq) {   // a new coupling
-                        if (nr == S.lr_cap) { lfallback(S); return; }
-                        R[nr] = (uint32_t)t;
-                        S.lchain[t].rix = ++nr;
-                        grown = true;
-                    }
+        c.rix = 0;
+        const int64_t aid = c.aid, sid = c.sid;
+        PState P{c.ia, c.iv, c.ipres != 0};
+        int64_t cd = 0;
+        int q = 0;
+        const uint32_t hi = S.lseg[aid + 1];
+        for (uint32_t p = head; p < hi && K[p] == K[head]; ++p) {
+            const uint32_t sq = V[p];
+            if (p != head && S.lsid[sq] != sid) continue;
+            for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
+                for (; q < nin && in[q] < es; ++q) {
+                    const long4 x = S.lvw[in[q]];
+                    write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[in[q]] & 3u});
                 }
-            }
-            st[4 * E.r] = P.a; st[4 * E.r + 1] = P.v; st[4 * E.r + 2] = P.present;
+                VWrite w;
+                cd = jladd(cd, apply_effect(S, io, sq, es, aid, sid, P, w));
+                const uint32_t om = S.lvw_meta[es];
+                const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
+                bool changed = (om & 3u) != (nm & 3u);
+                if (!changed && w.kind) {
+                    const long4 ow = S.lvw[es];
+                    changed = ow.x != w.k0 || ow.y != w.k1 || (w.kind == VW_PUT && (ow.z != w.v0 || ow.w != w.v1));
+                }
+                if (changed) {
+                    S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                    S.lvw_meta[es] = nm;
+                    const unsigned long long k = atomicAdd(lc(S, LC_CHG), 1ull);
+                    if (k < S.lc_cap) S.lchg[k] = es; else lfallback(S);
+                }
+            });
         }
-        if (grown) continue;
-        // converged: the chains' results and value writes replace the first pass's
-        for (uint32_t e = 0; e < ne; ++e) {
-            if (ev[e].ext) continue;
-            S.lvw[ev[e].seq] = nw[e];
-            S.lvw_meta[ev[e].seq] = nk[e] | (R[ev[e].r] << 2);
-            if (nk[e]) {
-                const long4 x = nw[e];
-                S.lvw_tgt[ev[e].seq] = find_chain(S, x.x, x.y);
-            }
+        c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
+        atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[aid]), (unsigned long long)jlsub(cd, c.delta));
+        c.delta = cd;
+    }
+}
+__global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_round) {
+    if (!lr_active(S)) return;
+    const uint32_t nc = (uint32_t)min(S.lctr[ci(LC_CHG)], (unsigned long long)S.lc_cap);
+    const uint32_t k0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (nc == 0) {                                // converged
+        if (k0 == 0) {
+            S.lctr[ci(LC_DONE)] = 1;
+            const unsigned long long nd = S.lctr[ci(LC_DIRTY)];
+            S.lctr[ci(LC_REPAIRED)] = nd;
+            S.ctr[ci(C_LREPAIRED)] = nd;
         }
-        for (uint32_t r = 0; r < nr; ++r) {
-            KG LChain& c = S.lchain[R[r]];
-            c.fa = st[4 * r]; c.fv = st[4 * r + 1]; c.fpres = st[4 * r + 2] != 0;
-            S.ldelta[c.aid] = jladd(S.ldelta[c.aid], jlsub(st[4 * r + 3], c.delta));
-            c.delta = st[4 * r + 3];
-            c.rix = 0;
-        }
-        atomicAdd(lc(S, LC_REPAIRED), (unsigned long long)nr);
-        S.ctr[ci(C_LREPAIRED)] = nr;
         return;
     }
-    lfallback(S);   // (no convergence in 32 rounds)
+    if (last_round) {                             // still changing: the serial replay
+        if (k0 == 0) lfallback(S);
+        return;
+    }
+    for (uint32_t k = k0; k < nc; k += gridDim.x * blockDim.x) {
+        const uint32_t s = S.lchg[k];
+        const uint32_t meta = S.lvw_meta[s];
+        int32_t c = -1;
+        if (meta & 3u) {
+            const long4 w = S.lvw[s];
+            c = find_chain(S, w.x, w.y);
+        }
+        S.lvw_tgt[s] = c;
+        if (coupling(S, s, meta, c)) list_coupling(S, s);
+    }
 }
 
 // ---------------------------------------------------------------- 6. commit
@@ -648,13 +651,13 @@ __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
 }
 
 // ---------------------------------------------------------------- launcher
-void launch_ledger_parallel(const DevState& S, const DevState* S_dev, const EpochIO& io, const EpochIO* io_dev,
-                            uint32_t max_trades, hipStream_t st) {
+void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_trades, hipStream_t st) {
     const uint32_t n = io.n;
     auto cdiv = [](uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); };
     const uint64_t nseq = (uint64_t)n + 2ull * max_trades;
     (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
     (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nseq, st);
+    (void)hipMemsetAsync(S.lxmark, 0, nseq, st);
     (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
     (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
     (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
@@ -679,7 +682,12 @@ void launch_ledger_parallel(const DevState& S, const DevState* S_dev, const Epoc
     hipLaunchKernelGGL(k_lchains, dim3(cdiv((uint32_t)S.A, 4)), dim3(256), 0, st, S, io);
     const uint32_t gs = std::min<uint32_t>(cdiv(nseq, 256), 4096);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lrepair, dim3(1), dim3(64), 0, st, S_dev, io_dev);
+    // (with no coupling the first round's link finds none, runs nothing and the detect converges)
+    for (uint32_t r = 0; r < S.lrounds; ++r) {
+        hipLaunchKernelGGL(k_lr_link, dim3(64), dim3(256), 0, st, S);
+        hipLaunchKernelGGL(k_lr_run, dim3(256), dim3(256), 0, st, S, io);
+        hipLaunchKernelGGL(k_lr_detect, dim3(64), dim3(256), 0, st, S, (uint32_t)(r + 1 == S.lrounds));
+    }
     hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 0);
     hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 1);

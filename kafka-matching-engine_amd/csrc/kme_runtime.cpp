@@ -286,9 +286,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             int bits = 0;
             while ((1ull << bits) < ((uint64_t)cfg->max_accounts << 8)) ++bits;
             S.lpasses = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
-            S.lr_cap = 512;
-            S.le_cap = 16384;
-            S.lx_cap = 65536;
+            S.lr_cap = 1u << 18;     // chains re-run by the repair rounds
+            S.lx_cap = 1u << 19;     // couplings
+            S.lc_cap = 1u << 20;     // value writes changed in one round
+            S.lrounds = 8;           // repair rounds before the serial replay (KME_LEDGER_ROUNDS: tests)
+            if (const char* v = std::getenv("KME_LEDGER_ROUNDS")) S.lrounds = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
             const uint64_t vk = pow2_at_least(std::min<uint64_t>(2 * nseq, 1ull << 22));
             S.lvk_mask = vk - 1;
             const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE - 1) / RADIX_TILE);
@@ -304,9 +306,10 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
             ALLOC(S.ldelta, cfg->max_accounts);
             ALLOC(S.lvk, vk);
-            ALLOC(S.lx, S.lx_cap);
-            ALLOC(S.ldirty, S.lr_cap);
-            ALLOC(S.lrscr, (4ull * S.lr_cap + 16ull * S.le_cap + 32ull * S.lr_cap + 32ull * S.le_cap + 4ull * S.le_cap) / 4);
+            ALLOC(S.lx, S.lx_cap); ALLOC(S.lxn, S.lx_cap);
+            ALLOC(S.lxmark, nseq);
+            ALLOC(S.lrun, S.lr_cap);
+            ALLOC(S.lchg, S.lc_cap);
             ALLOC(S.lctr, (size_t)LC_N * CTR_STRIDE);
         }
     }
@@ -522,7 +525,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         }
         if (S.ledger_replay) {
             phase_begin(e, PH_REPLAY);
-            if (S.lpar) launch_ledger_parallel(S, e->d_S, io, e->d_io, e->cfg.max_trades, st);
+            if (S.lpar) launch_ledger_parallel(S, io, e->cfg.max_trades, st);
             launch_ledger_replay(e->d_S, e->d_io, st);   // (works only when the parallel pass fell back)
             phase_end(e, PH_REPLAY);
         }

@@ -5,8 +5,10 @@ the oracle after every epoch, in the three regimes of the parallel pass --
 * sparse keys (the C3 shape: many accounts x many symbols): chains independent, no repair;
 * value-keyed writes into live chains (hazard H2: a fill's setPosition(UUID, ...) under the old
   position VALUE as key, which is also some account's real (aid, sid) key): the coupled chains are
-  replayed in arrival order (kme_epoch_status.ledger_repaired > 0), still bit-exact;
-* so many couplings that the epoch goes to the serial replay (ledger_serial = 1).
+  re-run in parallel rounds, each with its incoming value writes in arrival order, to a fixed point
+  (kme_epoch_status.ledger_repaired > 0), still bit-exact;
+* couplings the rounds cannot settle (KME_LEDGER_ROUNDS=1 while a second round is needed; more than
+  32 value writes into one chain): the epoch goes to the serial replay (ledger_serial = 1).
 
 Every stream also runs with KME_LEDGER_SERIAL=1 (the serial replay only): same tape, books, ledger.
 """
@@ -18,8 +20,9 @@ from kme import workloads as W
 pytestmark = pytest.mark.gpu
 
 
-def _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, flags, serial_env, monkeypatch, check_every=True):
+def _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, flags, serial_env, monkeypatch, check_every=True, rounds=8):
     monkeypatch.setenv("KME_LEDGER_SERIAL", "1" if serial_env else "0")
+    monkeypatch.setenv("KME_LEDGER_ROUNDS", str(rounds))
     eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=n_sym + 1, max_epoch=E,
                                                 max_resting=1 << 21, max_trades=2 * E + (1 << 12), max_accounts=n_acc,
                                                 ledger_capacity=1 << 20, flags=flags))
@@ -70,14 +73,39 @@ def test_value_keyed_writes_into_live_chains_are_replayed(kme_mod, oracle_mod, m
     assert led == led_serial
 
 
-def test_dense_couplings_take_the_serial_replay(kme_mod, oracle_mod, monkeypatch):
-    """The same universe in 2^15-record epochs: thousands of couplings per epoch, beyond the repair's
-    capacity -- those epochs take the serial replay, and the ledger is still the oracle's."""
+def test_dense_couplings(kme_mod, oracle_mod, monkeypatch):
+    """The same universe in 2^15-record epochs: thousands of couplings per epoch, many value writes
+    into the same few chains -- whichever pass keeps an epoch (the rounds or the serial replay), the
+    ledger is the oracle's."""
     n_sym, n_acc, E = 63, 64, 1 << 15
     body = W.uniform(3 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2003)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
     stats, _ = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    assert all(r > 0 or s for r, s in stats[1:]), stats        # every order epoch coupled
+
+
+def test_unsettled_couplings_take_the_serial_replay(kme_mod, oracle_mod, monkeypatch):
+    """One repair round only: an epoch whose couplings need a second round (a re-run chain's value
+    writes changed) goes to the serial replay, and the ledger is still the oracle's."""
+    n_sym, n_acc, E = 63, 64, 1 << 12
+    body = W.uniform(8 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2006)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, _ = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch,
+                    rounds=1)
     assert any(s for _, s in stats[1:]), stats
+
+
+def test_c3_shape_couplings_settle_in_parallel(kme_mod, oracle_mod, monkeypatch):
+    """The bench's C3 universe (65,536 accounts x 65,536 symbols) in 2^18-record epochs: the position
+    values (amount, available) of small magnitude are also live (aid, sid) keys, so every epoch has
+    couplings; the rounds settle them (no serial replay) and the ledger is the oracle's."""
+    n_sym, n_acc, E = 65_536, 65_536, 1 << 18
+    body = W.uniform(3 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2007)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, _ = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch,
+                    check_every=False)
+    assert all(s == 0 for _, s in stats[1:]), stats
+    print("c3-shape epochs (chains repaired, serial):", stats[1:])
 
 
 @pytest.mark.parametrize("kind", ["uniform", "cancel_replace"])
