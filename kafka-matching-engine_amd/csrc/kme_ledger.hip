@@ -68,47 +68,38 @@ KDEV uint32_t ld_state(const KG uint32_t* p) { return __hip_atomic_load(p, __ATO
 KDEV uint32_t pos_hash(const DevState& S, int64_t k0, int64_t k1) {
     return (uint32_t)mix64((uint64_t)k0 * 0x9e3779b97f4a7c15ull ^ mix64((uint64_t)k1)) & S.pos_mask;
 }
-// positions.get(UUID(k0, k1)): the slot of a live entry, or -1
+// positions.get(UUID(k0, k1)): the slot of a live entry, or -1.  The ledger pass never inserts and
+// reads the table in one kernel (updates in place and deletes in k_lcommit, inserts in k_linsert), so
+// plain loads see every earlier kernel's writes.
 KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
     uint32_t h = pos_hash(S, k0, k1);
     for (uint32_t p = 0; p <= S.pos_mask; ++p) {
-        const uint32_t st = ld_state(&S.pos_state[h]);
+        const uint32_t st = S.pos_state[h];
         if (st == 0) return -1;
         if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) return (int32_t)h;
         h = (h + 1) & S.pos_mask;
     }
     return -1;
 }
-// positions.put by the one thread that commits this key: update in place, or claim a free slot (the
-// probe chain's first tombstone, else its empty end) by CAS to the transient state 3, write the
-// entry, publish state 1.  A prober meeting state 3 passes it (another key: every key has one
-// committing thread).  false = no room.
-KDEV bool pos_upsert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1) {
-    for (int attempt = 0; attempt < 4096; ++attempt) {
-        uint32_t h = pos_hash(S, k0, k1);
-        int32_t tomb = -1;
-        uint32_t p = 0;
-        for (; p <= S.pos_mask; ++p) {
-            const uint32_t st = ld_state(&S.pos_state[h]);
-            if (st == 0) break;
-            if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) {
-                S.pos[h].v0 = v0;
-                S.pos[h].v1 = v1;
-                return true;
-            }
-            if (st == 2 && tomb < 0) tomb = (int32_t)h;
-            h = (h + 1) & S.pos_mask;
+// positions.put of a key known to be absent (k_linsert: every key inserted by one thread, no reader
+// in the kernel): the first free slot (empty or tombstone) of its probe sequence, claimed by CAS.
+// Returns 1 when it took an empty slot (the table's load grows), 0 for a tombstone, -1: no room.
+KDEV int pos_insert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1) {
+    uint32_t h = pos_hash(S, k0, k1);
+    for (uint32_t p = 0; p <= S.pos_mask; ++p) {
+        const uint32_t st = S.pos_state[h];
+        if ((st == 0 || st == 2) && atomicCAS((unsigned int*)&S.pos_state[h], st, 1u) == st) {
+            S.pos[h].k0 = k0; S.pos[h].k1 = k1; S.pos[h].v0 = v0; S.pos[h].v1 = v1;
+            return st == 0 ? 1 : 0;
         }
-        if (p > S.pos_mask && tomb < 0) return false;
-        const uint32_t at = tomb >= 0 ? (uint32_t)tomb : h, expect = tomb >= 0 ? 2u : 0u;
-        if (atomicCAS((unsigned int*)&S.pos_state[at], expect, 3u) != expect) continue;   // taken meanwhile
-        S.pos[at].k0 = k0; S.pos[at].k1 = k1; S.pos[at].v0 = v0; S.pos[at].v1 = v1;
-        __threadfence();
-        __hip_atomic_store(&S.pos_state[at], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        if (expect == 0) atomicAdd(&S.ctr[ci(C_POS_USED)], 1ull);
-        return true;
+        h = (h + 1) & S.pos_mask;
     }
-    return false;
+    return -1;
+}
+// the sum of v over the wavefront, added by lane 0 (every lane of the wavefront calls it)
+KDEV void wave_add(KG unsigned long long* p, uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, (unsigned long long)v);
 }
 KDEV int32_t bal_lookup(const DevState& S, int64_t aid) {
     uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
@@ -334,62 +325,70 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
 }
 
-// ---------------------------------------------------------------- 3. chains: one wavefront per account
-// Lane l takes the account's buckets 4l .. 4l + 3; a chain is the ops of one sid inside a bucket run
-// (in arrival order: the sort is stable).  Its start state is the Positions entry (aid, sid); its
-// record (LChain) sits at the position of its first op, which is also its name.
+// ---------------------------------------------------------------- 3. chains: one thread per sorted op
+// Op p heads a chain when no earlier op of its bucket run has its sid (the sort is stable: a chain's
+// ops are in arrival order).  The head's thread applies the chain -- start state the Positions entry
+// (aid, sid), its ops' effects in order -- and records it (LChain at the head's position, which is
+// also the chain's name).  The account's balance delta: a segmented sum over the wavefront's lanes
+// (the ops are sorted by account), one atomic per account run.
 __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
-    const uint32_t a = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (a >= (uint32_t)S.A || lskip(S) || lops(S) == 0) return;
-    const uint32_t lo = S.lseg[a], hi = S.lseg[a + 1];
-    if (lo == hi) return;
+    const uint32_t no = lops(S);
+    if (lskip(S) || no == 0) return;
     const KG uint32_t* K = skeys(S);
     const KG uint32_t* V = svals(S);
-    const uint32_t kb = a << LB_BUCKET_BITS;
-    const uint32_t ls = lower_bound(K, lo, hi, kb + 4 * lane), le = lower_bound(K, ls, hi, kb + 4 * lane + 4);
-    int64_t dsum = 0;
-    for (uint32_t j = ls; j < le; ++j) {
-        const uint32_t bj = K[j], sj = V[j];
-        const int64_t sid = S.lsid[sj];
-        bool head = true;   // the first op of its sid in this bucket run?
-        for (uint32_t p = j; p > ls && K[p - 1] == bj; --p)
-            if (S.lsid[V[p - 1]] == sid) { head = false; break; }
-        KG LChain& c = S.lchain[j];
-        if (!head) { c.aid = -1; continue; }
-        const int32_t slot = pos_lookup(S, a, sid);
-        PState P;
-        P.present = slot >= 0;
-        P.a = P.present ? S.pos[slot].v0 : 0;
-        P.v = P.present ? S.pos[slot].v1 : 0;
-        c.sid = sid; c.aid = (int32_t)a; c.islot = slot;
-        c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
-        int64_t cd = 0;
-        uint32_t last = 0;
-        for (uint32_t p = j; p < le && K[p] == bj; ++p) {
-            const uint32_t sq = V[p];
-            if (p != j && S.lsid[sq] != sid) continue;
-            for_effects(S, io, sq, (int64_t)a, sid, [&](uint32_t es) {
-                VWrite w;
-                cd = jladd(cd, apply_effect(S, io, sq, es, (int64_t)a, sid, P, w));
-                last = es;
-                if (w.kind) {
-                    S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
-                    S.lvw_meta[es] = w.kind | (j << 2);
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < no; base += gridDim.x * blockDim.x) {
+        const uint32_t j = base + threadIdx.x;
+        int64_t aid = -1, cd = 0;
+        if (j < no) {
+            const uint32_t bj = K[j];
+            const int64_t sid = S.lsid[V[j]];
+            aid = bj >> LB_BUCKET_BITS;
+            bool head = true;
+            for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
+                if (S.lsid[V[p - 1]] == sid) { head = false; break; }
+            KG LChain& c = S.lchain[j];
+            if (!head) {
+                c.aid = -1;
+            } else {
+                const int32_t slot = pos_lookup(S, aid, sid);
+                PState P;
+                P.present = slot >= 0;
+                P.a = P.present ? S.pos[slot].v0 : 0;
+                P.v = P.present ? S.pos[slot].v1 : 0;
+                c.sid = sid; c.aid = (int32_t)aid; c.islot = slot;
+                c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
+                uint32_t last = 0;
+                for (uint32_t p = j; p < no && K[p] == bj; ++p) {
+                    const uint32_t sq = V[p];
+                    if (p != j && S.lsid[sq] != sid) continue;
+                    for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
+                        VWrite w;
+                        cd = jladd(cd, apply_effect(S, io, sq, es, aid, sid, P, w));
+                        last = es;
+                        if (w.kind) {
+                            S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                            S.lvw_meta[es] = w.kind | (j << 2);
+                        }
+                    });
                 }
-            });
+                c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
+                c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
+            }
         }
-        c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
-        c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
-        dsum = jladd(dsum, cd);
+        // segmented inclusive sum of cd over runs of equal aid (wrap-around, order-free)
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)cd, off, 64);
+            const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((uint64_t)cd >> 32), off, 64);
+            const int64_t oa = (int64_t)(((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)((uint64_t)aid >> 32), off, 64) << 32) |
+                                         (uint32_t)__shfl_up((int)(uint32_t)aid, off, 64));
+            if (lane >= off && oa == aid) cd = jladd(cd, (int64_t)(((uint64_t)hi << 32) | lo));
+        }
+        const int64_t next = (int64_t)(((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)((uint64_t)aid >> 32), 1, 64) << 32) |
+                                       (uint32_t)__shfl_down((int)(uint32_t)aid, 1, 64));
+        if (aid >= 0 && cd != 0 && (lane == 63 || next != aid))
+            atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[aid]), (unsigned long long)cd);
     }
-    // the account's balance delta: a wavefront sum (wrap-around, order-free)
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)dsum, off, 64);
-        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)dsum >> 32), off, 64);
-        dsum = jladd(dsum, (int64_t)(((uint64_t)hi32 << 32) | lo32));
-    }
-    if (lane == 0) S.ldelta[a] = dsum;
 }
 
 // ---------------------------------------------------------------- 4. couplings between chains
@@ -595,6 +594,21 @@ __global__ void __launch_bounds__(256) k_lacct(DevState S, EpochIO io) {
         atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[io.aid[i]]), (unsigned long long)(int64_t)io.size[i]);
     }
 }
+// Updates in place and deletes; a key to create is left to k_linsert (the VW winner's vk entry marked
+// LVK_INSERT, the chain by its state).
+constexpr unsigned long long LVK_INSERT = 1ull << 62;
+KDEV bool chain_final(const DevState& S, const KG LChain& c, int64_t& fa, int64_t& fv) {
+    bool fp = c.fpres != 0;
+    fa = c.fa; fv = c.fv;
+    if (c.late) {
+        const uint32_t s = c.late - 1;
+        const long4 w = S.lvw[s];
+        fp = (S.lvw_meta[s] & 3u) == VW_PUT;
+        fa = w.z;
+        fv = w.w;
+    }
+    return fp;
+}
 __global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
     const uint32_t ns = lseqs(S, io), no = lops(S);
@@ -605,35 +619,55 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io) {
         if (!(meta & 3u) || S.lvw_tgt[s] >= 0) continue;
         const long4 w = S.lvw[s];
         const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), false);
-        if (p < 0 || S.lvk[p].y != (unsigned long long)s + 1) continue;
+        if (p < 0 || (S.lvk[p].y & ~LVK_INSERT) != (unsigned long long)s + 1) continue;
+        const int32_t h = pos_lookup(S, w.x, w.y);
         if ((meta & 3u) == VW_DEL) {
-            const int32_t h = pos_lookup(S, w.x, w.y);
-            if (h >= 0) __hip_atomic_store(&S.pos_state[h], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (!pos_upsert(S, w.x, w.y, w.z, w.w)) {
-            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+            if (h >= 0) S.pos_state[h] = 2u;
+        } else if (h >= 0) {
+            S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
+        } else {
+            S.lvk[p].y |= LVK_INSERT;
         }
     }
     // every chain's final entry (its own last state, or a later value write into it)
     for (uint32_t p = t0; p < no; p += stride) {
         const KG LChain& c = S.lchain[p];
-        if (c.aid < 0) continue;
-        bool fp = c.fpres != 0;
-        int64_t fa = c.fa, fv = c.fv;
-        if (c.late) {
-            const uint32_t s = c.late - 1;
-            const long4 w = S.lvw[s];
-            fp = (S.lvw_meta[s] & 3u) == VW_PUT;
-            fa = w.z;
-            fv = w.w;
-        }
-        if (fp == (c.ipres != 0) && (!fp || (fa == c.ia && fv == c.iv))) continue;
-        if (c.ipres) {
-            if (fp) { S.pos[c.islot].v0 = fa; S.pos[c.islot].v1 = fv; }
-            else __hip_atomic_store(&S.pos_state[c.islot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (fp && !pos_upsert(S, (int64_t)c.aid, c.sid, fa, fv)) {
-            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
-        }
+        if (c.aid < 0 || !c.ipres) continue;
+        int64_t fa, fv;
+        const bool fp = chain_final(S, c, fa, fv);
+        if (fp && fa == c.ia && fv == c.iv) continue;
+        if (fp) { S.pos[c.islot].v0 = fa; S.pos[c.islot].v1 = fv; }
+        else S.pos_state[c.islot] = 2u;
     }
+}
+// The keys to create: chains absent at the epoch's start that end present, and value-write winners
+// into absent keys.  Every key is new and inserted by one thread (pos_insert).
+__global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
+    if (lskip(S) || lops(S) == 0 || lfell(S)) return;
+    const uint32_t no = lops(S);
+    const uint64_t nvk = S.lvk_mask + 1;
+    uint32_t grew = 0;
+    bool full = false;
+    const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t p = t0; p < no; p += stride) {
+        const KG LChain& c = S.lchain[p];
+        if (c.aid < 0 || c.ipres) continue;
+        int64_t fa, fv;
+        if (!chain_final(S, c, fa, fv)) continue;
+        const int r = pos_insert(S, (int64_t)c.aid, c.sid, fa, fv);
+        full |= r < 0;
+        grew += r > 0;
+    }
+    for (uint64_t p = t0; p < nvk; p += stride) {
+        const ulonglong4 e = S.lvk[p];
+        if (!(e.y & LVK_INSERT)) continue;
+        const long4 w = S.lvw[(uint32_t)(e.y & ~LVK_INSERT) - 1];
+        const int r = pos_insert(S, w.x, w.y, w.z, w.w);
+        full |= r < 0;
+        grew += r > 0;
+    }
+    if (full) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+    wave_add(&S.ctr[ci(C_POS_USED)], grew);
 }
 __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -679,7 +713,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.passes = S.lpasses;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(n + max_trades + 1ull, 256)), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_lchains, dim3(cdiv((uint32_t)S.A, 4)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lchains, dim3(std::min<uint32_t>(cdiv(n + max_trades, 256), 8192)), dim3(256), 0, st, S, io);
     const uint32_t gs = std::min<uint32_t>(cdiv(nseq, 256), 4096);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S, io);
     // (with no coupling the first round's link finds none, runs nothing and the detect converges)
@@ -693,6 +727,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 1);
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_linsert, dim3(gs), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lbalances, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }
 
