@@ -537,33 +537,45 @@ __global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_rou
 // key, and a second pass checks every writer's key against it: a hash collision of two different keys
 // sends the epoch to the serial replay).
 KDEV uint64_t vkey_hash(int64_t k0, int64_t k1) { return mix64((uint64_t)k0 * 0xc2b2ae3d27d4eb4full ^ mix64((uint64_t)k1 + 1)) | 1ull; }
+// The slot of key hash h (insert: claimed when absent), or -1.  A position value is a small pair, so
+// a few keys take most value writes of an epoch: the probe reads before it claims (no atomic on a
+// hot key's line unless the slot is empty).
 KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert) {
     uint64_t p = h & S.lvk_mask;
     for (uint32_t probes = 0; probes < 4096; ++probes) {
         KG unsigned long long* e = reinterpret_cast<KG unsigned long long*>(&S.lvk[p]);
-        const unsigned long long cur = insert ? atomicCAS(e, 0ull, (unsigned long long)h)
-                                              : __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0 && insert) cur = atomicCAS(e, 0ull, (unsigned long long)h);
         if (cur == h || (insert && cur == 0)) return (int64_t)p;
         if (cur == 0) return -1;
         p = (p + 1) & S.lvk_mask;
     }
     return -1;
 }
+// The latest value write per key: the writers take the seqs from the last down, so the first to
+// reach a hot key usually holds the maximum and the others skip the atomic.
+KDEV void vk_max(KG unsigned long long* p, unsigned long long v) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) atomicMax(p, v);
+}
 __global__ void __launch_bounds__(256) k_lvw_classify(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
     const uint32_t ns = lseqs(S, io);
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += gridDim.x * blockDim.x) {
+        const uint32_t s = ns - 1 - k;
         const uint32_t meta = S.lvw_meta[s];
         if (!(meta & 3u)) continue;
         const int32_t c = S.lvw_tgt[s];
         if (c >= 0) {
-            if ((uint32_t)c != (meta >> 2) && s > S.lchain[c].last_seq) atomicMax(&S.lchain[c].late, s + 1);
+            if ((uint32_t)c != (meta >> 2) && s > S.lchain[c].last_seq) {
+                KG uint32_t* l = &S.lchain[c].late;
+                if (__hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < s + 1) atomicMax(l, s + 1);
+            }
             continue;
         }
         const long4 w = S.lvw[s];
         const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), true);
         if (p < 0) { lfallback(S); return; }
-        atomicMax(reinterpret_cast<KG unsigned long long*>(&S.lvk[p]) + 1, (unsigned long long)s + 1);
+        vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[p]) + 1, (unsigned long long)s + 1);
     }
 }
 __global__ void __launch_bounds__(256) k_lvw_claim(DevState S, EpochIO io, int check) {
