@@ -265,6 +265,7 @@ def parse_args(argv=None):
     ap.add_argument("--epoch", type=int, default=1 << 22)
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--symbols", type=int, default=0, help="diagnostic: symbols per GPU for c3 (default: the murmur2 partition of 65,536)")
+    ap.add_argument("--shard", default="", help="diagnostic: R/N, the records of rank R of an N-GPU run (c3, c4) on this one GPU")
     ap.add_argument("--mix", default="", help="diagnostic: BUY,SELL,CANCEL fractions of the c2/c3 stream")
     ap.add_argument("--orders", type=int, default=16_000_000, help="stream length per GPU (>= (W+K)*E)")
     ap.add_argument("--max-resting", type=int, default=0,
@@ -328,8 +329,14 @@ def main():
     host_epochs = args.host_path_epochs if world == 1 else 0
     # + 1: the phase-breakdown epoch; then the host-path epochs
     total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs) * E)
+    # --shard R/N (one GPU): the records rank R of an N-GPU run would match, e.g. C4's hot shard
+    w_rank, w_world = (rank, world) if not args.shard else tuple(int(x) for x in args.shard.split("/"))
+    if args.shard and world > 1:
+        raise SystemExit("bench.py: --shard is a one-GPU diagnostic")
     setup, stream, sids, nacc, shards, desc = make_workload(
-        args.workload, total, rank, world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
+        args.workload, total, w_rank, w_world, args.symbols, [float(x) for x in args.mix.split(",")] if args.mix else None)
+    if args.shard:
+        desc += f" -- shard {w_rank} of {w_world} on one GPU"
     max_sid = int(sids.max())
     flags = parse_flags(args.flags)
     if flags and world > 1:
@@ -544,7 +551,7 @@ def main():
         pmc = os.path.join(ROOT, "profiles", f"pmc_k_match_{args.workload}.json")
         # the committed PMC pass is of the default single-GPU configuration only (tools/gpu_round4.sh),
         # and counts only when it profiled this very build
-        if world == 1 and not args.symbols and not args.mix and E == (1 << 22) and not flags:
+        if world == 1 and not args.symbols and not args.mix and not args.shard and E == (1 << 22) and not flags:
             traffic, pmc_derived, pmc_src = pmc_for_build(pmc, build_id)
         out = {
             "metric": METRIC,

@@ -106,6 +106,18 @@ def test_c4_zipf_65536_symbols(kme_mod, oracle_mod):
     _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
 
 
+@pytest.mark.parametrize("rank", [0, 5])
+def test_c4_zipf_n8_shard(kme_mod, oracle_mod, rank):
+    """The records rank r of an 8-GPU C4 run matches (``W.zipf(shard=(r, 8))``: its murmur2 share of
+    the 65,536 symbols, with their popularity in the whole universe) -- the shard whose hot books
+    bound C4's weak scaling (bench.py --workload c4 --shard r/8)."""
+    n_sym, n_acc, n = 65536, 65536, 2 * E
+    stream = W.zipf(n, n_symbols=n_sym, n_accounts=n_acc, seed=1000 + rank, shard=(rank, 8))
+    sids = W.shard_symbols(n_sym, 8, rank)
+    setup = W.funded_setup(n_acc, sids)
+    _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
+
+
 def test_c2_uniform_at_scale(kme_mod, oracle_mod):
     """C2's shape (1,024 symbols): every group busy, one wavefront each."""
     n_sym, n_acc, n = 1024, 4096, 4 * E

@@ -5,7 +5,8 @@
 #   3. a rocprofv3 kernel trace of the same command (its averages are the frac's denominator);
 #   4. the PMC traffic passes and the L2-request passes of k_match_lanes (the summary records the
 #      profiled build's kme_build_id(); bench.py reports roofline.traffic only for that build);
-#   5. the extra configuration lines (shards of C3, C2, C5, C4, the exact-ledger drop-in line).
+#   5. the extra configuration lines (rank 0 of the N = 8 / 4 / 2 runs of C3, C2, C5, C4 and its N = 8
+#      shard, the exact-ledger drop-in line).
 # Usage: bash tools/gpu_round4.sh <tag> [skip-tests]
 set -o pipefail
 TAG=${1:-round}
@@ -30,7 +31,7 @@ f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
 python3 tools/trace_summary.py $f 5 $OUT/trace_summary.json "C3, 65,536 symbols, E = 2^22, 5 timed epochs" > /dev/null
 bash tools/pmc_kmatch.sh $TAG/pmc k_match_lanes --host-path-epochs 0 || exit $?
 bash tools/pmc_tcc.sh $TAG/tcc k_match_lanes kafka-matching-engine_amd/kme/libkme.so || exit $?
-for extra in "--workload c3 --symbols 8192" "--workload c3 --symbols 16384" "--workload c3 --symbols 32768" "--workload c2" "--workload c5" "--workload c4 --steps 2 --warmup 1" "--workload c4 --epoch 262144 --steps 16 --warmup 2" "--flags exact_ledger,serial_fallback --steps 5 --warmup 2"; do
+for extra in "--workload c3 --shard 0/8" "--workload c3 --shard 0/4" "--workload c3 --shard 0/2" "--workload c2" "--workload c5" "--workload c4 --steps 2 --warmup 1" "--workload c4 --shard 0/8 --steps 2 --warmup 1" "--workload c4 --epoch 262144 --steps 16 --warmup 2" "--flags exact_ledger,serial_fallback --steps 5 --warmup 2"; do
   timeout -k 10 400 python3 -u bench.py --no-cpu-baseline --host-path-epochs 0 $extra >> $OUT/bench_extra.jsonl 2>> $OUT/bench_extra.err
   rc=$?; echo "extra [$extra] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
