@@ -323,7 +323,10 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                 const int32_t price = io.price[i], size = io.size[i];
                 const int64_t aid = io.aid[i];
                 if (price < 0 || price > 100 || size < 0) raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
-                // (the per-account need: k_need, on a side stream beside k_route and the partition)
+                else if (aid >= 0 && aid < S.A && !KME_DIAG_EMAP_NONEED) {   // the account's reservation need
+                    const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
+                    atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
+                }
                 // k_route's work for the order, done here while its fields are in registers (the
                 // streaming stores overlap this kernel's atomics): symbol group, the packed record
                 // with the order's oid-table position, or the books.get == null reject (KP:202-203).
@@ -358,24 +361,8 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     }
 }
 
-// FUNDED per-account reservation need of the epoch: sum over its BUY/SELL of the larger end of
-// checkBalance's risk (KP:172-176).  Memory-side atomics on a 8-byte-per-account array; the kernel
-// runs on a side stream concurrently with k_route and the partition (nothing there reads it), joined
-// before the matching.
-__global__ void __launch_bounds__(256) k_need(DevState S, EpochIO io) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
-        const int32_t a = io.action[i];
-        if (a != BUY && a != SELL) continue;
-        const int32_t price = io.price[i], size = io.size[i];
-        const int64_t aid = io.aid[i];
-        if (price < 0 || price > 100 || size < 0 || aid < 0 || aid >= S.A || KME_DIAG_EMAP_NONEED) continue;
-        const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
-        atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
-    }
-}
-
 // With account records in the epoch (k_ledger_funded has applied them), a BUY/SELL's acct_ok is
-// decided again (k_emap read the accounts as they stood before the epoch): runs after the join.
+// decided again (k_emap read the accounts as they stood before the epoch).
 __global__ void __launch_bounds__(256) k_acct_refresh(DevState S, EpochIO io) {
     if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
@@ -3875,10 +3862,6 @@ void launch_epoch_reset(const DevState& S, hipStream_t st) {
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st) {
     const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
     hipLaunchKernelGGL(k_emap, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);
-}
-void launch_need(const DevState& S, const EpochIO& io, hipStream_t st) {
-    const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
-    hipLaunchKernelGGL(k_need, dim3(nb), dim3(256), 0, st, S, io);
 }
 void launch_acct_refresh(const DevState& S, const EpochIO& io, hipStream_t st) {
     const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);

@@ -44,9 +44,6 @@ struct kme_engine {
     hipStream_t own_stream = nullptr;
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipStream_t aux_stream = nullptr;    // the funded proof, beside k_route and the partition
-    hipEvent_t ev_aux_fork = nullptr, ev_aux_join = nullptr;
-    bool aux = true;
     uint64_t last_busy = 1;              // groups k_match took in the last epoch (C_BUSY)
     // k_match in two-wavefront mode when 1 .. two_max groups were busy in the last epoch (KME_TWO_MAX;
     // 0: never) and fewer than 1 in 8 of its records were cancels that removed an order: the serial
@@ -210,9 +207,6 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     HIP_TRY(hipStreamCreateWithFlags(&e->lane_stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-    HIP_TRY(hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_aux_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_aux_join, hipEventDisableTiming));
     e->stream = e->own_stream;
     for (auto& evs : e->ev)
         for (auto& ev : evs) HIP_TRY(hipEventCreate(&ev));
@@ -337,7 +331,6 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (const char* v = std::getenv("KME_FAST")) S.fast = std::atoi(v) != 0;   // A/B diagnostics
     if (const char* v = std::getenv("KME_TWO_DRAIN")) if (S.fast && std::atoi(v)) S.fast |= 2;   // diagnostics
     if (const char* v = std::getenv("KME_TWO_MAX")) e->two_max = (uint64_t)std::max(0, std::atoi(v));   // A/B diagnostics
-    if (const char* v = std::getenv("KME_AUX_STREAM")) e->aux = std::atoi(v) != 0;                    // A/B diagnostics
     if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
@@ -397,7 +390,6 @@ kme_status kme_destroy(kme_engine* e) {
     if (e->in_stream) (void)hipStreamSynchronize(e->in_stream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->lane_stream) (void)hipStreamSynchronize(e->lane_stream);
-    if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
     if (e->out_stream) (void)hipStreamSynchronize(e->out_stream);
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
@@ -414,9 +406,6 @@ kme_status kme_destroy(kme_engine* e) {
         if (r.owned) (void)hipHostUnregister((void*)r.p);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->lane_stream) (void)hipStreamDestroy(e->lane_stream);
-    if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
-    if (e->ev_aux_fork) (void)hipEventDestroy(e->ev_aux_fork);
-    if (e->ev_aux_join) (void)hipEventDestroy(e->ev_aux_join);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
@@ -467,21 +456,15 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     phase_begin(e, PH_EMAP);
     launch_emap(S, io, funded, e->d_io, st);
     phase_end(e, PH_EMAP);
-    // the funded proof (need, account records, check, roll-forward) on the side stream, beside
-    // k_route and the partition (they read none of it); joined before the matching (KME_AUX_STREAM=0:
-    // in line, for A/B runs)
-    hipStream_t ps = e->aux ? e->aux_stream : st;
+    // the funded proof: account records in order, the per-account check and roll-forward (k_emap
+    // summed the need).  (Measured and not kept: the need in a kernel of its own on a side stream
+    // beside k_route and the partition -- the epoch was 0.08 ms longer: the phases beside it are
+    // bound by the same random accesses.)
     if (funded) {
-        if (e->aux) {
-            HIP_TRY(hipEventRecord(e->ev_aux_fork, st));
-            HIP_TRY(hipStreamWaitEvent(e->aux_stream, e->ev_aux_fork, 0));
-        }
-        phase_begin(e, PH_LEDGER, ps);
-        launch_need(S, io, ps);
-        launch_ledger_funded(S, io, ps);
-        launch_check_funded(S, io, ps);
-        phase_end(e, PH_LEDGER, ps);
-        if (e->aux) HIP_TRY(hipEventRecord(e->ev_aux_join, e->aux_stream));
+        phase_begin(e, PH_LEDGER);
+        launch_ledger_funded(S, io, st);
+        launch_check_funded(S, io, st);
+        phase_end(e, PH_LEDGER);
     }
     phase_begin(e, PH_ROUTE);
     launch_route(S, io, funded, st);
@@ -490,7 +473,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         phase_begin(e, PH_PART);
         const int buf = launch_partition(S, io, st);
         phase_end(e, PH_PART);
-        if (e->aux) HIP_TRY(hipStreamWaitEvent(st, e->ev_aux_join, 0));
         launch_acct_refresh(S, io, st);
         phase_begin(e, PH_MATCH);
         // light groups one lane each, concurrently with k_match's busy ones (a second stream).  When
