@@ -202,6 +202,7 @@ struct DevState {
     KG uint32_t* lghist;
     KG uint32_t* lop;                 // per arrival number: record | kind << 30
     KG int64_t* lsid;                 //   and its chain's sid
+    KG int64_t* lssid;                // per sorted op: its chain's sid (k_lseg gathers it once)
     KG LChain* lchain;                // per sorted op
     KG long4* lvw;                    // per arrival number: a value write (key, value)
     KG uint32_t* lvw_meta;            //   kind | writer chain << 2

@@ -258,7 +258,7 @@ KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
     const uint32_t key = lkey_of(k0, k1);
     const uint32_t hi = S.lseg[k0 + 1];
     for (uint32_t p = lower_bound(K, S.lseg[k0], hi, key); p < hi && K[p] == key; ++p)
-        if (S.lsid[V[p]] == k1) return (int32_t)p;
+        if (S.lssid[p] == k1) return (int32_t)p;
     return -1;
 }
 
@@ -315,11 +315,13 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 }
 
 // ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
+// (and each sorted op's sid, gathered once: the chain kernels then read it in sorted order)
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k > n || n == 0) return;      // (no ops: lseg stays zero)
     const KG uint32_t* K = skeys(S);
+    if (k < n) S.lssid[k] = S.lsid[svals(S)[k]];
     const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> LB_BUCKET_BITS);
     const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> LB_BUCKET_BITS);
     for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
@@ -342,11 +344,11 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
         int64_t aid = -1, cd = 0;
         if (j < no) {
             const uint32_t bj = K[j];
-            const int64_t sid = S.lsid[V[j]];
+            const int64_t sid = S.lssid[j];
             aid = bj >> LB_BUCKET_BITS;
             bool head = true;
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
-                if (S.lsid[V[p - 1]] == sid) { head = false; break; }
+                if (S.lssid[p - 1] == sid) { head = false; break; }
             KG LChain& c = S.lchain[j];
             if (!head) {
                 c.aid = -1;
@@ -360,8 +362,8 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
                 c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
                 uint32_t last = 0;
                 for (uint32_t p = j; p < no && K[p] == bj; ++p) {
+                    if (p != j && S.lssid[p] != sid) continue;
                     const uint32_t sq = V[p];
-                    if (p != j && S.lsid[sq] != sid) continue;
                     for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
                         VWrite w;
                         cd = jladd(cd, apply_effect(S, io, sq, es, aid, sid, P, w));
@@ -471,8 +473,8 @@ __global__ void __launch_bounds__(256) k_lr_run(DevState S, EpochIO io) {
         int q = 0;
         const uint32_t hi = S.lseg[aid + 1];
         for (uint32_t p = head; p < hi && K[p] == K[head]; ++p) {
+            if (p != head && S.lssid[p] != sid) continue;
             const uint32_t sq = V[p];
-            if (p != head && S.lsid[sq] != sid) continue;
             for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
                 for (; q < nin && in[q] < es; ++q) {
                     const long4 x = S.lvw[in[q]];

@@ -294,7 +294,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lkey[0], nops); ALLOC(S.lkey[1], nops);
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
-            ALLOC(S.lop, nseq); ALLOC(S.lsid, nseq);
+            ALLOC(S.lop, nseq); ALLOC(S.lsid, nseq); ALLOC(S.lssid, nops);
             ALLOC(S.lchain, nops);
             ALLOC(S.lvw, nseq); ALLOC(S.lvw_meta, nseq); ALLOC(S.lvw_tgt, nseq);
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
