@@ -96,14 +96,26 @@ struct LChain {
     int64_t ia, iv;                // the entry at the epoch's start (ipres)
     int64_t fa, fv;                // after the chain's last effect (fpres)
     int64_t delta;                 // the balance change of its effects
+    uint64_t late;                 // (1 + arrival number) << 32 | op position of the latest value write
+                                   // into it after its last effect (0: none)
     uint32_t last_seq;             // arrival number of its last effect
     uint32_t dirty;                // in the repair rounds' run list (a value write into it preceded one of its reads)
-    uint32_t late;                 // 1 + arrival number of the latest value write after its last effect
     uint32_t rix;                  // 1 + the coupling list index of its first incoming value write (this round)
     int32_t aid, islot;            // islot: the entry's table slot at the start (-1: absent)
-    uint8_t ipres, fpres, _p[6];
+    uint8_t ipres, fpres, _p[2];
 };
 static_assert(sizeof(LChain) == 80, "LChain");
+// One ledger effect of the epoch (kme_ledger.hip): checkBalance, a fill, or postRemoveAdjustments on
+// the position (aid, sid), with its arrival number
+struct LOp {
+    int64_t sid;
+    uint32_t es;                   // arrival number
+    int32_t size, price;           // the effect's size and price term
+    int32_t aid;
+    uint32_t flags;                // kind (check / fill / cancel) | buy << 2
+    uint32_t _pad;
+};
+static_assert(sizeof(LOp) == 32, "LOp");
 // the ledger pass's counters (DevState::lctr, one line each)
 enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
 
@@ -200,19 +212,18 @@ struct DevState {
     KG uint32_t* lkey[2];
     KG uint32_t* lval[2];
     KG uint32_t* lghist;
-    KG uint32_t* lop;                 // per arrival number: record | kind << 30
-    KG int64_t* lsid;                 //   and its chain's sid
-    KG int64_t* lssid;                // per sorted op: its chain's sid (k_lseg gathers it once)
+    KG LOp* lrec;                     // per op, arrival order
+    KG LOp* lsrt;                     // per op, sorted order (k_lseg gathers them once)
     KG LChain* lchain;                // per sorted op
-    KG long4* lvw;                    // per arrival number: a value write (key, value)
+    KG long4* lvw;                    // per sorted op: its value write (key, value)
     KG uint32_t* lvw_meta;            //   kind | writer chain << 2
     KG int32_t* lvw_tgt;              //   the chain it writes into (-1: none)
     KG uint32_t* lseg;                // per account: its first sorted op
     KG int64_t* ldelta;               // per account: the epoch's balance change
     KG ulonglong4* lvk;               // value-key table: hash, 1 + latest arrival, key
-    KG uint32_t* lx;                  // couplings: arrival numbers of value writes into chains that read later
+    KG uint32_t* lx;                  // couplings: the ops whose value writes go into chains that read later
     KG uint32_t* lxn;                 //   per coupling: 1 + the next one into the same chain (this round)
-    KG uint8_t* lxmark;               // per arrival number: listed in lx
+    KG uint8_t* lxmark;               // per sorted op: listed in lx
     KG uint32_t* lrun;                // the repair rounds' run list (chain heads)
     KG uint32_t* lchg;                // the value writes a repair round changed
     KG unsigned long long* lctr;      // LC_N x CTR_STRIDE words

@@ -47,8 +47,9 @@ namespace kme {
 namespace {
 
 constexpr int LB_BUCKET_BITS = 8;                 // hash8(sid): 256 buckets per account
-constexpr uint32_t L_OP_REC = 0u, L_OP_MAKER = 1u, L_OP_CANCEL = 2u;
+constexpr uint32_t OP_CHECK = 0u, OP_FILL = 1u, OP_CANCEL = 2u;   // LOp::flags & 3 (bit 2: buy / bought)
 constexpr uint32_t VW_PUT = 1u, VW_DEL = 2u;
+constexpr int32_t VT_NONE = -1, VT_INSERT = -2;     // lvw_tgt: into no chain of the epoch / a winner to create
 
 KDEV uint32_t hash8(int64_t sid) { return (uint32_t)(mix64((uint64_t)sid ^ 0x632be59bd9b4e019ull) >> 56); }
 KDEV uint32_t lkey_of(int64_t aid, int64_t sid) { return (uint32_t)aid << LB_BUCKET_BITS | hash8(sid); }
@@ -61,7 +62,6 @@ KDEV bool lfell(const DevState& S) {
 // not this path's epoch: a fault (nothing of it is replayed), or a serial epoch (k_serial kept the ledger)
 KDEV bool lskip(const DevState& S) { return failed(S.ctr) || S.ctr[ci(C_FALLBACK)] != 0; }
 KDEV uint32_t lops(const DevState& S) { return (uint32_t)S.lctr[ci(LC_OPS)]; }
-KDEV uint32_t lseqs(const DevState& S, const EpochIO& io) { return io.n + 2 * (uint32_t)S.ctr[ci(C_TRADES)]; }
 
 // ---------------------------------------------------------------- stores (Core's layout, shared)
 KDEV uint32_t ld_state(const KG uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
@@ -203,44 +203,20 @@ KDEV void write_into(PState& P, const VWrite& w) {
     }
 }
 
-// The effect with arrival number `es` of the op at `seq` (its check / cancel: es == seq; trade k's
-// maker fill: i + 2k + 1; its taker fill: i + 2k + 2) on chain (aid, sid); returns the balance delta.
-KDEV int64_t apply_effect(const DevState& S, const EpochIO& io, uint32_t seq, uint32_t es, int64_t aid, int64_t sid,
-                          PState& P, VWrite& w) {
-    const uint32_t meta = S.lop[seq];
-    const uint32_t kind = meta >> 30, i = meta & 0x3FFFFFFFu;
+// One op: its effect on its chain's position P; returns the balance delta, w = its value write.
+KDEV int64_t apply_op(const LOp& o, PState& P, VWrite& w) {
+    const bool buy = (o.flags >> 2) & 1u;
+    const uint32_t kind = o.flags & 3u;
     w.kind = 0;
     int64_t d;
-    if (kind == L_OP_CANCEL) {
-        const int4 o = S.vic[i];
-        d = eff_cancel(P, (o.x >> 8) == BUY, o.y, o.x & 0xFF, w);
-    } else if (kind == L_OP_REC && es == seq) {
-        d = eff_check(P, io.action[i] == BUY, io.size[i], io.price[i]);
-    } else {
-        const uint32_t q = (es - i - 1) / 2;   // (maker fill: es - i odd; taker fill: even)
-        const TradeRec tr = io.trades[q];
-        const bool taker_buy = io.action[i] == BUY;
-        if (((es - i) & 1u) == 1u) d = eff_fill(P, !taker_buy, tr.size, 0, w);                               // KP:266-267
-        else d = eff_fill(P, taker_buy, tr.size, jisub(io.price[i], tr.mprice), w);                          // KP:268-269
-    }
-    if (w.kind && w.k0 == aid && w.k1 == sid) write_into(P, w);
+    if (kind == OP_CHECK) d = eff_check(P, buy, o.size, o.price);
+    else if (kind == OP_FILL) d = eff_fill(P, buy, o.size, o.price, w);
+    else d = eff_cancel(P, buy, o.size, o.price, w);
+    if (w.kind && w.k0 == (int64_t)o.aid && w.k1 == o.sid) write_into(P, w);   // into its own key
     return d;
 }
-// The effects of one op, in order: f(es).
-template <class F>
-KDEV void for_effects(const DevState& S, const EpochIO& io, uint32_t seq, int64_t aid, int64_t sid, F&& f) {
-    const uint32_t meta = S.lop[seq];
-    f(seq);
-    if ((meta >> 30) != L_OP_REC) return;
-    const uint32_t i = meta & 0x3FFFFFFFu;
-    for (uint32_t q = io.trade_off[i]; q < io.trade_off[i + 1]; ++q) {
-        const TradeRec tr = io.trades[q];
-        if (tr.maid == aid && tr.msid == sid) f(i + 2 * q + 1);   // a maker fill on this same key
-        f(i + 2 * q + 2);
-    }
-}
 
-// The sorted ops: keys (aid * 256 + hash8(sid)) and values (seq) of the last radix pass.
+// The sorted ops: keys (aid * 256 + hash8(sid)) and values (arrival op index) of the last radix pass.
 KDEV const KG uint32_t* skeys(const DevState& S) { return S.lkey[S.lpasses & 1]; }
 KDEV const KG uint32_t* svals(const DevState& S) { return S.lval[S.lpasses & 1]; }
 KDEV uint32_t lower_bound(const KG uint32_t* k, uint32_t lo, uint32_t hi, uint32_t key) {
@@ -254,74 +230,72 @@ KDEV uint32_t lower_bound(const KG uint32_t* k, uint32_t lo, uint32_t hi, uint32
 KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
     if (k0 < 0 || k0 >= S.A) return -1;
     const KG uint32_t* K = skeys(S);
-    const KG uint32_t* V = svals(S);
     const uint32_t key = lkey_of(k0, k1);
     const uint32_t hi = S.lseg[k0 + 1];
     for (uint32_t p = lower_bound(K, S.lseg[k0], hi, key); p < hi && K[p] == key; ++p)
-        if (S.lssid[p] == k1) return (int32_t)p;
+        if (S.lsrt[p].sid == k1) return (int32_t)p;
     return -1;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------- 1. the ops in arrival order
+// One op per effect: an accepted BUY/SELL's checkBalance, each of its trades' maker fill (on the
+// maker's key) and taker fill, an accepted cancel's postRemoveAdjustments.
 __global__ void __launch_bounds__(256) k_lcount(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= io.n) return;
     uint32_t c = 0;
     if (!lskip(S)) {
         const int32_t a = io.action[i], out = io.out_action[i];
-        if ((a == BUY || a == SELL) && out == a) {
-            c = 1;
-            const int64_t aid = io.aid[i], sid = io.sid[i];
-            for (uint32_t q = io.trade_off[i]; q < io.trade_off[i + 1]; ++q) {
-                const TradeRec tr = io.trades[q];
-                c += (tr.maid == aid && tr.msid == sid) ? 0u : 1u;
-            }
-        } else if (a == CANCEL && out == CANCEL) {
-            c = 1;
-        }
+        if ((a == BUY || a == SELL) && out == a) c = 1 + 2 * (io.trade_off[i + 1] - io.trade_off[i]);
+        else if (a == CANCEL && out == CANCEL) c = 1;
     }
     S.lcnt[i] = c;
 }
-// At the scanned offsets: sort key aid * 256 + hash8(sid) and value seq; per seq the op's record and
-// kind (lop) and its chain's sid (lsid).
+// At the scanned offsets, in arrival order: the op (LOp: chain sid and account, arrival number, the
+// effect's size / price / side) and its sort key aid * 256 + hash8(sid).  Record i's check / cancel
+// has arrival number i + 2 trade_off[i], trade q's maker and taker fills i + 2q + 1 and i + 2q + 2
+// (executeTrade's order, KP:265-274).
 __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= io.n || lskip(S)) return;
     const int32_t a = io.action[i], out = io.out_action[i];
     uint32_t o = S.lcnt[i];
-    const uint32_t t0 = io.trade_off[i], seq = i + 2 * t0;
+    const uint32_t t0 = io.trade_off[i];
+    auto put = [&](int64_t aid, int64_t sid, uint32_t es, int32_t size, int32_t price, uint32_t flags) {
+        LOp op;
+        op.sid = sid; op.es = es; op.size = size; op.price = price; op.aid = (int32_t)aid; op.flags = flags; op._pad = 0;
+        S.lrec[o] = op;
+        S.lk0[o] = lkey_of(aid, sid);
+        S.lv0[o] = o;
+        ++o;
+    };
     if ((a == BUY || a == SELL) && out == a) {
         const int64_t aid = io.aid[i], sid = io.sid[i];
-        S.lk0[o] = lkey_of(aid, sid); S.lv0[o] = seq; ++o;
-        S.lop[seq] = L_OP_REC << 30 | i;
-        S.lsid[seq] = sid;
+        const int32_t price = io.price[i];
+        const uint32_t buy = a == BUY ? 1u : 0u;
+        put(aid, sid, i + 2 * t0, io.size[i], price, OP_CHECK | buy << 2);                          // KP:167-182
         for (uint32_t q = t0; q < io.trade_off[i + 1]; ++q) {
             const TradeRec tr = io.trades[q];
-            if (tr.maid == aid && tr.msid == sid) continue;
-            const uint32_t ms = i + 2 * q + 1;
-            S.lk0[o] = lkey_of(tr.maid, tr.msid); S.lv0[o] = ms; ++o;
-            S.lop[ms] = L_OP_MAKER << 30 | i;
-            S.lsid[ms] = tr.msid;
+            put(tr.maid, tr.msid, i + 2 * q + 1, tr.size, 0, OP_FILL | (buy ^ 1u) << 2);             // KP:266-267
+            put(aid, sid, i + 2 * q + 2, tr.size, jisub(price, tr.mprice), OP_FILL | buy << 2);      // KP:268-269
         }
     } else if (a == CANCEL && out == CANCEL) {
-        const int4 v = S.vic[i];
+        const int4 v = S.vic[i];                      // the removed order: action << 8 | price, size, sid
         const int64_t vsid = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
-        S.lk0[o] = lkey_of(io.aid[i], vsid); S.lv0[o] = seq;
-        S.lop[seq] = L_OP_CANCEL << 30 | i;
-        S.lsid[seq] = vsid;
+        put(io.aid[i], vsid, i + 2 * t0, v.y, v.x & 0xFF, OP_CANCEL | ((v.x >> 8) == BUY ? 1u : 0u) << 2);   // KP:325-333
     }
 }
 
 // ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
-// (and each sorted op's sid, gathered once: the chain kernels then read it in sorted order)
+// (and the ops themselves gathered into sorted order, once: every later kernel reads them there)
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k > n || n == 0) return;      // (no ops: lseg stays zero)
     const KG uint32_t* K = skeys(S);
-    if (k < n) S.lssid[k] = S.lsid[svals(S)[k]];
+    if (k < n) S.lsrt[k] = S.lrec[svals(S)[k]];
     const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> LB_BUCKET_BITS);
     const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> LB_BUCKET_BITS);
     for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
@@ -330,25 +304,25 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
 // ---------------------------------------------------------------- 3. chains: one thread per sorted op
 // Op p heads a chain when no earlier op of its bucket run has its sid (the sort is stable: a chain's
 // ops are in arrival order).  The head's thread applies the chain -- start state the Positions entry
-// (aid, sid), its ops' effects in order -- and records it (LChain at the head's position, which is
-// also the chain's name).  The account's balance delta: a segmented sum over the wavefront's lanes
-// (the ops are sorted by account), one atomic per account run.
-__global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
+// (aid, sid), its ops in order -- and records it (LChain at the head's position, which is also the
+// chain's name); an op's value write is kept at the op's sorted position.  The account's balance
+// delta: a segmented sum over the wavefront's lanes (the ops are sorted by account), one atomic per
+// account run.
+__global__ void __launch_bounds__(256) k_lchains(DevState S) {
     const uint32_t no = lops(S);
     if (lskip(S) || no == 0) return;
     const KG uint32_t* K = skeys(S);
-    const KG uint32_t* V = svals(S);
     const int lane = threadIdx.x & 63;
     for (uint32_t base = blockIdx.x * blockDim.x; base < no; base += gridDim.x * blockDim.x) {
         const uint32_t j = base + threadIdx.x;
         int64_t aid = -1, cd = 0;
         if (j < no) {
             const uint32_t bj = K[j];
-            const int64_t sid = S.lssid[j];
+            const int64_t sid = S.lsrt[j].sid;
             aid = bj >> LB_BUCKET_BITS;
             bool head = true;
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
-                if (S.lssid[p - 1] == sid) { head = false; break; }
+                if (S.lsrt[p - 1].sid == sid) { head = false; break; }
             KG LChain& c = S.lchain[j];
             if (!head) {
                 c.aid = -1;
@@ -362,17 +336,15 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
                 c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
                 uint32_t last = 0;
                 for (uint32_t p = j; p < no && K[p] == bj; ++p) {
-                    if (p != j && S.lssid[p] != sid) continue;
-                    const uint32_t sq = V[p];
-                    for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
-                        VWrite w;
-                        cd = jladd(cd, apply_effect(S, io, sq, es, aid, sid, P, w));
-                        last = es;
-                        if (w.kind) {
-                            S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
-                            S.lvw_meta[es] = w.kind | (j << 2);
-                        }
-                    });
+                    const LOp op = S.lsrt[p];
+                    if (op.sid != sid) continue;
+                    VWrite w;
+                    cd = jladd(cd, apply_op(op, P, w));
+                    last = op.es;
+                    if (w.kind) {
+                        S.lvw[p] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                        S.lvw_meta[p] = w.kind | (j << 2);
+                    }
                 }
                 c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
                 c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
@@ -394,26 +366,29 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S, EpochIO io) {
 }
 
 // ---------------------------------------------------------------- 4. couplings between chains
-// A value write into a chain of this epoch that the chain reads afterwards (seq < its last effect).
-KDEV bool coupling(const DevState& S, uint32_t s, uint32_t meta, int32_t c) {
-    return (meta & 3u) && c >= 0 && (uint32_t)c != (meta >> 2) && s < S.lchain[c].last_seq;
+// A value write (op p) into a chain of this epoch that the chain reads afterwards (an earlier
+// arrival number than its last effect's).
+namespace {
+KDEV bool coupling(const DevState& S, uint32_t p, uint32_t meta, int32_t c) {
+    return (meta & 3u) && c >= 0 && (uint32_t)c != (meta >> 2) && S.lsrt[p].es < S.lchain[c].last_seq;
 }
-KDEV void list_coupling(const DevState& S, uint32_t s) {
-    if (S.lxmark[s]) return;                     // (one writer per s: no race)
-    S.lxmark[s] = 1;
+KDEV void list_coupling(const DevState& S, uint32_t p) {
+    if (S.lxmark[p]) return;                     // (one writer per p: no race)
+    S.lxmark[p] = 1;
     const unsigned long long x = atomicAdd(lc(S, LC_CROSS), 1ull);
-    if (x < S.lx_cap) S.lx[x] = s; else lfallback(S);
+    if (x < S.lx_cap) S.lx[x] = p; else lfallback(S);
 }
-__global__ void __launch_bounds__(256) k_ldetect(DevState S, EpochIO io) {
+}  // namespace
+__global__ void __launch_bounds__(256) k_ldetect(DevState S) {
     if (lskip(S) || lops(S) == 0) return;
-    const uint32_t ns = lseqs(S, io);
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
-        const uint32_t meta = S.lvw_meta[s];
+    const uint32_t no = lops(S);
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < no; p += gridDim.x * blockDim.x) {
+        const uint32_t meta = S.lvw_meta[p];
         if (!(meta & 3u)) continue;
-        const long4 w = S.lvw[s];
+        const long4 w = S.lvw[p];
         const int32_t c = find_chain(S, w.x, w.y);
-        S.lvw_tgt[s] = c;
-        if (coupling(S, s, meta, c)) list_coupling(S, s);
+        S.lvw_tgt[p] = c;
+        if (coupling(S, p, meta, c)) list_coupling(S, p);
     }
 }
 
@@ -428,18 +403,20 @@ __global__ void __launch_bounds__(256) k_ldetect(DevState S, EpochIO io) {
 // k_lr_detect re-targets the changed value writes and lists new couplings; no change = converged
 // (LC_DONE: the later rounds' launches return at once).  Not converged in S.lrounds rounds, or past a
 // capacity: the epoch goes to the serial replay.
+namespace {
 KDEV bool lr_active(const DevState& S) {
     return !lskip(S) && lops(S) != 0 && S.lctr[ci(LC_DONE)] == 0 && !lfell(S);
 }
+}  // namespace
 __global__ void __launch_bounds__(256) k_lr_link(DevState S) {
     if (!lr_active(S)) return;
-    const uint32_t nx = (uint32_t)S.lctr[ci(LC_CROSS)];
+    const uint32_t nx = (uint32_t)min(S.lctr[ci(LC_CROSS)], (unsigned long long)S.lx_cap);
     const uint32_t x0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (x0 == 0) S.lctr[ci(LC_CHG)] = 0;         // (the run kernel's list, filled after this launch)
     for (uint32_t x = x0; x < nx; x += gridDim.x * blockDim.x) {
-        const uint32_t s = S.lx[x];
-        const int32_t c = S.lvw_tgt[s];
-        if (!coupling(S, s, S.lvw_meta[s], c)) continue;
+        const uint32_t p = S.lx[x];
+        const int32_t c = S.lvw_tgt[p];
+        if (!coupling(S, p, S.lvw_meta[p], c)) continue;
         S.lxn[x] = atomicExch(&S.lchain[c].rix, x + 1);
         if (atomicExch(&S.lchain[c].dirty, 1u) == 0u) {
             const unsigned long long d = atomicAdd(lc(S, LC_DIRTY), 1ull);
@@ -448,57 +425,56 @@ __global__ void __launch_bounds__(256) k_lr_link(DevState S) {
     }
 }
 constexpr int LR_IN = 32;   // incoming value writes one chain takes in a round (more: the serial replay)
-__global__ void __launch_bounds__(256) k_lr_run(DevState S, EpochIO io) {
+__global__ void __launch_bounds__(256) k_lr_run(DevState S) {
     if (!lr_active(S)) return;
     const uint32_t nd = (uint32_t)min(S.lctr[ci(LC_DIRTY)], (unsigned long long)S.lr_cap);
+    const uint32_t no = lops(S);
     const KG uint32_t* K = skeys(S);
-    const KG uint32_t* V = svals(S);
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nd; d += gridDim.x * blockDim.x) {
         const uint32_t head = S.lrun[d];
         KG LChain& c = S.lchain[head];
-        // the incoming value writes, in arrival order
-        uint32_t in[LR_IN];
+        // the incoming value writes (ops of other chains), in arrival order
+        uint64_t in[LR_IN];                       // arrival number << 32 | op position
         int nin = 0;
         for (uint32_t x = c.rix; x != 0; x = S.lxn[x - 1]) {
             if (nin == LR_IN) { lfallback(S); return; }
-            const uint32_t s = S.lx[x - 1];
+            const uint32_t p = S.lx[x - 1];
+            const uint64_t e = (uint64_t)S.lsrt[p].es << 32 | p;
             int k = nin++;
-            for (; k > 0 && in[k - 1] > s; --k) in[k] = in[k - 1];
-            in[k] = s;
+            for (; k > 0 && in[k - 1] > e; --k) in[k] = in[k - 1];
+            in[k] = e;
         }
         c.rix = 0;
-        const int64_t aid = c.aid, sid = c.sid;
+        const int64_t sid = c.sid;
         PState P{c.ia, c.iv, c.ipres != 0};
         int64_t cd = 0;
         int q = 0;
-        const uint32_t hi = S.lseg[aid + 1];
-        for (uint32_t p = head; p < hi && K[p] == K[head]; ++p) {
-            if (p != head && S.lssid[p] != sid) continue;
-            const uint32_t sq = V[p];
-            for_effects(S, io, sq, aid, sid, [&](uint32_t es) {
-                for (; q < nin && in[q] < es; ++q) {
-                    const long4 x = S.lvw[in[q]];
-                    write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[in[q]] & 3u});
-                }
-                VWrite w;
-                cd = jladd(cd, apply_effect(S, io, sq, es, aid, sid, P, w));
-                const uint32_t om = S.lvw_meta[es];
-                const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
-                bool changed = (om & 3u) != (nm & 3u);
-                if (!changed && w.kind) {
-                    const long4 ow = S.lvw[es];
-                    changed = ow.x != w.k0 || ow.y != w.k1 || (w.kind == VW_PUT && (ow.z != w.v0 || ow.w != w.v1));
-                }
-                if (changed) {
-                    S.lvw[es] = make_long4(w.k0, w.k1, w.v0, w.v1);
-                    S.lvw_meta[es] = nm;
-                    const unsigned long long k = atomicAdd(lc(S, LC_CHG), 1ull);
-                    if (k < S.lc_cap) S.lchg[k] = es; else lfallback(S);
-                }
-            });
+        for (uint32_t p = head; p < no && K[p] == K[head]; ++p) {
+            const LOp op = S.lsrt[p];
+            if (op.sid != sid) continue;
+            for (; q < nin && (uint32_t)(in[q] >> 32) < op.es; ++q) {
+                const uint32_t ip = (uint32_t)in[q];
+                const long4 x = S.lvw[ip];
+                write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[ip] & 3u});
+            }
+            VWrite w;
+            cd = jladd(cd, apply_op(op, P, w));
+            const uint32_t om = S.lvw_meta[p];
+            const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
+            bool changed = (om & 3u) != (nm & 3u);
+            if (!changed && w.kind) {
+                const long4 ow = S.lvw[p];
+                changed = ow.x != w.k0 || ow.y != w.k1 || (w.kind == VW_PUT && (ow.z != w.v0 || ow.w != w.v1));
+            }
+            if (changed) {
+                S.lvw[p] = make_long4(w.k0, w.k1, w.v0, w.v1);
+                S.lvw_meta[p] = nm;
+                const unsigned long long k = atomicAdd(lc(S, LC_CHG), 1ull);
+                if (k < S.lc_cap) S.lchg[k] = p; else lfallback(S);
+            }
         }
         c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
-        atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[aid]), (unsigned long long)jlsub(cd, c.delta));
+        atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[c.aid]), (unsigned long long)jlsub(cd, c.delta));
         c.delta = cd;
     }
 }
@@ -520,15 +496,15 @@ __global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_rou
         return;
     }
     for (uint32_t k = k0; k < nc; k += gridDim.x * blockDim.x) {
-        const uint32_t s = S.lchg[k];
-        const uint32_t meta = S.lvw_meta[s];
-        int32_t c = -1;
+        const uint32_t p = S.lchg[k];
+        const uint32_t meta = S.lvw_meta[p];
+        int32_t c = VT_NONE;
         if (meta & 3u) {
-            const long4 w = S.lvw[s];
+            const long4 w = S.lvw[p];
             c = find_chain(S, w.x, w.y);
         }
-        S.lvw_tgt[s] = c;
-        if (coupling(S, s, meta, c)) list_coupling(S, s);
+        S.lvw_tgt[p] = c;
+        if (coupling(S, p, meta, c)) list_coupling(S, p);
     }
 }
 
@@ -538,6 +514,7 @@ __global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_rou
 // per key through a per-epoch table keyed by a 64-bit hash of the key (the winner then stores the
 // key, and a second pass checks every writer's key against it: a hash collision of two different keys
 // sends the epoch to the serial replay).
+namespace {
 KDEV uint64_t vkey_hash(int64_t k0, int64_t k1) { return mix64((uint64_t)k0 * 0xc2b2ae3d27d4eb4full ^ mix64((uint64_t)k1 + 1)) | 1ull; }
 // The slot of key hash h (insert: claimed when absent), or -1.  A position value is a small pair, so
 // a few keys take most value writes of an epoch: the probe reads before it claims (no atomic on a
@@ -559,38 +536,38 @@ KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert) {
 KDEV void vk_max(KG unsigned long long* p, unsigned long long v) {
     if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) atomicMax(p, v);
 }
-__global__ void __launch_bounds__(256) k_lvw_classify(DevState S, EpochIO io) {
+}  // namespace
+__global__ void __launch_bounds__(256) k_lvw_classify(DevState S) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t ns = lseqs(S, io);
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += gridDim.x * blockDim.x) {
-        const uint32_t s = ns - 1 - k;
-        const uint32_t meta = S.lvw_meta[s];
+    const uint32_t no = lops(S);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < no; k += gridDim.x * blockDim.x) {
+        const uint32_t p = no - 1 - k;           // (top-down: see vk_max)
+        const uint32_t meta = S.lvw_meta[p];
         if (!(meta & 3u)) continue;
-        const int32_t c = S.lvw_tgt[s];
+        const int32_t c = S.lvw_tgt[p];
+        const uint32_t es = S.lsrt[p].es;
         if (c >= 0) {
-            if ((uint32_t)c != (meta >> 2) && s > S.lchain[c].last_seq) {
-                KG uint32_t* l = &S.lchain[c].late;
-                if (__hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < s + 1) atomicMax(l, s + 1);
-            }
+            if ((uint32_t)c != (meta >> 2) && es > S.lchain[c].last_seq)
+                vk_max(reinterpret_cast<KG unsigned long long*>(&S.lchain[c].late), (unsigned long long)(es + 1) << 32 | p);
             continue;
         }
-        const long4 w = S.lvw[s];
-        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), true);
-        if (p < 0) { lfallback(S); return; }
-        vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[p]) + 1, (unsigned long long)s + 1);
+        const long4 w = S.lvw[p];
+        const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), true);
+        if (v < 0) { lfallback(S); return; }
+        vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[v]) + 1, (unsigned long long)es + 1);
     }
 }
-__global__ void __launch_bounds__(256) k_lvw_claim(DevState S, EpochIO io, int check) {
+__global__ void __launch_bounds__(256) k_lvw_claim(DevState S, int check) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t ns = lseqs(S, io);
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
-        if (!(S.lvw_meta[s] & 3u) || S.lvw_tgt[s] >= 0) continue;
-        const long4 w = S.lvw[s];
-        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), false);
-        if (p < 0) { lfallback(S); return; }
-        KG ulonglong4& e = S.lvk[p];
+    const uint32_t no = lops(S);
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < no; p += gridDim.x * blockDim.x) {
+        if (!(S.lvw_meta[p] & 3u) || S.lvw_tgt[p] >= 0) continue;
+        const long4 w = S.lvw[p];
+        const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
+        if (v < 0) { lfallback(S); return; }
+        KG ulonglong4& e = S.lvk[v];
         if (!check) {
-            if (e.y == (unsigned long long)s + 1) { e.z = (unsigned long long)w.x; e.w = (unsigned long long)w.y; }
+            if (e.y == (unsigned long long)S.lsrt[p].es + 1) { e.z = (unsigned long long)w.x; e.w = (unsigned long long)w.y; }
         } else if ((int64_t)e.z != w.x || (int64_t)e.w != w.y) {
             lfallback(S);   // two keys with one hash
         }
@@ -608,43 +585,44 @@ __global__ void __launch_bounds__(256) k_lacct(DevState S, EpochIO io) {
         atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[io.aid[i]]), (unsigned long long)(int64_t)io.size[i]);
     }
 }
-// Updates in place and deletes; a key to create is left to k_linsert (the VW winner's vk entry marked
-// LVK_INSERT, the chain by its state).
-constexpr unsigned long long LVK_INSERT = 1ull << 62;
+// Updates in place and deletes; a key to create is left to k_linsert (the winning value write's
+// lvw_tgt = VT_INSERT, the chain by its state).
+namespace {
 KDEV bool chain_final(const DevState& S, const KG LChain& c, int64_t& fa, int64_t& fv) {
     bool fp = c.fpres != 0;
     fa = c.fa; fv = c.fv;
     if (c.late) {
-        const uint32_t s = c.late - 1;
-        const long4 w = S.lvw[s];
-        fp = (S.lvw_meta[s] & 3u) == VW_PUT;
+        const uint32_t p = (uint32_t)c.late;
+        const long4 w = S.lvw[p];
+        fp = (S.lvw_meta[p] & 3u) == VW_PUT;
         fa = w.z;
         fv = w.w;
     }
     return fp;
 }
-__global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io) {
+}  // namespace
+__global__ void __launch_bounds__(256) k_lcommit(DevState S) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t ns = lseqs(S, io), no = lops(S);
+    const uint32_t no = lops(S);
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
-    // the winning value write of each key no chain reads
-    for (uint32_t s = t0; s < ns; s += stride) {
-        const uint32_t meta = S.lvw_meta[s];
-        if (!(meta & 3u) || S.lvw_tgt[s] >= 0) continue;
-        const long4 w = S.lvw[s];
-        const int64_t p = vk_slot(S, vkey_hash(w.x, w.y), false);
-        if (p < 0 || (S.lvk[p].y & ~LVK_INSERT) != (unsigned long long)s + 1) continue;
-        const int32_t h = pos_lookup(S, w.x, w.y);
-        if ((meta & 3u) == VW_DEL) {
-            if (h >= 0) S.pos_state[h] = 2u;
-        } else if (h >= 0) {
-            S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
-        } else {
-            S.lvk[p].y |= LVK_INSERT;
-        }
-    }
-    // every chain's final entry (its own last state, or a later value write into it)
     for (uint32_t p = t0; p < no; p += stride) {
+        // the winning value write of each key no chain reads
+        const uint32_t meta = S.lvw_meta[p];
+        if ((meta & 3u) && S.lvw_tgt[p] < 0) {
+            const long4 w = S.lvw[p];
+            const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
+            if (v >= 0 && S.lvk[v].y == (unsigned long long)S.lsrt[p].es + 1) {
+                const int32_t h = pos_lookup(S, w.x, w.y);
+                if ((meta & 3u) == VW_DEL) {
+                    if (h >= 0) S.pos_state[h] = 2u;
+                } else if (h >= 0) {
+                    S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
+                } else {
+                    S.lvw_tgt[p] = VT_INSERT;
+                }
+            }
+        }
+        // every chain's final entry (its own last state, or a later value write into it)
         const KG LChain& c = S.lchain[p];
         if (c.aid < 0 || !c.ipres) continue;
         int64_t fa, fv;
@@ -659,24 +637,21 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io) {
 __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
     const uint32_t no = lops(S);
-    const uint64_t nvk = S.lvk_mask + 1;
     uint32_t grew = 0;
     bool full = false;
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t p = t0; p < no; p += stride) {
+        if ((S.lvw_meta[p] & 3u) && S.lvw_tgt[p] == VT_INSERT) {
+            const long4 w = S.lvw[p];
+            const int r = pos_insert(S, w.x, w.y, w.z, w.w);
+            full |= r < 0;
+            grew += r > 0;
+        }
         const KG LChain& c = S.lchain[p];
         if (c.aid < 0 || c.ipres) continue;
         int64_t fa, fv;
         if (!chain_final(S, c, fa, fv)) continue;
         const int r = pos_insert(S, (int64_t)c.aid, c.sid, fa, fv);
-        full |= r < 0;
-        grew += r > 0;
-    }
-    for (uint64_t p = t0; p < nvk; p += stride) {
-        const ulonglong4 e = S.lvk[p];
-        if (!(e.y & LVK_INSERT)) continue;
-        const long4 w = S.lvw[(uint32_t)(e.y & ~LVK_INSERT) - 1];
-        const int r = pos_insert(S, w.x, w.y, w.z, w.w);
         full |= r < 0;
         grew += r > 0;
     }
@@ -702,10 +677,10 @@ __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
 void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_trades, hipStream_t st) {
     const uint32_t n = io.n;
     auto cdiv = [](uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); };
-    const uint64_t nseq = (uint64_t)n + 2ull * max_trades;
+    const uint64_t nops = (uint64_t)n + 2ull * max_trades;    // (ops: at most one per arrival number)
     (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
-    (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nseq, st);
-    (void)hipMemsetAsync(S.lxmark, 0, nseq, st);
+    (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nops, st);
+    (void)hipMemsetAsync(S.lxmark, 0, nops, st);
     (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
     (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
     (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
@@ -722,25 +697,25 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.ghist = S.lghist;
     R.rank = nullptr;
     R.none = 0;
-    R.n = n + max_trades;
+    R.n = (uint32_t)nops;
     R.n_dev = S.lctr + ci(LC_OPS);
     R.passes = S.lpasses;
     launch_radix(R, st);
-    hipLaunchKernelGGL(k_lseg, dim3(cdiv(n + max_trades + 1ull, 256)), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_lchains, dim3(std::min<uint32_t>(cdiv(n + max_trades, 256), 8192)), dim3(256), 0, st, S, io);
-    const uint32_t gs = std::min<uint32_t>(cdiv(nseq, 256), 4096);
-    hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
+    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), 8192);
+    hipLaunchKernelGGL(k_lchains, dim3(gs), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
     // (with no coupling the first round's link finds none, runs nothing and the detect converges)
     for (uint32_t r = 0; r < S.lrounds; ++r) {
         hipLaunchKernelGGL(k_lr_link, dim3(64), dim3(256), 0, st, S);
-        hipLaunchKernelGGL(k_lr_run, dim3(256), dim3(256), 0, st, S, io);
+        hipLaunchKernelGGL(k_lr_run, dim3(256), dim3(256), 0, st, S);
         hipLaunchKernelGGL(k_lr_detect, dim3(64), dim3(256), 0, st, S, (uint32_t)(r + 1 == S.lrounds));
     }
-    hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 0);
-    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, io, 1);
+    hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, 0);
+    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, 1);
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_linsert, dim3(gs), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lbalances, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }

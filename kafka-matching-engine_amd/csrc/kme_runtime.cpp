@@ -273,9 +273,10 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         if (S.ledger_replay) ALLOC(S.vic, E);
     }
     if (S.ledger_replay) {   // the parallel ledger pass (kme_ledger.hip); KME_LEDGER_SERIAL=1: the serial replay only
-        const uint64_t nops = (uint64_t)E + cfg->max_trades, nseq = (uint64_t)E + 2ull * cfg->max_trades;
+        // ops: one per ledger effect (a check / cancel per record, two fills per trade)
+        const uint64_t nops = (uint64_t)E + 2ull * cfg->max_trades;
         const char* ls = std::getenv("KME_LEDGER_SERIAL");
-        S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && nseq < (1ull << 30) ? 1 : 0;
+        S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && nops < (1ull << 30) ? 1 : 0;
         if (S.lpar) {
             int bits = 0;
             while ((1ull << bits) < ((uint64_t)cfg->max_accounts << 8)) ++bits;
@@ -285,7 +286,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             S.lc_cap = 1u << 20;     // value writes changed in one round
             S.lrounds = 8;           // repair rounds before the serial replay (KME_LEDGER_ROUNDS: tests)
             if (const char* v = std::getenv("KME_LEDGER_ROUNDS")) S.lrounds = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-            const uint64_t vk = pow2_at_least(std::min<uint64_t>(2 * nseq, 1ull << 22));
+            const uint64_t vk = pow2_at_least(std::min<uint64_t>(2 * nops, 1ull << 22));
             S.lvk_mask = vk - 1;
             const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE - 1) / RADIX_TILE);
             ALLOC(S.lcnt, E);
@@ -294,14 +295,14 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lkey[0], nops); ALLOC(S.lkey[1], nops);
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
-            ALLOC(S.lop, nseq); ALLOC(S.lsid, nseq); ALLOC(S.lssid, nops);
+            ALLOC(S.lrec, nops); ALLOC(S.lsrt, nops);
             ALLOC(S.lchain, nops);
-            ALLOC(S.lvw, nseq); ALLOC(S.lvw_meta, nseq); ALLOC(S.lvw_tgt, nseq);
+            ALLOC(S.lvw, nops); ALLOC(S.lvw_meta, nops); ALLOC(S.lvw_tgt, nops);
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
             ALLOC(S.ldelta, cfg->max_accounts);
             ALLOC(S.lvk, vk);
             ALLOC(S.lx, S.lx_cap); ALLOC(S.lxn, S.lx_cap);
-            ALLOC(S.lxmark, nseq);
+            ALLOC(S.lxmark, nops);
             ALLOC(S.lrun, S.lr_cap);
             ALLOC(S.lchg, S.lc_cap);
             ALLOC(S.lctr, (size_t)LC_N * CTR_STRIDE);
