@@ -319,14 +319,18 @@ kme_status kme_router_split(kme_router* r, const kme_orders* in, uint32_t n, con
         a = (uint32_t)((uint64_t)n * t / T);
         b = (uint32_t)((uint64_t)n * (t + 1) / T);
     };
+    // (per-thread counters and write positions in thread-local memory: no shared cache line)
     parallel(T, [&](uint32_t t) {
         uint32_t a, b;
         range(t, a, b);
-        uint32_t* c = &cnt[(size_t)t * P];
+        std::vector<uint32_t> c(P, 0);
+        uint32_t all = 0;
         for (uint32_t i = a; i < b; ++i) {
-            if (dest[i] == KME_ROUTE_ALL) { for (uint32_t k = 0; k < P; ++k) ++c[k]; }
-            else ++c[dest[i]];
+            const int32_t d = dest[i];
+            if (d == KME_ROUTE_ALL) ++all;
+            else ++c[d];
         }
+        for (uint32_t k = 0; k < P; ++k) cnt[(size_t)t * P + k] = c[k] + all;
     });
     for (uint32_t k = 0; k < P; ++k) {   // each range's first slot in partition k
         uint32_t acc = 0;
@@ -340,7 +344,7 @@ kme_status kme_router_split(kme_router* r, const kme_orders* in, uint32_t n, con
     parallel(T, [&](uint32_t t) {
         uint32_t a, b;
         range(t, a, b);
-        uint32_t* o = &cnt[(size_t)t * P];
+        std::vector<uint32_t> o(&cnt[(size_t)t * P], &cnt[(size_t)t * P] + P);
         for (uint32_t i = a; i < b; ++i) {
             const int32_t d = dest[i];
             const uint32_t k0 = d == KME_ROUTE_ALL ? 0 : (uint32_t)d, k1 = d == KME_ROUTE_ALL ? P : (uint32_t)d + 1;
