@@ -106,18 +106,18 @@ struct LChain {
 };
 static_assert(sizeof(LChain) == 80, "LChain");
 // One ledger effect of the epoch (kme_ledger.hip): checkBalance, a fill, or postRemoveAdjustments on
-// the position (aid, sid), with its arrival number
+// the position (aid, sid) -- the account is the op's sort key -- with its arrival number.  FUNDED
+// sids are symbol groups (|sid| < max_symbols < 2^30) and prices 0..126, so both fit narrow fields.
 struct LOp {
-    int64_t sid;
+    int32_t sid;
     uint32_t es;                   // arrival number
-    int32_t size, price;           // the effect's size and price term
-    int32_t aid;
-    uint32_t flags;                // kind (check / fill / cancel) | buy << 2
-    uint32_t _pad;
+    int32_t size;
+    int16_t price;                 // the effect's price term
+    uint16_t flags;                // kind (check / fill / cancel) | buy << 2
 };
-static_assert(sizeof(LOp) == 32, "LOp");
+static_assert(sizeof(LOp) == 16, "LOp");
 // the ledger pass's counters (DevState::lctr, one line each)
-enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
+enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_HEADS, LC_N = 8 };
 
 // Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
 // counters never contend for one L2 line.
@@ -214,7 +214,8 @@ struct DevState {
     KG uint32_t* lghist;
     KG LOp* lrec;                     // per op, arrival order
     KG LOp* lsrt;                     // per op, sorted order (k_lseg gathers them once)
-    KG LChain* lchain;                // per sorted op
+    KG LChain* lchain;                // per sorted op (written at chain heads only)
+    KG uint32_t* lheads;              // the chain heads (sorted positions), in no particular order
     KG long4* lvw;                    // per sorted op: its value write (key, value)
     KG uint32_t* lvw_meta;            //   kind | writer chain << 2
     KG int32_t* lvw_tgt;              //   the chain it writes into (-1: none)

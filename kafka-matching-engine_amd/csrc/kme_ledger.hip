@@ -203,8 +203,8 @@ KDEV void write_into(PState& P, const VWrite& w) {
     }
 }
 
-// One op: its effect on its chain's position P; returns the balance delta, w = its value write.
-KDEV int64_t apply_op(const LOp& o, PState& P, VWrite& w) {
+// One op of chain (aid, o.sid): its effect on the position P; returns the balance delta, w = its value write.
+KDEV int64_t apply_op(const LOp& o, int64_t aid, PState& P, VWrite& w) {
     const bool buy = (o.flags >> 2) & 1u;
     const uint32_t kind = o.flags & 3u;
     w.kind = 0;
@@ -212,7 +212,7 @@ KDEV int64_t apply_op(const LOp& o, PState& P, VWrite& w) {
     if (kind == OP_CHECK) d = eff_check(P, buy, o.size, o.price);
     else if (kind == OP_FILL) d = eff_fill(P, buy, o.size, o.price, w);
     else d = eff_cancel(P, buy, o.size, o.price, w);
-    if (w.kind && w.k0 == (int64_t)o.aid && w.k1 == o.sid) write_into(P, w);   // into its own key
+    if (w.kind && w.k0 == aid && w.k1 == (int64_t)o.sid) write_into(P, w);   // into its own key
     return d;
 }
 
@@ -233,7 +233,7 @@ KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
     const uint32_t key = lkey_of(k0, k1);
     const uint32_t hi = S.lseg[k0 + 1];
     for (uint32_t p = lower_bound(K, S.lseg[k0], hi, key); p < hi && K[p] == key; ++p)
-        if (S.lsrt[p].sid == k1) return (int32_t)p;
+        if ((int64_t)S.lsrt[p].sid == k1) return (int32_t)p;
     return -1;
 }
 
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
     const uint32_t t0 = io.trade_off[i];
     auto put = [&](int64_t aid, int64_t sid, uint32_t es, int32_t size, int32_t price, uint32_t flags) {
         LOp op;
-        op.sid = sid; op.es = es; op.size = size; op.price = price; op.aid = (int32_t)aid; op.flags = flags; op._pad = 0;
+        op.sid = (int32_t)sid; op.es = es; op.size = size; op.price = (int16_t)price; op.flags = (uint16_t)flags;
         S.lrec[o] = op;
         S.lk0[o] = lkey_of(aid, sid);
         S.lv0[o] = o;
@@ -316,17 +316,16 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
     for (uint32_t base = blockIdx.x * blockDim.x; base < no; base += gridDim.x * blockDim.x) {
         const uint32_t j = base + threadIdx.x;
         int64_t aid = -1, cd = 0;
+        bool head = false;
         if (j < no) {
             const uint32_t bj = K[j];
-            const int64_t sid = S.lsrt[j].sid;
+            const int32_t sid = S.lsrt[j].sid;
             aid = bj >> LB_BUCKET_BITS;
-            bool head = true;
+            head = true;
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
                 if (S.lsrt[p - 1].sid == sid) { head = false; break; }
-            KG LChain& c = S.lchain[j];
-            if (!head) {
-                c.aid = -1;
-            } else {
+            if (head) {
+                KG LChain& c = S.lchain[j];
                 const int32_t slot = pos_lookup(S, aid, sid);
                 PState P;
                 P.present = slot >= 0;
@@ -339,7 +338,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
                     const LOp op = S.lsrt[p];
                     if (op.sid != sid) continue;
                     VWrite w;
-                    cd = jladd(cd, apply_op(op, P, w));
+                    cd = jladd(cd, apply_op(op, aid, P, w));
                     last = op.es;
                     if (w.kind) {
                         S.lvw[p] = make_long4(w.k0, w.k1, w.v0, w.v1);
@@ -350,6 +349,12 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
                 c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
             }
         }
+        // the heads into the list: one atomic per wavefront
+        const uint64_t hm = __ballot(head);
+        uint32_t hb = 0;
+        if (lane == 0 && hm) hb = (uint32_t)atomicAdd(lc(S, LC_HEADS), (unsigned long long)__popcll(hm));
+        hb = (uint32_t)__shfl((int)hb, 0, 64);
+        if (head) S.lheads[hb + __popcll(hm & ((1ull << lane) - 1))] = j;
         // segmented inclusive sum of cd over runs of equal aid (wrap-around, order-free)
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)cd, off, 64);
@@ -445,7 +450,8 @@ __global__ void __launch_bounds__(256) k_lr_run(DevState S) {
             in[k] = e;
         }
         c.rix = 0;
-        const int64_t sid = c.sid;
+        const int32_t sid = (int32_t)c.sid;
+        const int64_t aid = c.aid;
         PState P{c.ia, c.iv, c.ipres != 0};
         int64_t cd = 0;
         int q = 0;
@@ -458,7 +464,7 @@ __global__ void __launch_bounds__(256) k_lr_run(DevState S) {
                 write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[ip] & 3u});
             }
             VWrite w;
-            cd = jladd(cd, apply_op(op, P, w));
+            cd = jladd(cd, apply_op(op, aid, P, w));
             const uint32_t om = S.lvw_meta[p];
             const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
             bool changed = (om & 3u) != (nm & 3u);
@@ -511,20 +517,23 @@ __global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_rou
 // ---------------------------------------------------------------- 6. commit
 // Value writes: into a chain of the epoch after its last read -> the chain's final value (latest
 // wins, `late`); into a chain it reads later -> already applied; into no chain -> last-writer-wins
-// per key through a per-epoch table keyed by a 64-bit hash of the key (the winner then stores the
-// key, and a second pass checks every writer's key against it: a hash collision of two different keys
-// sends the epoch to the serial replay).
+// per key through a per-epoch table keyed by a 64-bit hash of the key (the key stored by the writer
+// that inserted it, and a second pass checks every writer's key against it: a hash collision of two
+// different keys sends the epoch to the serial replay).
 namespace {
 KDEV uint64_t vkey_hash(int64_t k0, int64_t k1) { return mix64((uint64_t)k0 * 0xc2b2ae3d27d4eb4full ^ mix64((uint64_t)k1 + 1)) | 1ull; }
 // The slot of key hash h (insert: claimed when absent), or -1.  A position value is a small pair, so
 // a few keys take most value writes of an epoch: the probe reads before it claims (no atomic on a
 // hot key's line unless the slot is empty).
-KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert) {
+KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert, bool* inserted = nullptr) {
     uint64_t p = h & S.lvk_mask;
     for (uint32_t probes = 0; probes < 4096; ++probes) {
         KG unsigned long long* e = reinterpret_cast<KG unsigned long long*>(&S.lvk[p]);
         unsigned long long cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == 0 && insert) cur = atomicCAS(e, 0ull, (unsigned long long)h);
+        if (cur == 0 && insert) {
+            cur = atomicCAS(e, 0ull, (unsigned long long)h);
+            if (cur == 0 && inserted) *inserted = true;
+        }
         if (cur == h || (insert && cur == 0)) return (int64_t)p;
         if (cur == 0) return -1;
         p = (p + 1) & S.lvk_mask;
@@ -552,25 +561,23 @@ __global__ void __launch_bounds__(256) k_lvw_classify(DevState S) {
             continue;
         }
         const long4 w = S.lvw[p];
-        const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), true);
+        bool ins = false;
+        const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), true, &ins);
         if (v < 0) { lfallback(S); return; }
+        if (ins) { S.lvk[v].z = (unsigned long long)w.x; S.lvk[v].w = (unsigned long long)w.y; }   // the key, by its inserter
         vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[v]) + 1, (unsigned long long)es + 1);
     }
 }
-__global__ void __launch_bounds__(256) k_lvw_claim(DevState S, int check) {
+// Every writer's key against the one its hash slot holds: two keys with one hash send the epoch to
+// the serial replay.
+__global__ void __launch_bounds__(256) k_lvw_check(DevState S) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
     const uint32_t no = lops(S);
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < no; p += gridDim.x * blockDim.x) {
         if (!(S.lvw_meta[p] & 3u) || S.lvw_tgt[p] >= 0) continue;
         const long4 w = S.lvw[p];
         const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
-        if (v < 0) { lfallback(S); return; }
-        KG ulonglong4& e = S.lvk[v];
-        if (!check) {
-            if (e.y == (unsigned long long)S.lsrt[p].es + 1) { e.z = (unsigned long long)w.x; e.w = (unsigned long long)w.y; }
-        } else if ((int64_t)e.z != w.x || (int64_t)e.w != w.y) {
-            lfallback(S);   // two keys with one hash
-        }
+        if (v < 0 || (int64_t)S.lvk[v].z != w.x || (int64_t)S.lvk[v].w != w.y) { lfallback(S); return; }
     }
 }
 // Account records (createBalance / transfer, KP:131-146): outcomes fixed by k_ledger_funded.
@@ -603,28 +610,28 @@ KDEV bool chain_final(const DevState& S, const KG LChain& c, int64_t& fa, int64_
 }  // namespace
 __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t no = lops(S);
+    const uint32_t no = lops(S), nh = (uint32_t)S.lctr[ci(LC_HEADS)];
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    // the winning value write of each key no chain reads
     for (uint32_t p = t0; p < no; p += stride) {
-        // the winning value write of each key no chain reads
         const uint32_t meta = S.lvw_meta[p];
-        if ((meta & 3u) && S.lvw_tgt[p] < 0) {
-            const long4 w = S.lvw[p];
-            const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
-            if (v >= 0 && S.lvk[v].y == (unsigned long long)S.lsrt[p].es + 1) {
-                const int32_t h = pos_lookup(S, w.x, w.y);
-                if ((meta & 3u) == VW_DEL) {
-                    if (h >= 0) S.pos_state[h] = 2u;
-                } else if (h >= 0) {
-                    S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
-                } else {
-                    S.lvw_tgt[p] = VT_INSERT;
-                }
-            }
+        if (!(meta & 3u) || S.lvw_tgt[p] >= 0) continue;
+        const long4 w = S.lvw[p];
+        const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
+        if (v < 0 || S.lvk[v].y != (unsigned long long)S.lsrt[p].es + 1) continue;
+        const int32_t h = pos_lookup(S, w.x, w.y);
+        if ((meta & 3u) == VW_DEL) {
+            if (h >= 0) S.pos_state[h] = 2u;
+        } else if (h >= 0) {
+            S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
+        } else {
+            S.lvw_tgt[p] = VT_INSERT;
         }
-        // every chain's final entry (its own last state, or a later value write into it)
-        const KG LChain& c = S.lchain[p];
-        if (c.aid < 0 || !c.ipres) continue;
+    }
+    // every chain's final entry (its own last state, or a later value write into it)
+    for (uint32_t k = t0; k < nh; k += stride) {
+        const KG LChain& c = S.lchain[S.lheads[k]];
+        if (!c.ipres) continue;
         int64_t fa, fv;
         const bool fp = chain_final(S, c, fa, fv);
         if (fp && fa == c.ia && fv == c.iv) continue;
@@ -636,19 +643,20 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
 // into absent keys.  Every key is new and inserted by one thread (pos_insert).
 __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t no = lops(S);
+    const uint32_t no = lops(S), nh = (uint32_t)S.lctr[ci(LC_HEADS)];
     uint32_t grew = 0;
     bool full = false;
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t p = t0; p < no; p += stride) {
-        if ((S.lvw_meta[p] & 3u) && S.lvw_tgt[p] == VT_INSERT) {
-            const long4 w = S.lvw[p];
-            const int r = pos_insert(S, w.x, w.y, w.z, w.w);
-            full |= r < 0;
-            grew += r > 0;
-        }
-        const KG LChain& c = S.lchain[p];
-        if (c.aid < 0 || c.ipres) continue;
+        if (!(S.lvw_meta[p] & 3u) || S.lvw_tgt[p] != VT_INSERT) continue;
+        const long4 w = S.lvw[p];
+        const int r = pos_insert(S, w.x, w.y, w.z, w.w);
+        full |= r < 0;
+        grew += r > 0;
+    }
+    for (uint32_t k = t0; k < nh; k += stride) {
+        const KG LChain& c = S.lchain[S.lheads[k]];
+        if (c.ipres) continue;
         int64_t fa, fv;
         if (!chain_final(S, c, fa, fv)) continue;
         const int r = pos_insert(S, (int64_t)c.aid, c.sid, fa, fv);
@@ -712,8 +720,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
         hipLaunchKernelGGL(k_lr_detect, dim3(64), dim3(256), 0, st, S, (uint32_t)(r + 1 == S.lrounds));
     }
     hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, 0);
-    hipLaunchKernelGGL(k_lvw_claim, dim3(gs), dim3(256), 0, st, S, 1);
+    hipLaunchKernelGGL(k_lvw_check, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_linsert, dim3(gs), dim3(256), 0, st, S, io);

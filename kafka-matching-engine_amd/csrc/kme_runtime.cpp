@@ -276,7 +276,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         // ops: one per ledger effect (a check / cancel per record, two fills per trade)
         const uint64_t nops = (uint64_t)E + 2ull * cfg->max_trades;
         const char* ls = std::getenv("KME_LEDGER_SERIAL");
-        S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && nops < (1ull << 30) ? 1 : 0;
+        S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && cfg->max_symbols < (1u << 30) &&
+                 nops < (1ull << 30) ? 1 : 0;
         if (S.lpar) {
             int bits = 0;
             while ((1ull << bits) < ((uint64_t)cfg->max_accounts << 8)) ++bits;
@@ -296,7 +297,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
             ALLOC(S.lrec, nops); ALLOC(S.lsrt, nops);
-            ALLOC(S.lchain, nops);
+            ALLOC(S.lchain, nops); ALLOC(S.lheads, nops);
             ALLOC(S.lvw, nops); ALLOC(S.lvw_meta, nops); ALLOC(S.lvw_tgt, nops);
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
             ALLOC(S.ldelta, cfg->max_accounts);
