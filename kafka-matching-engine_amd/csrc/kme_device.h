@@ -117,7 +117,7 @@ struct LOp {
 };
 static_assert(sizeof(LOp) == 16, "LOp");
 // the ledger pass's counters (DevState::lctr, one line each)
-enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_HEADS, LC_N = 8 };
+enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
 
 // Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
 // counters never contend for one L2 line.
@@ -215,7 +215,7 @@ struct DevState {
     KG LOp* lrec;                     // per op, arrival order
     KG LOp* lsrt;                     // per op, sorted order (k_lseg gathers them once)
     KG LChain* lchain;                // per sorted op (written at chain heads only)
-    KG uint32_t* lheads;              // the chain heads (sorted positions), in no particular order
+    KG uint8_t* lhead;                // per sorted op: 1 = it heads its chain
     KG long4* lvw;                    // per sorted op: its value write (key, value)
     KG uint32_t* lvw_meta;            //   kind | writer chain << 2
     KG int32_t* lvw_tgt;              //   the chain it writes into (-1: none)

@@ -349,12 +349,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
                 c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
             }
         }
-        // the heads into the list: one atomic per wavefront
-        const uint64_t hm = __ballot(head);
-        uint32_t hb = 0;
-        if (lane == 0 && hm) hb = (uint32_t)atomicAdd(lc(S, LC_HEADS), (unsigned long long)__popcll(hm));
-        hb = (uint32_t)__shfl((int)hb, 0, 64);
-        if (head) S.lheads[hb + __popcll(hm & ((1ull << lane) - 1))] = j;
+        if (j < no) S.lhead[j] = head ? 1 : 0;   // (a list would serialise on one counter)
         // segmented inclusive sum of cd over runs of equal aid (wrap-around, order-free)
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)cd, off, 64);
@@ -610,7 +605,7 @@ KDEV bool chain_final(const DevState& S, const KG LChain& c, int64_t& fa, int64_
 }  // namespace
 __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t no = lops(S), nh = (uint32_t)S.lctr[ci(LC_HEADS)];
+    const uint32_t no = lops(S);
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
     // the winning value write of each key no chain reads
     for (uint32_t p = t0; p < no; p += stride) {
@@ -629,8 +624,9 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         }
     }
     // every chain's final entry (its own last state, or a later value write into it)
-    for (uint32_t k = t0; k < nh; k += stride) {
-        const KG LChain& c = S.lchain[S.lheads[k]];
+    for (uint32_t p = t0; p < no; p += stride) {
+        if (!S.lhead[p]) continue;
+        const KG LChain& c = S.lchain[p];
         if (!c.ipres) continue;
         int64_t fa, fv;
         const bool fp = chain_final(S, c, fa, fv);
@@ -643,7 +639,7 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
 // into absent keys.  Every key is new and inserted by one thread (pos_insert).
 __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
-    const uint32_t no = lops(S), nh = (uint32_t)S.lctr[ci(LC_HEADS)];
+    const uint32_t no = lops(S);
     uint32_t grew = 0;
     bool full = false;
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -654,8 +650,9 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
         full |= r < 0;
         grew += r > 0;
     }
-    for (uint32_t k = t0; k < nh; k += stride) {
-        const KG LChain& c = S.lchain[S.lheads[k]];
+    for (uint32_t p = t0; p < no; p += stride) {
+        if (!S.lhead[p]) continue;
+        const KG LChain& c = S.lchain[p];
         if (c.ipres) continue;
         int64_t fa, fv;
         if (!chain_final(S, c, fa, fv)) continue;

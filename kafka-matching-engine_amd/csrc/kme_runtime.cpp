@@ -297,7 +297,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
             ALLOC(S.lrec, nops); ALLOC(S.lsrt, nops);
-            ALLOC(S.lchain, nops); ALLOC(S.lheads, nops);
+            ALLOC(S.lchain, nops); ALLOC(S.lhead, nops);
             ALLOC(S.lvw, nops); ALLOC(S.lvw_meta, nops); ALLOC(S.lvw_tgt, nops);
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
             ALLOC(S.ldelta, cfg->max_accounts);
