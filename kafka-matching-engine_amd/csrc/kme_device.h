@@ -202,7 +202,7 @@ struct DevState {
     KG unsigned long long* ctr;       // C_NCTR x CTR_STRIDE words
     KG unsigned long long* dbg;     // diagnostic stamps (KME_STAMPS builds), G x 16 words
     // FUNDED + exact ledger, applied in parallel (kme_ledger.hip; lpar = 0: the serial replay)
-    int32_t lpar, lpasses;
+    int32_t lpar, lpasses, lhbits, _lpad2;
     uint32_t lr_cap, lx_cap, lc_cap, lrounds;
     uint64_t lvk_mask;
     KG uint32_t* lcnt;                // per record: its ops, then their offset

@@ -21,7 +21,7 @@
 //   * A value write whose key is another chain of this epoch, read after the write, couples the two
 //     chains: the reference clobbers that real position.  k_ldetect finds them; repair rounds re-run
 //     the coupled chains in parallel, each with its incoming value writes merged in arrival order,
-//     until a fixed point (k_lr_link / k_lr_run / k_lr_detect).  At C3 (65,536 accounts x 65,536
+//     until a fixed point (k_lr_rounds: link / run / detect).  At C3 (65,536 accounts x 65,536
 //     symbols) thousands of position values per epoch are also live keys -- (amount, available) ~
 //     (50, 50) is account 50's position on symbol 50.  No fixed point within S.lrounds rounds, or
 //     past a capacity, sends the epoch to the serial replay (k_ledger_replay).
@@ -46,13 +46,15 @@ namespace kme {
 
 namespace {
 
-constexpr int LB_BUCKET_BITS = 8;                 // hash8(sid): 256 buckets per account
+// sort key: aid << S.lhbits | a hash of the sid in lhbits bits (the runtime picks lhbits so that the
+// key needs the fewest radix passes: 2 bits at 65,536 accounts, 8 bits below 1,024)
 constexpr uint32_t OP_CHECK = 0u, OP_FILL = 1u, OP_CANCEL = 2u;   // LOp::flags & 3 (bit 2: buy / bought)
 constexpr uint32_t VW_PUT = 1u, VW_DEL = 2u;
 constexpr int32_t VT_NONE = -1, VT_INSERT = -2;     // lvw_tgt: into no chain of the epoch / a winner to create
 
-KDEV uint32_t hash8(int64_t sid) { return (uint32_t)(mix64((uint64_t)sid ^ 0x632be59bd9b4e019ull) >> 56); }
-KDEV uint32_t lkey_of(int64_t aid, int64_t sid) { return (uint32_t)aid << LB_BUCKET_BITS | hash8(sid); }
+KDEV uint32_t lkey_of(const DevState& S, int64_t aid, int64_t sid) {
+    return (uint32_t)aid << S.lhbits | (uint32_t)(mix64((uint64_t)sid ^ 0x632be59bd9b4e019ull) >> (64 - S.lhbits));
+}
 
 KDEV unsigned long long* lc(const DevState& S, int k) { return &S.lctr[ci(k)]; }
 KDEV void lfallback(const DevState& S) { atomicOr(lc(S, LC_FALLBACK), 1ull); }
@@ -230,7 +232,7 @@ KDEV uint32_t lower_bound(const KG uint32_t* k, uint32_t lo, uint32_t hi, uint32
 KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
     if (k0 < 0 || k0 >= S.A) return -1;
     const KG uint32_t* K = skeys(S);
-    const uint32_t key = lkey_of(k0, k1);
+    const uint32_t key = lkey_of(S, k0, k1);
     const uint32_t hi = S.lseg[k0 + 1];
     for (uint32_t p = lower_bound(K, S.lseg[k0], hi, key); p < hi && K[p] == key; ++p)
         if ((int64_t)S.lsrt[p].sid == k1) return (int32_t)p;
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
         LOp op;
         op.sid = (int32_t)sid; op.es = es; op.size = size; op.price = (int16_t)price; op.flags = (uint16_t)flags;
         S.lrec[o] = op;
-        S.lk0[o] = lkey_of(aid, sid);
+        S.lk0[o] = lkey_of(S, aid, sid);
         S.lv0[o] = o;
         ++o;
     };
@@ -296,8 +298,8 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     if (k > n || n == 0) return;      // (no ops: lseg stays zero)
     const KG uint32_t* K = skeys(S);
     if (k < n) S.lsrt[k] = S.lrec[svals(S)[k]];
-    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> LB_BUCKET_BITS);
-    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> LB_BUCKET_BITS);
+    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
+    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
     for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
 }
 
@@ -320,7 +322,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
         if (j < no) {
             const uint32_t bj = K[j];
             const int32_t sid = S.lsrt[j].sid;
-            aid = bj >> LB_BUCKET_BITS;
+            aid = bj >> S.lhbits;
             head = true;
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
                 if (S.lsrt[p - 1].sid == sid) { head = false; break; }
@@ -396,24 +398,23 @@ __global__ void __launch_bounds__(256) k_ldetect(DevState S) {
 // The coupled chains re-run in parallel, each with the value writes into it merged into its own
 // effects in arrival order, until nothing changes (a fixed point: a value write only affects later
 // effects, so after round r every effect whose causal chain of couplings is at most r deep is
-// final).  Round: (a) k_lr_link threads each chain's incoming couplings into a list and adds the
-// chain to the run list (which only grows: a chain whose coupling went away re-runs without it);
-// (b) k_lr_run re-runs every chain of the run list from its start state -- new final state, balance
-// delta (the difference goes to the account's sum) and value writes, the changed ones listed; (c)
-// k_lr_detect re-targets the changed value writes and lists new couplings; no change = converged
-// (LC_DONE: the later rounds' launches return at once).  Not converged in S.lrounds rounds, or past a
-// capacity: the epoch goes to the serial replay.
+// final).  Round: (a) link: each chain's incoming couplings threaded into a list, the chain added to
+// the run list (which only grows: a chain whose coupling went away re-runs without it); (b) run:
+// every chain of the run list re-run from its start state -- new final state, balance delta (the
+// difference goes to the account's sum) and value writes, the changed ones listed; (c) detect: the
+// changed value writes re-targeted, new couplings listed.  No change = converged.  Not converged in
+// S.lrounds rounds, or past a capacity: the epoch goes to the serial replay.
+//
+// One workgroup runs all rounds (k_lr_rounds: the phases separated by barriers, so an epoch without
+// couplings costs one launch; thousands of coupled chains take a few microseconds per round).  Values
+// another thread wrote by atomics are read back with atomic loads.
 namespace {
-KDEV bool lr_active(const DevState& S) {
-    return !lskip(S) && lops(S) != 0 && S.lctr[ci(LC_DONE)] == 0 && !lfell(S);
+KDEV uint32_t lc_get(const DevState& S, int k) {
+    return (uint32_t)__hip_atomic_load(lc(S, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-}  // namespace
-__global__ void __launch_bounds__(256) k_lr_link(DevState S) {
-    if (!lr_active(S)) return;
-    const uint32_t nx = (uint32_t)min(S.lctr[ci(LC_CROSS)], (unsigned long long)S.lx_cap);
-    const uint32_t x0 = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x0 == 0) S.lctr[ci(LC_CHG)] = 0;         // (the run kernel's list, filled after this launch)
-    for (uint32_t x = x0; x < nx; x += gridDim.x * blockDim.x) {
+KDEV void lr_link(const DevState& S, uint32_t t0, uint32_t nt) {
+    const uint32_t nx = min(lc_get(S, LC_CROSS), S.lx_cap);
+    for (uint32_t x = t0; x < nx; x += nt) {
         const uint32_t p = S.lx[x];
         const int32_t c = S.lvw_tgt[p];
         if (!coupling(S, p, S.lvw_meta[p], c)) continue;
@@ -425,78 +426,57 @@ __global__ void __launch_bounds__(256) k_lr_link(DevState S) {
     }
 }
 constexpr int LR_IN = 32;   // incoming value writes one chain takes in a round (more: the serial replay)
-__global__ void __launch_bounds__(256) k_lr_run(DevState S) {
-    if (!lr_active(S)) return;
-    const uint32_t nd = (uint32_t)min(S.lctr[ci(LC_DIRTY)], (unsigned long long)S.lr_cap);
+KDEV void lr_run_chain(const DevState& S, uint32_t head) {
     const uint32_t no = lops(S);
     const KG uint32_t* K = skeys(S);
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nd; d += gridDim.x * blockDim.x) {
-        const uint32_t head = S.lrun[d];
-        KG LChain& c = S.lchain[head];
-        // the incoming value writes (ops of other chains), in arrival order
-        uint64_t in[LR_IN];                       // arrival number << 32 | op position
-        int nin = 0;
-        for (uint32_t x = c.rix; x != 0; x = S.lxn[x - 1]) {
-            if (nin == LR_IN) { lfallback(S); return; }
-            const uint32_t p = S.lx[x - 1];
-            const uint64_t e = (uint64_t)S.lsrt[p].es << 32 | p;
-            int k = nin++;
-            for (; k > 0 && in[k - 1] > e; --k) in[k] = in[k - 1];
-            in[k] = e;
-        }
-        c.rix = 0;
-        const int32_t sid = (int32_t)c.sid;
-        const int64_t aid = c.aid;
-        PState P{c.ia, c.iv, c.ipres != 0};
-        int64_t cd = 0;
-        int q = 0;
-        for (uint32_t p = head; p < no && K[p] == K[head]; ++p) {
-            const LOp op = S.lsrt[p];
-            if (op.sid != sid) continue;
-            for (; q < nin && (uint32_t)(in[q] >> 32) < op.es; ++q) {
-                const uint32_t ip = (uint32_t)in[q];
-                const long4 x = S.lvw[ip];
-                write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[ip] & 3u});
-            }
-            VWrite w;
-            cd = jladd(cd, apply_op(op, aid, P, w));
-            const uint32_t om = S.lvw_meta[p];
-            const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
-            bool changed = (om & 3u) != (nm & 3u);
-            if (!changed && w.kind) {
-                const long4 ow = S.lvw[p];
-                changed = ow.x != w.k0 || ow.y != w.k1 || (w.kind == VW_PUT && (ow.z != w.v0 || ow.w != w.v1));
-            }
-            if (changed) {
-                S.lvw[p] = make_long4(w.k0, w.k1, w.v0, w.v1);
-                S.lvw_meta[p] = nm;
-                const unsigned long long k = atomicAdd(lc(S, LC_CHG), 1ull);
-                if (k < S.lc_cap) S.lchg[k] = p; else lfallback(S);
-            }
-        }
-        c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
-        atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[c.aid]), (unsigned long long)jlsub(cd, c.delta));
-        c.delta = cd;
+    KG LChain& c = S.lchain[head];
+    // the incoming value writes (ops of other chains), in arrival order
+    uint64_t in[LR_IN];                           // arrival number << 32 | op position
+    int nin = 0;
+    for (uint32_t x = __hip_atomic_load(&c.rix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); x != 0; x = S.lxn[x - 1]) {
+        if (nin == LR_IN) { lfallback(S); return; }
+        const uint32_t p = S.lx[x - 1];
+        const uint64_t e = (uint64_t)S.lsrt[p].es << 32 | p;
+        int k = nin++;
+        for (; k > 0 && in[k - 1] > e; --k) in[k] = in[k - 1];
+        in[k] = e;
     }
+    __hip_atomic_store(&c.rix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t sid = (int32_t)c.sid;
+    const int64_t aid = c.aid;
+    PState P{c.ia, c.iv, c.ipres != 0};
+    int64_t cd = 0;
+    int q = 0;
+    for (uint32_t p = head; p < no && K[p] == K[head]; ++p) {
+        const LOp op = S.lsrt[p];
+        if (op.sid != sid) continue;
+        for (; q < nin && (uint32_t)(in[q] >> 32) < op.es; ++q) {
+            const uint32_t ip = (uint32_t)in[q];
+            const long4 x = S.lvw[ip];
+            write_into(P, VWrite{x.x, x.y, x.z, x.w, S.lvw_meta[ip] & 3u});
+        }
+        VWrite w;
+        cd = jladd(cd, apply_op(op, aid, P, w));
+        const uint32_t om = S.lvw_meta[p];
+        const uint32_t nm = w.kind ? (w.kind | head << 2) : 0u;
+        bool changed = (om & 3u) != (nm & 3u);
+        if (!changed && w.kind) {
+            const long4 ow = S.lvw[p];
+            changed = ow.x != w.k0 || ow.y != w.k1 || (w.kind == VW_PUT && (ow.z != w.v0 || ow.w != w.v1));
+        }
+        if (changed) {
+            S.lvw[p] = make_long4(w.k0, w.k1, w.v0, w.v1);
+            S.lvw_meta[p] = nm;
+            const unsigned long long k = atomicAdd(lc(S, LC_CHG), 1ull);
+            if (k < S.lc_cap) S.lchg[k] = p; else lfallback(S);
+        }
+    }
+    c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
+    atomicAdd(reinterpret_cast<KG unsigned long long*>(&S.ldelta[c.aid]), (unsigned long long)jlsub(cd, c.delta));
+    c.delta = cd;
 }
-__global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_round) {
-    if (!lr_active(S)) return;
-    const uint32_t nc = (uint32_t)min(S.lctr[ci(LC_CHG)], (unsigned long long)S.lc_cap);
-    const uint32_t k0 = blockIdx.x * blockDim.x + threadIdx.x;
-    if (nc == 0) {                                // converged
-        if (k0 == 0) {
-            S.lctr[ci(LC_DONE)] = 1;
-            const unsigned long long nd = S.lctr[ci(LC_DIRTY)];
-            S.lctr[ci(LC_REPAIRED)] = nd;
-            S.ctr[ci(C_LREPAIRED)] = nd;
-        }
-        return;
-    }
-    if (last_round) {                             // still changing: the serial replay
-        if (k0 == 0) lfallback(S);
-        return;
-    }
-    for (uint32_t k = k0; k < nc; k += gridDim.x * blockDim.x) {
+KDEV void lr_detect(const DevState& S, uint32_t t0, uint32_t nt, uint32_t nc) {
+    for (uint32_t k = t0; k < nc; k += nt) {
         const uint32_t p = S.lchg[k];
         const uint32_t meta = S.lvw_meta[p];
         int32_t c = VT_NONE;
@@ -507,6 +487,33 @@ __global__ void __launch_bounds__(256) k_lr_detect(DevState S, uint32_t last_rou
         S.lvw_tgt[p] = c;
         if (coupling(S, p, meta, c)) list_coupling(S, p);
     }
+}
+}  // namespace
+__global__ void __launch_bounds__(1024) k_lr_rounds(DevState S) {
+    if (lskip(S) || lops(S) == 0) return;
+    const uint32_t t = threadIdx.x, nt = blockDim.x;
+    for (uint32_t r = 0; r < S.lrounds; ++r) {
+        if (lfell(S)) return;                     // (read after a barrier: the same for every thread)
+        if (t == 0) __hip_atomic_store(lc(S, LC_CHG), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        lr_link(S, t, nt);
+        __syncthreads();
+        const uint32_t nd = min(lc_get(S, LC_DIRTY), S.lr_cap);
+        for (uint32_t d = t; d < nd; d += nt) lr_run_chain(S, S.lrun[d]);
+        __syncthreads();
+        const uint32_t nc = min(lc_get(S, LC_CHG), S.lc_cap);
+        if (nc == 0) {                            // converged
+            if (t == 0) {
+                S.lctr[ci(LC_DONE)] = 1;
+                S.lctr[ci(LC_REPAIRED)] = nd;
+                S.ctr[ci(C_LREPAIRED)] = nd;
+            }
+            return;
+        }
+        lr_detect(S, t, nt, nc);
+        __syncthreads();
+    }
+    if (t == 0) lfallback(S);                     // still changing after the last round: the serial replay
 }
 
 // ---------------------------------------------------------------- 6. commit
@@ -710,12 +717,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), 8192);
     hipLaunchKernelGGL(k_lchains, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
-    // (with no coupling the first round's link finds none, runs nothing and the detect converges)
-    for (uint32_t r = 0; r < S.lrounds; ++r) {
-        hipLaunchKernelGGL(k_lr_link, dim3(64), dim3(256), 0, st, S);
-        hipLaunchKernelGGL(k_lr_run, dim3(256), dim3(256), 0, st, S);
-        hipLaunchKernelGGL(k_lr_detect, dim3(64), dim3(256), 0, st, S, (uint32_t)(r + 1 == S.lrounds));
-    }
+    hipLaunchKernelGGL(k_lr_rounds, dim3(1), dim3(1024), 0, st, S);
     hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lvw_check, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);

@@ -279,9 +279,15 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && cfg->max_symbols < (1u << 30) &&
                  nops < (1ull << 30) ? 1 : 0;
         if (S.lpar) {
-            int bits = 0;
-            while ((1ull << bits) < ((uint64_t)cfg->max_accounts << 8)) ++bits;
-            S.lpasses = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+            // sort key aid << hb | hash(sid): hb = 8 bits of sid hash, fewer when that saves a radix
+            // pass (a bucket then holds more of the account's chains; KME_LEDGER_HBITS: A/B runs)
+            int abits = 0;
+            while ((1ull << abits) < (uint64_t)cfg->max_accounts) ++abits;
+            int hb = 8;
+            if (abits + hb > 2 * RADIX_BITS && abits + 2 <= 2 * RADIX_BITS) hb = 2 * RADIX_BITS - abits;
+            if (const char* v = std::getenv("KME_LEDGER_HBITS")) hb = std::max(1, std::min(8, std::atoi(v)));
+            S.lhbits = hb;
+            S.lpasses = std::max(1, (abits + hb + RADIX_BITS - 1) / RADIX_BITS);
             S.lr_cap = 1u << 18;     // chains re-run by the repair rounds
             S.lx_cap = 1u << 19;     // couplings
             S.lc_cap = 1u << 20;     // value writes changed in one round
