@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kme.h"
 #include "kme_device.h"
@@ -46,8 +47,7 @@ namespace kme {
 
 namespace {
 
-// sort key: aid << S.lhbits | a hash of the sid in lhbits bits (the runtime picks lhbits so that the
-// key needs the fewest radix passes: 2 bits at 65,536 accounts, 8 bits below 1,024)
+// sort key: aid << S.lhbits | a hash of the sid in lhbits (8) bits
 constexpr uint32_t OP_CHECK = 0u, OP_FILL = 1u, OP_CANCEL = 2u;   // LOp::flags & 3 (bit 2: buy / bought)
 constexpr uint32_t VW_PUT = 1u, VW_DEL = 2u;
 constexpr int32_t VT_NONE = -1, VT_INSERT = -2;     // lvw_tgt: into no chain of the epoch / a winner to create
@@ -714,7 +714,13 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.passes = S.lpasses;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
-    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), 8192);
+    // grid of the per-op kernels: blocks for ~every op of a full epoch (their work per thread is a chain
+    // of dependent loads; more threads in flight hide it).  KME_LEDGER_GRID: A/B runs.
+    static const uint32_t grid_cap = [] {
+        const char* v = std::getenv("KME_LEDGER_GRID");
+        return v ? (uint32_t)std::max(64, std::atoi(v)) : 32768u;
+    }();
+    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
     hipLaunchKernelGGL(k_lchains, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lr_rounds, dim3(1), dim3(1024), 0, st, S);

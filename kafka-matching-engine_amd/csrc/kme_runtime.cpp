@@ -279,12 +279,12 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         S.lpar = (!ls || !std::atoi(ls)) && cfg->max_accounts <= (1u << 23) && cfg->max_symbols < (1u << 30) &&
                  nops < (1ull << 30) ? 1 : 0;
         if (S.lpar) {
-            // sort key aid << hb | hash(sid): hb = 8 bits of sid hash, fewer when that saves a radix
-            // pass (a bucket then holds more of the account's chains; KME_LEDGER_HBITS: A/B runs)
+            // sort key aid << hb | hash(sid), hb = 8: a bucket holds ~one chain.  (Measured and not
+            // kept: hb = 2 at 65,536 accounts, two radix passes instead of three -- the longer bucket
+            // runs cost k_lchains and k_ldetect far more than the pass saves.  KME_LEDGER_HBITS: A/B.)
             int abits = 0;
             while ((1ull << abits) < (uint64_t)cfg->max_accounts) ++abits;
             int hb = 8;
-            if (abits + hb > 2 * RADIX_BITS && abits + 2 <= 2 * RADIX_BITS) hb = 2 * RADIX_BITS - abits;
             if (const char* v = std::getenv("KME_LEDGER_HBITS")) hb = std::max(1, std::min(8, std::atoi(v)));
             S.lhbits = hb;
             S.lpasses = std::max(1, (abits + hb + RADIX_BITS - 1) / RADIX_BITS);
