@@ -228,6 +228,7 @@ struct DevState {
     KG uint32_t* lrun;                // the repair rounds' run list (chain heads)
     KG uint32_t* lchg;                // the value writes a repair round changed
     KG unsigned long long* lctr;      // LC_N x CTR_STRIDE words
+    KG unsigned long long* lposc;     // 64 x CTR_STRIDE words: positions k_linsert created (k_lbalances folds them)
 };
 
 struct EpochIO {

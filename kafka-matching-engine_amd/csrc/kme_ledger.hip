@@ -98,10 +98,13 @@ KDEV int pos_insert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64
     }
     return -1;
 }
-// the sum of v over the wavefront, added by lane 0 (every lane of the wavefront calls it)
-KDEV void wave_add(KG unsigned long long* p, uint32_t v) {
+// the sum of v over the wavefront, added by lane 0 to one of 64 counter lines (k_lbalances folds
+// them): a single counter hit once per wavefront serialises the kernel (every lane calls it)
+constexpr int LPOSC_LINES = 64;
+KDEV void wave_add_spread(const DevState& S, uint32_t v) {
     for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, (unsigned long long)v);
+    const uint32_t line = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (LPOSC_LINES - 1);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&S.lposc[(size_t)line * CTR_STRIDE], (unsigned long long)v);
 }
 KDEV int32_t bal_lookup(const DevState& S, int64_t aid) {
     uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
@@ -668,21 +671,24 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
         grew += r > 0;
     }
     if (full) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
-    wave_add(&S.ctr[ci(C_POS_USED)], grew);
+    wave_add_spread(S, grew);
 }
 __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A || lskip(S) || lfell(S)) return;
+    if (a == 0) {   // the positions k_linsert created (its spread counters), and the tables' load, as Core's inserts check it
+        unsigned long long grew = 0;
+        for (int k = 0; k < LPOSC_LINES; ++k) grew += S.lposc[(size_t)k * CTR_STRIDE];
+        const unsigned long long used = S.ctr[ci(C_POS_USED)] + grew;
+        S.ctr[ci(C_POS_USED)] = used;
+        if (used * 4 > ((unsigned long long)S.pos_mask + 1) * 3 || S.ctr[ci(C_BAL_USED)] * 2 > (unsigned long long)S.bal_mask + 1)
+            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+    }
     const int64_t d = S.ldelta[a];
     if (d == 0) return;
     const int32_t h = bal_lookup(S, a);
     if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); return; }   // (cannot happen)
     S.bal_val[h] = jladd(S.bal_val[h], d);
-    if (a == 0) {   // the tables' load (one thread), as Core's inserts check it
-        if (S.ctr[ci(C_POS_USED)] * 4 > ((unsigned long long)S.pos_mask + 1) * 3 ||
-            S.ctr[ci(C_BAL_USED)] * 2 > (unsigned long long)S.bal_mask + 1)
-            raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
-    }
 }
 
 // ---------------------------------------------------------------- launcher
@@ -691,6 +697,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     auto cdiv = [](uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); };
     const uint64_t nops = (uint64_t)n + 2ull * max_trades;    // (ops: at most one per arrival number)
     (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
+    (void)hipMemsetAsync(S.lposc, 0, sizeof(unsigned long long) * LPOSC_LINES * CTR_STRIDE, st);
     (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nops, st);
     (void)hipMemsetAsync(S.lxmark, 0, nops, st);
     (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
@@ -714,21 +721,22 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.passes = S.lpasses;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
-    // grid of the per-op kernels: blocks for ~every op of a full epoch (their work per thread is a chain
-    // of dependent loads; more threads in flight hide it).  KME_LEDGER_GRID: A/B runs.
+    // grid of k_lchains / k_linsert: more blocks (their work per thread is a chain of dependent loads:
+    // more threads in flight hide it; 8,192 -> 32,768 blocks: k_lchains 0.52 -> 0.42 ms).
+    // KME_LEDGER_GRID: A/B runs.
     static const uint32_t grid_cap = [] {
         const char* v = std::getenv("KME_LEDGER_GRID");
         return v ? (uint32_t)std::max(64, std::atoi(v)) : 32768u;
     }();
-    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
-    hipLaunchKernelGGL(k_lchains, dim3(gs), dim3(256), 0, st, S);
+    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), 8192), gl = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
+    hipLaunchKernelGGL(k_lchains, dim3(gl), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lr_rounds, dim3(1), dim3(1024), 0, st, S);
     hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lvw_check, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_linsert, dim3(gs), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_linsert, dim3(gl), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lbalances, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }
 

@@ -313,6 +313,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lrun, S.lr_cap);
             ALLOC(S.lchg, S.lc_cap);
             ALLOC(S.lctr, (size_t)LC_N * CTR_STRIDE);
+            ALLOC(S.lposc, (size_t)64 * CTR_STRIDE);
         }
     }
     if (exact_ledger) {
