@@ -95,10 +95,10 @@ def test_unsettled_couplings_take_the_serial_replay(kme_mod, oracle_mod, monkeyp
     assert any(s for _, s in stats[1:]), stats
 
 
-def test_c3_shape_couplings_settle_in_parallel(kme_mod, oracle_mod, monkeypatch):
-    """The bench's C3 universe (65,536 accounts x 65,536 symbols) in 2^18-record epochs: the position
-    values (amount, available) of small magnitude are also live (aid, sid) keys, so every epoch has
-    couplings; the rounds settle them (no serial replay) and the ledger is the oracle's."""
+def test_c3_shape_ledger_in_parallel(kme_mod, oracle_mod, monkeypatch):
+    """The bench's C3 universe (65,536 accounts x 65,536 symbols) in 2^18-record epochs: position
+    values (amount, available) of small magnitude are also live (aid, sid) keys; whatever couplings
+    arise, the parallel pass keeps every epoch (no serial replay) and the ledger is the oracle's."""
     n_sym, n_acc, E = 65_536, 65_536, 1 << 18
     body = W.uniform(3 * E, n_symbols=n_sym, n_accounts=n_acc, seed=2007)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
