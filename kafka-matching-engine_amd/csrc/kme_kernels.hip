@@ -741,6 +741,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     KG uint32_t* okeys = R.keys[dst];
     KG uint32_t* ovals = R.vals[dst];
     const bool last = pass == R.passes - 1 && R.rank;
+    const bool pay = pass == R.passes - 1 && R.pay_src;
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
         const uint32_t e = j * 256 + t;
@@ -750,6 +751,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
             okeys[pos] = key;
             ovals[pos] = val;
             if (last) R.rank[val] = (int32_t)pos;
+            if (pay) R.pay_dst[pos] = R.pay_src[val];   // a 16-B payload gathered into sorted order
         }
     }
 }

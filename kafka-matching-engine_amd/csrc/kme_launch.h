@@ -26,6 +26,8 @@ struct RadixIO {
     KG uint32_t* vals[2];
     KG uint32_t* ghist;              // RADIX_DIGITS x tiles + the scan's scratch
     KG int32_t* rank;                // the last pass: rank[value] = position (nullptr: none)
+    const KG uint4* pay_src;         // the last pass: pay_dst[position] = pay_src[value] (nullptr: none)
+    KG uint4* pay_dst;
     uint32_t none;
     uint32_t n;
     const KG unsigned long long* n_dev;

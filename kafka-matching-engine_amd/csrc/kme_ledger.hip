@@ -294,13 +294,12 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 }
 
 // ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
-// (and the ops themselves gathered into sorted order, once: every later kernel reads them there)
+// (the ops themselves were gathered into sorted order by the sort's last pass: lsrt)
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k > n || n == 0) return;      // (no ops: lseg stays zero)
     const KG uint32_t* K = skeys(S);
-    if (k < n) S.lsrt[k] = S.lrec[svals(S)[k]];
     const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
     const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
     for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
@@ -715,6 +714,8 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.vals[0] = S.lval[0]; R.vals[1] = S.lval[1];
     R.ghist = S.lghist;
     R.rank = nullptr;
+    R.pay_src = reinterpret_cast<const KG uint4*>(S.lrec);   // the ops themselves, into sorted order
+    R.pay_dst = reinterpret_cast<KG uint4*>(S.lsrt);
     R.none = 0;
     R.n = (uint32_t)nops;
     R.n_dev = S.lctr + ci(LC_OPS);
