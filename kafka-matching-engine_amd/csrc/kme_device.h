@@ -207,8 +207,7 @@ struct DevState {
     uint64_t lvk_mask;
     KG uint32_t* lcnt;                // per record: its ops, then their offset
     KG uint32_t* lscan;               // scan scratch
-    KG uint32_t* lk0;                 // per op (arrival order): sort key aid * 256 + hash8(sid)
-    KG uint32_t* lv0;                 //   and its arrival number
+    KG uint32_t* lk0;                 // per op (arrival order): sort key aid << 8 | hash8(sid)
     KG uint32_t* lkey[2];
     KG uint32_t* lval[2];
     KG uint32_t* lghist;

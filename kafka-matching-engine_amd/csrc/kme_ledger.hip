@@ -221,9 +221,8 @@ KDEV int64_t apply_op(const LOp& o, int64_t aid, PState& P, VWrite& w) {
     return d;
 }
 
-// The sorted ops: keys (aid * 256 + hash8(sid)) and values (arrival op index) of the last radix pass.
+// The sorted ops' keys (aid << 8 | hash8(sid)) after the last radix pass (the ops themselves: lsrt).
 KDEV const KG uint32_t* skeys(const DevState& S) { return S.lkey[S.lpasses & 1]; }
-KDEV const KG uint32_t* svals(const DevState& S) { return S.lval[S.lpasses & 1]; }
 KDEV uint32_t lower_bound(const KG uint32_t* k, uint32_t lo, uint32_t hi, uint32_t key) {
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -272,8 +271,7 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
         LOp op;
         op.sid = (int32_t)sid; op.es = es; op.size = size; op.price = (int16_t)price; op.flags = (uint16_t)flags;
         S.lrec[o] = op;
-        S.lk0[o] = lkey_of(S, aid, sid);
-        S.lv0[o] = o;
+        S.lk0[o] = lkey_of(S, aid, sid);   // (its value in the sort: o itself, R.val0 = nullptr)
         ++o;
     };
     if ((a == BUY || a == SELL) && out == a) {
@@ -709,7 +707,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     hipLaunchKernelGGL(k_lgen, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     RadixIO R{};
     R.key0 = reinterpret_cast<const KG int32_t*>(S.lk0);
-    R.val0 = S.lv0;
+    R.val0 = nullptr;
     R.keys[0] = S.lkey[0]; R.keys[1] = S.lkey[1];
     R.vals[0] = S.lval[0]; R.vals[1] = S.lval[1];
     R.ghist = S.lghist;

@@ -298,7 +298,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE - 1) / RADIX_TILE);
             ALLOC(S.lcnt, E);
             ALLOC(S.lscan, E / 4096 + 64);
-            ALLOC(S.lk0, nops); ALLOC(S.lv0, nops);
+            ALLOC(S.lk0, nops);
             ALLOC(S.lkey[0], nops); ALLOC(S.lkey[1], nops);
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
