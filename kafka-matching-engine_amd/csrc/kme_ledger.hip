@@ -272,6 +272,8 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
         op.sid = (int32_t)sid; op.es = es; op.size = size; op.price = (int16_t)price; op.flags = (uint16_t)flags;
         S.lrec[o] = op;
         S.lk0[o] = lkey_of(S, aid, sid);   // (its value in the sort: o itself, R.val0 = nullptr)
+        S.lvw_meta[o] = 0;                  // (per sorted position, and positions cover the same range)
+        S.lxmark[o] = 0;
         ++o;
     };
     if ((a == BUY || a == SELL) && out == a) {
@@ -695,8 +697,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     const uint64_t nops = (uint64_t)n + 2ull * max_trades;    // (ops: at most one per arrival number)
     (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
     (void)hipMemsetAsync(S.lposc, 0, sizeof(unsigned long long) * LPOSC_LINES * CTR_STRIDE, st);
-    (void)hipMemsetAsync(S.lvw_meta, 0, sizeof(uint32_t) * nops, st);
-    (void)hipMemsetAsync(S.lxmark, 0, nops, st);
+    // (lvw_meta and lxmark of the epoch's ops are cleared by k_lgen: the ops fill [0, count) exactly)
     (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
     (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
     (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
