@@ -87,7 +87,14 @@ KDEV_HOST_INLINE uint32_t tt_ordp(uint32_t ord, int32_t price, bool sneg) {
     return ord | ((uint32_t)price << TT_ORD_BITS) | (sneg ? 1u << 30 : 0u);
 }
 
-struct PosEntry { int64_t k0, k1, v0, v1; };   // Positions: UUID(aid,sid) -> UUID(amount,available)
+// Positions: UUID(aid,sid) -> UUID(amount,available), with the slot's state (0 empty, 1 live, 2
+// tombstone) in the same 64-byte line: a probe or an insert touches one line
+struct alignas(64) PosEntry {
+    int64_t k0, k1, v0, v1;
+    uint32_t state;
+    uint32_t _pad[7];
+};
+static_assert(sizeof(PosEntry) == 64, "PosEntry");
 
 // kme_ledger.hip: one position chain of an epoch (the ops on Positions key (aid, sid)), stored at the
 // sorted position of its first op (aid -1 there: that op is not a chain's first)
@@ -174,7 +181,6 @@ struct DevState {
     KG uint32_t* bal_state;
     KG int64_t* bal_key;
     KG int64_t* bal_val;
-    KG uint32_t* pos_state;
     KG PosEntry* pos;
     // per-epoch scratch
     KG uint32_t* epos;                // oid-table position of this epoch's BUY/SELL i (k_emap -> k_table)

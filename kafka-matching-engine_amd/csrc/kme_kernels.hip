@@ -1033,7 +1033,7 @@ struct Core {
         uint32_t h = (uint32_t)mix64((uint64_t)k0 * 0x9e3779b97f4a7c15ull ^ mix64((uint64_t)k1)) & S.pos_mask;
         int32_t first_free = -1;
         for (uint32_t p = 0; p <= S.pos_mask; ++p) {
-            const uint32_t st = S.pos_state[h];
+            const uint32_t st = S.pos[h].state;
             if (st == 0) { if (free_slot_out) *free_slot_out = first_free >= 0 ? first_free : (int32_t)h; return -1; }
             if (st == 1) {
                 const PosEntry& e = S.pos[h];
@@ -1058,18 +1058,18 @@ struct Core {
         if (h < 0) {
             if (fs < 0) { die(KME_E_CAPACITY, KME_D_CAP_LEDGER, idx); return; }
             h = fs;
-            if (S.pos_state[h] == 0) {
+            if (S.pos[h].state == 0) {
                 const unsigned long long used = S.ctr[ci(C_POS_USED)] + 1;
                 S.ctr[ci(C_POS_USED)] = used;
                 if (used * 4 > ((unsigned long long)S.pos_mask + 1) * 3) { die(KME_E_CAPACITY, KME_D_CAP_LEDGER, idx); return; }
             }
-            S.pos[h].k0 = k0; S.pos[h].k1 = k1; S.pos_state[h] = 1;
+            S.pos[h].k0 = k0; S.pos[h].k1 = k1; S.pos[h].state = 1;
         }
         S.pos[h].v0 = v0; S.pos[h].v1 = v1;
     }
     KDEV void pos_del(int64_t k0, int64_t k1) {
         const int32_t h = pos_find(k0, k1, nullptr);
-        if (h >= 0) S.pos_state[h] = 2;
+        if (h >= 0) S.pos[h].state = 2;
     }
 
     // createBalance, KP:131-138
@@ -1147,10 +1147,10 @@ struct Core {
         const int lane = lane_id();
         bool bad = false;
         for (uint32_t h = lane; h <= S.pos_mask; h += 64)
-            if (S.pos_state[h] == 1 && S.pos[h].k1 == sid && bal_find(S.pos[h].k0) < 0) bad = true;
+            if (S.pos[h].state == 1 && S.pos[h].k1 == sid && bal_find(S.pos[h].k0) < 0) bad = true;
         if (__ballot(bad)) { die(KME_E_DOMAIN, KME_D_NPE_BALANCE, idx); return; }
         for (uint32_t h = lane; h <= S.pos_mask; h += 64) {
-            if (S.pos_state[h] == 1 && S.pos[h].k1 == sid) {
+            if (S.pos[h].state == 1 && S.pos[h].k1 == sid) {
                 const int32_t b = bal_find(S.pos[h].k0);
                 atomicAdd((unsigned long long*)&S.bal_val[b], (unsigned long long)jlmul(S.pos[h].v0, (int64_t)size));
             }
@@ -1158,7 +1158,7 @@ struct Core {
         __threadfence();   // the atomics ran at L2: drop this CU's L1 copies before re-reading
         __builtin_amdgcn_wave_barrier();
         for (uint32_t h = lane; h <= S.pos_mask; h += 64)
-            if (S.pos_state[h] == 1 && S.pos[h].k1 == sid) S.pos_state[h] = 2;
+            if (S.pos[h].state == 1 && S.pos[h].k1 == sid) S.pos[h].state = 2;
         __threadfence();   // other lanes' tombstones become visible to every lane
         __builtin_amdgcn_wave_barrier();
     }

@@ -76,7 +76,7 @@ KDEV uint32_t pos_hash(const DevState& S, int64_t k0, int64_t k1) {
 KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
     uint32_t h = pos_hash(S, k0, k1);
     for (uint32_t p = 0; p <= S.pos_mask; ++p) {
-        const uint32_t st = S.pos_state[h];
+        const uint32_t st = S.pos[h].state;
         if (st == 0) return -1;
         if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) return (int32_t)h;
         h = (h + 1) & S.pos_mask;
@@ -89,8 +89,8 @@ KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
 KDEV int pos_insert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1) {
     uint32_t h = pos_hash(S, k0, k1);
     for (uint32_t p = 0; p <= S.pos_mask; ++p) {
-        const uint32_t st = S.pos_state[h];
-        if ((st == 0 || st == 2) && atomicCAS((unsigned int*)&S.pos_state[h], st, 1u) == st) {
+        const uint32_t st = S.pos[h].state;
+        if ((st == 0 || st == 2) && atomicCAS((unsigned int*)&S.pos[h].state, st, 1u) == st) {
             S.pos[h].k0 = k0; S.pos[h].k1 = k1; S.pos[h].v0 = v0; S.pos[h].v1 = v1;
             return st == 0 ? 1 : 0;
         }
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         if (v < 0 || S.lvk[v].y != (unsigned long long)S.lsrt[p].es + 1) continue;
         const int32_t h = pos_lookup(S, w.x, w.y);
         if ((meta & 3u) == VW_DEL) {
-            if (h >= 0) S.pos_state[h] = 2u;
+            if (h >= 0) S.pos[h].state = 2u;
         } else if (h >= 0) {
             S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
         } else {
@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         const bool fp = chain_final(S, c, fa, fv);
         if (fp && fa == c.ia && fv == c.iv) continue;
         if (fp) { S.pos[c.islot].v0 = fa; S.pos[c.islot].v1 = fv; }
-        else S.pos_state[c.islot] = 2u;
+        else S.pos[c.islot].state = 2u;
     }
 }
 // The keys to create: chains absent at the epoch's start that end present, and value-write winners

@@ -324,7 +324,6 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.bal_state, lc);
         ALLOC(S.bal_key, lc);
         ALLOC(S.bal_val, lc);
-        ALLOC(S.pos_state, lc);
         ALLOC(S.pos, lc);
     }
     ALLOC(S.epos, E);
@@ -382,7 +381,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (exact_ledger) {
         const size_t lc = (size_t)S.bal_mask + 1;
         HIP_TRY(hipMemsetAsync(S.bal_state, 0, lc * sizeof(uint32_t), st));
-        HIP_TRY(hipMemsetAsync(S.pos_state, 0, lc * sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(S.pos, 0, lc * sizeof(PosEntry), st));
     }
     launch_init_state(S, st);
     HIP_TRY(hipGetLastError());
@@ -983,7 +982,6 @@ std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
         b.push_back({S.bal_state, lc * sizeof(uint32_t)});
         b.push_back({S.bal_key, lc * sizeof(int64_t)});
         b.push_back({S.bal_val, lc * sizeof(int64_t)});
-        b.push_back({S.pos_state, lc * sizeof(uint32_t)});
         b.push_back({S.pos, lc * sizeof(PosEntry)});
     }
     return b;
@@ -1396,19 +1394,18 @@ kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     const size_t lc = (size_t)e->S.bal_mask + 1;
-    std::vector<uint32_t> bst(lc), pst(lc);
+    std::vector<uint32_t> bst(lc);
     std::vector<int64_t> bk(lc), bv(lc);
     std::vector<PosEntry> pos(lc);
     HIP_TRY(hipMemcpy(bst.data(), e->S.bal_state, lc * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(bk.data(), e->S.bal_key, lc * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(bv.data(), e->S.bal_val, lc * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(pst.data(), e->S.pos_state, lc * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(pos.data(), e->S.pos, lc * sizeof(PosEntry), hipMemcpyDeviceToHost));
     std::vector<std::pair<int64_t, int64_t>> bal;
     for (size_t h = 0; h < lc; ++h) if (bst[h] == 1) bal.push_back({bk[h], bv[h]});
     std::sort(bal.begin(), bal.end());
     std::vector<PosEntry> ps;
-    for (size_t h = 0; h < lc; ++h) if (pst[h] == 1) ps.push_back(pos[h]);
+    for (size_t h = 0; h < lc; ++h) if (pos[h].state == 1) ps.push_back(pos[h]);
     std::sort(ps.begin(), ps.end(), [](const PosEntry& a, const PosEntry& b) { return a.k0 != b.k0 ? a.k0 < b.k0 : a.k1 < b.k1; });
     std::string out;
     char line[256];
