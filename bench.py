@@ -240,7 +240,7 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
     a0, n_rec = first * E, n_epochs * E
     cols = {c: np.ascontiguousarray(getattr(stream, c)[a0:a0 + n_rec]) for c in ("action", "oid", "aid", "sid", "price", "size")}
     ko = kme.kme_orders(*[C.c_void_p(cols[c].ctypes.data) for c in ("action", "oid", "aid", "sid", "price", "size")])
-    stats = (C.c_double * 7)()
+    stats = (C.c_double * 8)()
     rc = lib.kme_host_path_run(eng.handle, C.byref(ko), E, n_epochs, max_trades, stats)
     if rc:
         raise kme.KmeError(rc, "kme_host_path_run")
@@ -251,7 +251,7 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
             "rows": int(stats[1]), "trades": int(stats[5]), "rows_per_s": stats[1] / dt, "h2d_bytes_per_epoch": h2d_b, "d2h_bytes_per_epoch": int(d2h_b),
             "pcie_GBps_each_way": round(max(h2d_b, d2h_b) * n_epochs / dt / 1e9, 2),
             "host_s": {"fill": round(stats[2], 4), "wait": round(stats[3], 4), "rows": round(stats[4], 4),
-                       "total": round(dt, 4)},
+                       "rows_expand": round(stats[7], 4), "rows_read": round(stats[4] - stats[7], 4), "total": round(dt, 4)},
             "path": "integration/host_harness.c: GpuMatchingEngine.java's schedule over kme_jni.c's C ABI calls "
                     "(registered host columns -> kme_submit_epoch_host -> kme_wait + kme_expand_rows -> rows read), "
                     "two epochs in flight; PCIe- and host-inclusive, not the headline value"}

@@ -39,7 +39,7 @@ static void* page_alloc(size_t bytes) {
 }
 
 /* Stats out: [0] seconds, [1] rows forwarded, [2] fill seconds, [3] complete (wait) seconds,
- * [4] expand + row-read seconds, [5] trades, [6] checksum of the rows read. */
+ * [4] expand + row-read seconds, [5] trades, [6] checksum of the rows read, [7] expand seconds. */
 int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, uint32_t n_epochs, uint32_t max_trades,
                       double* stats) {
     if (!e || !stream || !epoch || !stats) return KME_E_INVALID;
@@ -70,7 +70,7 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
             }
         }
     }
-    double t_fill = 0, t_wait = 0, t_rows = 0, trades = 0;
+    double t_fill = 0, t_wait = 0, t_rows = 0, t_expand = 0, trades = 0;
     uint64_t rows_total = 0, check = 0;
     int inflight = 0, oldest = 0;
     const double t0 = now_s();
@@ -88,6 +88,7 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
             size_t nr = 0;
             rc = kme_expand_rows_mt(&in, h->n, &h->res, h->rows, h->rows_cap, &nr, 0);
             if (rc != KME_OK) break;
+            t_expand += now_s() - b;
             for (size_t q = 0; q < nr; ++q)   /* the JVM reads every row (one Order each) */
                 check += (uint64_t)h->rows[q].oid + (uint64_t)h->rows[q].size + h->rows[q].kind;
             t_rows += now_s() - b;
@@ -134,5 +135,6 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
     stats[4] = t_rows;
     stats[5] = trades;
     stats[6] = (double)(check & ((1ull << 52) - 1));
+    stats[7] = t_expand;
     return rc;
 }
