@@ -128,3 +128,14 @@ def test_launcher_world_must_match_gpus(monkeypatch):
     with pytest.raises(SystemExit) as ei:
         bench.main()
     assert "--gpus 2" in str(ei.value.code)
+
+
+def test_c4_shard_workload_is_its_partition():
+    """bench.py --workload c4 --shard R/N: rank R's records of the N-GPU C4 run (its murmur2 share of the
+    65,536 symbols, Zipf popularity of the whole universe), funded for N credit shards."""
+    world = 8
+    for r in (0, 5):
+        setup, stream, sids, nacc, shards, _ = bench.make_workload("c4", 20_000, r, world)
+        assert shards == world and len(sids) == len(W.shard_symbols(65536, world, r))
+        bs = np.isin(stream.action, (W.BUY, W.SELL))
+        assert np.isin(stream.sid[bs], sids).all()

@@ -72,3 +72,27 @@ def test_credit_split_probe_counts_the_first_failing_epoch():
     # the max risk of checkBalance (KP:172-176): BUY size * price, SELL size * (100 - price)
     r = probe.max_risk(np.array([2, 3, 4]), np.array([30, 30, 0]), np.array([10, 10, 0]))
     assert r.tolist() == [300, 700, 0]
+
+
+def test_bench_reports_traffic_only_for_the_profiled_build(tmp_path):
+    """roofline.traffic comes from the committed PMC summary only when that summary profiled the very
+    library the bench loaded (its kme_build_id()); otherwise the line says why it has none."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"build_id": "abc", "hbm_bytes_per_launch": 123.0, "per_kernel_derived": {"k": {}},
+                             "source": "passes of build abc"}))
+    traffic, derived, src = bench.pmc_for_build(str(p), "abc")
+    assert traffic == 123.0 and derived == {"k": {}} and "abc" in src
+    traffic, derived, src = bench.pmc_for_build(str(p), "def")
+    assert traffic is None and derived is None and "abc" in src and "def" in src
+    assert bench.pmc_for_build(str(tmp_path / "missing.json"), "abc")[0] is None
+
+
+def test_pmc_summary_records_the_profiled_build(tmp_path):
+    """tools/pmc_summary.py takes the build id from the bench lines its passes printed."""
+    d = tmp_path / "pmc"
+    d.mkdir()
+    (d / "p1.log").write_text("some rocprof noise\n" + json.dumps({"metric": "m", "build_id": "0123456789abcdef"}) + "\n")
+    assert pmc_summary.build_id_of(str(d)) == "0123456789abcdef"
