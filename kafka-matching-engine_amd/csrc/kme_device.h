@@ -15,6 +15,7 @@
 //   ledger               FUNDED: per-account existence + reservation bound; EXACT: Balances and
 //                        Positions as device hash tables (KP:30-37).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 // Pointer members of the device structs live in the global address space (AS1) for the device
@@ -98,7 +99,7 @@ static_assert(sizeof(PosEntry) == 64, "PosEntry");
 
 // kme_ledger.hip: one position chain of an epoch (the ops on Positions key (aid, sid)), stored at the
 // sorted position of its first op (aid -1 there: that op is not a chain's first)
-struct LChain {
+struct alignas(16) LChain {
     int64_t sid;
     int64_t ia, iv;                // the entry at the epoch's start (ipres)
     int64_t fa, fv;                // after the chain's last effect (fpres)
@@ -122,7 +123,7 @@ struct LOp {
     int16_t price;                 // the effect's price term
     uint16_t flags;                // kind (check / fill / cancel) | buy << 2
 };
-static_assert(sizeof(LOp) == 16, "LOp");
+static_assert(sizeof(LOp) == 16 && offsetof(LOp, price) == 12 && offsetof(LOp, flags) == 14, "LOp (k_lgen packs it)");
 // the ledger pass's counters (DevState::lctr, one line each)
 enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
 

@@ -268,9 +268,9 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
     uint32_t o = S.lcnt[i];
     const uint32_t t0 = io.trade_off[i];
     auto put = [&](int64_t aid, int64_t sid, uint32_t es, int32_t size, int32_t price, uint32_t flags) {
-        LOp op;
-        op.sid = (int32_t)sid; op.es = es; op.size = size; op.price = (int16_t)price; op.flags = (uint16_t)flags;
-        S.lrec[o] = op;
+        // one 16-B store: sid, arrival number, size, price term | flags << 16 (LOp's layout)
+        reinterpret_cast<KG uint4*>(S.lrec)[o] =
+            make_uint4((uint32_t)(int32_t)sid, es, (uint32_t)size, (uint32_t)(uint16_t)(int16_t)price | flags << 16);
         S.lk0[o] = lkey_of(S, aid, sid);   // (its value in the sort: o itself, R.val0 = nullptr)
         S.lvw_meta[o] = 0;                  // (per sorted position, and positions cover the same range)
         S.lxmark[o] = 0;
@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
                 if (S.lsrt[p - 1].sid == sid) { head = false; break; }
             if (head) {
-                KG LChain& c = S.lchain[j];
+                LChain c;                        // built in registers, stored as five 16-B writes
                 const int32_t slot = pos_lookup(S, aid, sid);
                 PState P;
                 P.present = slot >= 0;
@@ -351,6 +351,11 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
                 }
                 c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
                 c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
+                c._p[0] = c._p[1] = 0;
+                const uint4* src = reinterpret_cast<const uint4*>(&c);
+                KG uint4* dst = reinterpret_cast<KG uint4*>(&S.lchain[j]);
+#pragma unroll
+                for (int q = 0; q < (int)(sizeof(LChain) / 16); ++q) dst[q] = src[q];
             }
         }
         if (j < no) S.lhead[j] = head ? 1 : 0;   // (a list would serialise on one counter)
