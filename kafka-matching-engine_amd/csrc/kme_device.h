@@ -204,6 +204,9 @@ struct DevState {
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;
     KG uint32_t* seg;
+    KG uint32_t* gflag;               // per group: 1 = k_match takes it this epoch (then its scanned offset)
+    KG uint32_t* glist;               // those groups, in id order (k_match's dense grid); gcount[0] = how many
+    KG uint32_t* gcount;
     KG TradeTmp* ttmp;                // TSHARDS regions of tshard_cap, then the overflow region
     KG unsigned long long* tsh;       // TSHARDS x CTR_STRIDE words (TShardWord in each line)
     KG unsigned long long* ctr;       // C_NCTR x CTR_STRIDE words

@@ -2784,10 +2784,11 @@ struct GroupWave {
 // TWO: two wavefronts per group (TwoLds): wave 0 below, wave 1 GroupWave::run_levels.
 template <bool TWO>
 __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
-                                                                      int buf, int all) {
+                                                                      int buf, int all, int dense) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
-    const int32_t g = blockIdx.x;
+    // dense: block k takes the k-th listed group (the busy ones first in the grid, the rest exit)
+    const int32_t g = dense ? (blockIdx.x < S.gcount[0] ? (int32_t)S.glist[blockIdx.x] : S.G) : (int32_t)blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e || (!all && e - b <= (uint32_t)S.light_max)) return;   // empty, or a light group (k_match_lanes)
@@ -3930,9 +3931,31 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src);
     return src;
 }
-void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two) {
-    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all);
-    else hipLaunchKernelGGL(k_match<false>, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all);
+// the groups k_match takes this epoch (non-empty; busy ones unless `all`), listed in id order
+__global__ void __launch_bounds__(256) k_glist_flags(DevState S, int all) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint32_t)S.G) return;
+    const uint32_t b = S.seg[g], e = S.seg[g + 1];
+    S.gflag[g] = (e > b && (all || e - b > (uint32_t)S.light_max)) ? 1u : 0u;
+}
+__global__ void __launch_bounds__(256) k_glist_scatter(DevState S, const uint32_t* __restrict__ pos) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint32_t)S.G) return;
+    const uint32_t b = S.seg[g], e = S.seg[g + 1];
+    if (e > b && pos[g + 1] != pos[g]) S.glist[pos[g]] = g;   // (pos: the exclusive scan of the flags, in place)
+}
+void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two,
+                  int dense) {
+    if (dense) {
+        const uint32_t G = (uint32_t)S.G;
+        hipLaunchKernelGGL(k_glist_flags, dim3(cdiv(G, 256)), dim3(256), 0, st, S, all);
+        // exclusive scan of G + 1 flags (the last one 0: pos[G] = the count), in place
+        (void)hipMemsetAsync(S.gflag + G, 0, sizeof(uint32_t), st);
+        launch_excl_scan(S.gflag, S.gflag, G + 1, S.gcount + 64, S.gcount, st);
+        hipLaunchKernelGGL(k_glist_scatter, dim3(cdiv(G, 256)), dim3(256), 0, st, S, (const uint32_t*)S.gflag);
+    }
+    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
+    else hipLaunchKernelGGL(k_match<false>, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

@@ -49,6 +49,7 @@ struct kme_engine {
     // 0: never) and fewer than 1 in 8 of its records were cancels that removed an order: the serial
     // path a cancel-heavy stream takes often makes wave 0 wait
     uint64_t two_max = 4096;
+    bool dense_grid = true;              // k_match's busy groups first in the grid (KME_DENSE_GRID=0: off, A/B)
     bool last_cancel_heavy = false;
     uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
@@ -339,6 +340,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (const char* v = std::getenv("KME_FAST")) S.fast = std::atoi(v) != 0;   // A/B diagnostics
     if (const char* v = std::getenv("KME_TWO_DRAIN")) if (S.fast && std::atoi(v)) S.fast |= 2;   // diagnostics
     if (const char* v = std::getenv("KME_TWO_MAX")) e->two_max = (uint64_t)std::max(0, std::atoi(v));   // A/B diagnostics
+    if (const char* v = std::getenv("KME_DENSE_GRID")) e->dense_grid = std::atoi(v) != 0;
     if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
@@ -349,6 +351,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     const uint64_t ntiles = (E + RADIX_TILE - 1) / RADIX_TILE;
     ALLOC(S.ghist, (size_t)(1 << RADIX_BITS) * ntiles + 2 * (E / 2048 + 16) + 4096);
     ALLOC(S.seg, (size_t)G + 2);
+    ALLOC(S.gflag, (size_t)G + 1); ALLOC(S.glist, (size_t)G + 1); ALLOC(S.gcount, 64 + (size_t)G / 4096 + 64);
     ALLOC(S.ctr, (size_t)C_NCTR * CTR_STRIDE);
     ALLOC(S.dbg, (size_t)G * KME_DBG_WORDS);
     HIP_TRY(hipMemsetAsync(S.dbg, 0, (size_t)G * KME_DBG_WORDS * sizeof(unsigned long long), e->stream));
@@ -501,7 +504,10 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         // two wavefronts per busy group when few groups were busy (a group's record chain, not the
         // CU's issue rate, is then the bound) and the stream is not cancel-heavy
         const bool two = S.fast && e->last_busy > 0 && e->last_busy <= e->two_max && !e->last_cancel_heavy;
-        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0);
+        // busy groups sparse in the id space (a symbol shard of a larger universe: 8,277 of 65,537
+        // ids at the N = 8 shard of C3): k_match's first blocks take them, from a compact list
+        const bool dense = e->dense_grid && e->last_busy > 0 && (uint64_t)e->last_busy * 4 < (uint64_t)S.G;
+        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);
