@@ -2822,11 +2822,8 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
                                                                       int buf, int all, int dense) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
-    // dense (one wavefront per group only): the listed groups, block k taking entries k, k + grid, ...
-    // -- the grid is sized for them, not for every group id (empty blocks cost dispatch time)
-    for (uint32_t bid = blockIdx.x; ; bid += gridDim.x) {
-    if (!dense && bid != blockIdx.x) return;
-    const int32_t g = dense ? (bid < S.gcount[0] ? (int32_t)S.glist[bid] : S.G) : (int32_t)bid;
+    // dense: block k takes the k-th listed group (the busy ones first in the grid, the rest exit)
+    const int32_t g = dense ? (blockIdx.x < S.gcount[0] ? (int32_t)S.glist[blockIdx.x] : S.G) : (int32_t)blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e || (!all && e - b <= (uint32_t)S.light_max)) return;   // empty, or a light group (k_match_lanes)
@@ -3042,7 +3039,6 @@ __global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const D
     if (lane == 0)
         for (int q = 0; q < ST_N; ++q) S.dbg[(size_t)g * KME_DBG_WORDS + q] += w.acc[q];
 #endif
-    }   // (next listed group)
 }
 
 // ------------------------------------------------------------------ (2') FUNDED, light groups
@@ -3991,7 +3987,6 @@ void launch_assign_levels(const DevState& S, const EpochIO& io, hipStream_t st) 
 }
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two,
                   int dense) {
-    if (two) dense = 0;   // (the two-wavefront blocks take one group each)
     if (dense) {
         const uint32_t G = (uint32_t)S.G;
         hipLaunchKernelGGL(k_glist_flags, dim3(cdiv(G, 256)), dim3(256), 0, st, S, all);
@@ -4000,9 +3995,8 @@ void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_de
         launch_excl_scan(S.gflag, S.gflag, G + 1, S.gcount + 64, S.gcount, st);
         hipLaunchKernelGGL(k_glist_scatter, dim3(cdiv(G, 256)), dim3(256), 0, st, S, (const uint32_t*)S.gflag);
     }
-    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, 0);
-    else hipLaunchKernelGGL(k_match<false>, dim3(dense ? std::min<uint32_t>((uint32_t)S.G, (uint32_t)dense) : (uint32_t)S.G),
-                            dim3(64), 0, st, S_dev, io_dev, buf, all, dense ? 1 : 0);
+    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
+    else hipLaunchKernelGGL(k_match<false>, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

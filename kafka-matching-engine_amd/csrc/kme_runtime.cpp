@@ -508,10 +508,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         // busy groups sparse in the id space (a symbol shard of a larger universe: 8,277 of 65,537
         // ids at the N = 8 shard of C3): k_match's first blocks take them, from a compact list
         const bool dense = e->dense_grid && e->last_busy > 0 && (uint64_t)e->last_busy * 4 < (uint64_t)S.G;
-        // (dense: the grid = last epoch's busy groups + a margin; blocks loop over the list, so a
-        // larger list this epoch is still covered)
-        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0,
-                     dense ? (int)std::min<uint64_t>((uint64_t)e->last_busy + (e->last_busy >> 3) + 256, (uint64_t)S.G) : 0);
+        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);
