@@ -64,13 +64,9 @@ struct alignas(64) GroupState {
     uint64_t bm0_lsb, bm0_msb;     // book +g  (KP:391-404 layout: lsb = prices 0..62, msb = 63..126)
     uint64_t bm1_lsb, bm1_msb;     // book -g
     int32_t exists, free_head, chunk_next, chunk_end;
-    int32_t lblk1;                 // 1 + its block of levels in DevState::lev (0: none yet); blocks go
-                                   // to symbols in the order of their first ADD_SYMBOL (k_assign_levels)
-    int32_t _pad[3];
+    int32_t _pad[4];
 };
 static_assert(sizeof(GroupState) == 64, "GroupState");
-// a group's block of 2 x NLEV levels; groups that never had an ADD_SYMBOL share the spare block G
-KDEV_HOST_INLINE int32_t level_block(const GroupState& gs, int32_t G) { return gs.lblk1 > 0 ? gs.lblk1 - 1 : G; }
 
 struct TradeRec {                  // == kme_trade
     int64_t moid, maid, msid;
@@ -150,9 +146,7 @@ enum Ctr : int {
                        // its quantity -- stay off)
     C_LREPAIRED,       // exact ledger: position chains the parallel pass replayed for value-key couplings
     C_LSERIAL,         // exact ledger: nonzero = the serial replay applied this epoch's ledger
-    C_ADDSYM,          // ADD_SYMBOL records in the epoch (k_assign_levels runs when nonzero)
-    C_LBLK,            // persistent: level blocks handed out
-    C_NCTR = 22
+    C_NCTR = 20
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
 constexpr int ci(int k) { return k * CTR_STRIDE; }

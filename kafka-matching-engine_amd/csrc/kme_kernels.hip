@@ -282,11 +282,10 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     __shared__ uint32_t red[4];
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
     if (t0 == 0) *io_dev = io;   // the group / serial kernels read the epoch descriptor from HBM
-    uint32_t n_orders = 0, n_acct = 0, n_ins = 0, n_add = 0;
+    uint32_t n_orders = 0, n_acct = 0, n_ins = 0;
     for (uint32_t i = t0; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
         n_orders += (a == BUY || a == SELL || a == CANCEL) ? 1u : 0u;
-        n_add += a == ADD_SYMBOL ? 1u : 0u;
         if ((a == BUY || a == SELL) && io.size[i] == 0 && !S.ctr[ci(C_SIZE0)]) atomicOr(&S.ctr[ci(C_SIZE0)], 1ull);
         if (a == BUY || a == SELL) {
             // the order's oid-table entry (pending until k_table); on the way, the duplicate-oid
@@ -355,9 +354,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     const uint32_t no = block_sum_256(n_orders, red);
     const uint32_t na = block_sum_256(n_acct, red);
     const uint32_t ni = block_sum_256(n_ins, red);
-    const uint32_t nadd = block_sum_256(n_add, red);
     if (threadIdx.x == 0) {
-        if (nadd) atomicAdd(&S.ctr[ci(C_ADDSYM)], (unsigned long long)nadd);
         if (no) atomicAdd(&S.ctr[ci(C_ORDERS)], (unsigned long long)no);
         if (na) atomicAdd(&S.ctr[ci(C_ACCT_OPS)], (unsigned long long)na);
         if (ni) atomicAdd(&S.ctr[ci(C_OTAB_USED)], (unsigned long long)ni);
@@ -624,38 +621,6 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
         p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), (int32_t)tgt, vlev);
     }
-}
-
-// Level blocks: a symbol group's 2 x NLEV levels are the block its first ADD_SYMBOL took, blocks in
-// arrival order of those ADD_SYMBOLs -- so a symbol shard of a larger universe (sparse ids) keeps its
-// levels as dense as a universe of its own (k_match's working set spans fewer pages).  One
-// wavefront, records in arrival order, only in epochs with ADD_SYMBOL records (k_emap counts them);
-// after k_route (route_grp), before any kernel that touches levels.
-__global__ void __launch_bounds__(64) k_assign_levels(DevState S, EpochIO io) {
-    if (S.ctr[ci(C_ADDSYM)] == 0) return;
-    const int lane = lane_id();
-    uint32_t next = (uint32_t)S.ctr[ci(C_LBLK)];
-    for (uint32_t base = 0; base < io.n; base += 64) {
-        const uint32_t i = base + lane;
-        int32_t g = -1;
-        if (i < io.n && io.action[i] == ADD_SYMBOL) {
-            g = S.route_grp[i];
-            if (g >= 0 && S.grp[g].lblk1 != 0) g = -1;
-        }
-        if (__ballot(g >= 0) == 0) continue;
-        // the first lane of the step with its group takes the block
-        bool first = g >= 0;
-        for (int k = 0; k < 64; ++k) {
-            const int32_t gk = __shfl(g, k, 64);
-            if (k < lane && gk == g) first = false;
-        }
-        const unsigned long long m = __ballot(first);
-        if (first) S.grp[g].lblk1 = (int32_t)(next + (uint32_t)__popcll(m & ((1ull << lane) - 1))) + 1;
-        next += (uint32_t)__popcll(m);
-        __builtin_amdgcn_s_waitcnt(0);             // (this step's stores before the next step reads lblk1)
-        __threadfence_block();
-    }
-    if (lane == 0) S.ctr[ci(C_LBLK)] = next;
 }
 
 // ------------------------------------------------------------------ (1) stable radix partition
@@ -983,7 +948,7 @@ struct Core {
         exists = G.exists;
         b0l = G.bm0_lsb; b0m = G.bm0_msb; b1l = G.bm1_lsb; b1m = G.bm1_msb;
         free_head = G.free_head; chunk_next = G.chunk_next; chunk_end = G.chunk_end;
-        glev = S.lev + (size_t)level_block(G, S.G) * 2 * NLEV;
+        glev = S.lev + (size_t)gg * 2 * NLEV;
     }
     KDEV void store_group() {
         if (g < 0) return;
@@ -1624,7 +1589,7 @@ struct GroupWave {
     // more spill.  cold() hands out the state through an opaque constant-space pointer, so each
     // use is a scalar load (scalar cache) at the point of use, never hoisted.
     KDEV const KC DevState& cold() const { return opaque_const(Sp); }
-    KDEV KG Level* lev() const { return cold().lev + (size_t)level_block(cold().grp[g], cold().G) * 2 * NLEV; }
+    KDEV KG Level* lev() const { return cold().lev + (size_t)g * 2 * NLEV; }
     KDEV KG GroupState* gst() const { return cold().grp + g; }
     KDEV KG unsigned long long* ctr() const { return cold().ctr; }
     KDEV KG unsigned long long* tsh() const { return cold().tsh + (size_t)(g & (TSHARDS - 1)) * CTR_STRIDE; }
@@ -3084,7 +3049,6 @@ struct GroupLane {
     int32_t g;
     uint64_t b0l, b0m, b1l, b1m;  // level bitmaps of book +g / book -g
     int32_t exists, free_head, chunk_next, chunk_end, fsp;
-    int32_t lblk;                 // the group's block of levels (load_group)
     uint32_t cur;
     bool dead;
     size_t tpos, tlim;            // this lane's reserved trade scratch [tpos, tlim) (LANE_TCH at a time)
@@ -3097,7 +3061,6 @@ struct GroupLane {
           tbase((blockIdx.x & (TSHARDS - 1)) * s.tshard_cap), lane(lane_id()), g(gg) {
         b0l = b0m = b1l = b1m = 0;
         exists = 0; free_head = -1; chunk_next = chunk_end = 0; fsp = 0;
-        lblk = s.G;
         cur = 0; dead = false;
         tpos = tlim = 0;
         tspare = 0; has_spare = false;
@@ -3106,15 +3069,14 @@ struct GroupLane {
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
     KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
     KDEV void set_bm(int side, uint64_t l, uint64_t m) { if (side) { b1l = l; b1m = m; } else { b0l = l; b0m = m; } }
-    KDEV KG Level* level(int side, int p) const { return &S.lev[((size_t)lblk * 2 + side) * NLEV + p]; }
+    KDEV KG Level* level(int side, int p) const { return &S.lev[((size_t)g * 2 + side) * NLEV + p]; }
 
     KDEV void load_group() {
         const KG int4* gs = reinterpret_cast<const KG int4*>(&S.grp[g]);
-        const int4 a = gs[0], b = gs[1], c = gs[2], d = gs[3];
+        const int4 a = gs[0], b = gs[1], c = gs[2];
         b0l = (uint64_t)mk64(a.x, a.y); b0m = (uint64_t)mk64(a.z, a.w);
         b1l = (uint64_t)mk64(b.x, b.y); b1m = (uint64_t)mk64(b.z, b.w);
         exists = c.x; free_head = c.y; chunk_next = c.z; chunk_end = c.w;
-        lblk = d.x > 0 ? d.x - 1 : S.G;                     // (level_block: GroupState::lblk1)
         if (free_head >= 0) load_block();                   // once per epoch, before the first record
     }
     KDEV void store_group() {
@@ -3831,7 +3793,7 @@ KDEV kme_tob tob_of(const DevState& S, int32_t g) {
     const GroupState gs = S.grp[g];
     kme_tob r{-1, -1, 0, 0};
     if (gs.exists) {
-        const Level* L = S.lev + (size_t)level_block(gs, S.G) * 2 * NLEV;
+        const Level* L = S.lev + (size_t)g * 2 * NLEV;
         // bids: highest occupied level of book +g; asks: lowest of book -g (sid 0: one book)
         const uint64_t bl = gs.bm0_lsb, bh = gs.bm0_msb;
         const uint64_t al = g == 0 ? gs.bm0_lsb : gs.bm1_lsb, ah = g == 0 ? gs.bm0_msb : gs.bm1_msb;
@@ -3881,7 +3843,7 @@ __global__ void k_epoch_reset(DevState S) {
     const int k = threadIdx.x;
     if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
     else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY || k == C_LIGHT ||
-             k == C_LREPAIRED || k == C_LSERIAL || k == C_ADDSYM)
+             k == C_LREPAIRED || k == C_LSERIAL)
         S.ctr[ci(k)] = 0ull;
 }
 
@@ -3981,9 +3943,6 @@ __global__ void __launch_bounds__(256) k_glist_scatter(DevState S, const uint32_
     if (g >= (uint32_t)S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (e > b && pos[g + 1] != pos[g]) S.glist[pos[g]] = g;   // (pos: the exclusive scan of the flags, in place)
-}
-void launch_assign_levels(const DevState& S, const EpochIO& io, hipStream_t st) {
-    if (io.n > 0) hipLaunchKernelGGL(k_assign_levels, dim3(1), dim3(64), 0, st, S, io);
 }
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two,
                   int dense) {

@@ -46,7 +46,6 @@ void launch_acct_refresh(const DevState& S, const EpochIO& io, hipStream_t st); 
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st);
-void launch_assign_levels(const DevState& S, const EpochIO& io, hipStream_t st);  // level blocks of new symbols
 // returns the buffer index (0/1) holding the sorted input permutation
 int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st);
 // two: two wavefronts per group (the pass one segment ahead of the level step; few busy groups)

@@ -253,7 +253,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.tshard_cap = (uint32_t)tshard_cap;
 
     ALLOC(S.grp, G);
-    ALLOC(S.lev, ((size_t)G + 1) * 2 * NLEV);   // (block G: the spare of groups that never had an ADD_SYMBOL)
+    ALLOC(S.lev, (size_t)G * 2 * NLEV);
     ALLOC(S.pool, P);
     ALLOC(S.otab, e->otab_cap);
     const bool exact_ledger = !funded || (cfg->flags & KME_FLAG_EXACT_LEDGER);
@@ -479,7 +479,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     }
     phase_begin(e, PH_ROUTE);
     launch_route(S, io, funded, st);
-    launch_assign_levels(S, io, st);
     phase_end(e, PH_ROUTE);
     if (funded) {
         phase_begin(e, PH_PART);
@@ -960,9 +959,8 @@ const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
 namespace {
-// (formats 1 / 2 of earlier builds held no level blocks and are refused)
-constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '3'};    // no application record
-constexpr char kCkptMagic2[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '4'};   // with an application record
+constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '1'};    // format 1: no application record
+constexpr char kCkptMagic2[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '2'};
 struct CkptHeader {
     char magic[8];
     kme_config cfg;
@@ -1110,12 +1108,6 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     ctr[ci(C_OTAB_USED)] = h.otab_used;
     ctr[ci(C_BAL_USED)] = h.bal_used;
     ctr[ci(C_POS_USED)] = h.pos_used;
-    {   // level blocks handed out: the highest a restored group holds
-        const GroupState* gs = reinterpret_cast<const GroupState*>(host[0].data());
-        int64_t used = 0;
-        for (size_t g = 0; g < (size_t)e->cfg.max_symbols; ++g) used = std::max<int64_t>(used, gs[g].lblk1);
-        ctr[ci(C_LBLK)] = (unsigned long long)used;
-    }
     {   // a restored book may hold size-0 makers: then the fast segments stay off (C_SIZE0)
         const Node* nodes = reinterpret_cast<const Node*>(host[2].data());
         ctr[ci(C_SIZE0)] = 0;
@@ -1320,7 +1312,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     const uint32_t G = e->cfg.max_symbols;
     std::vector<GroupState> grp(G);
-    std::vector<Level> lev(((size_t)G + 1) * 2 * NLEV);
+    std::vector<Level> lev((size_t)G * 2 * NLEV);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
     const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
@@ -1345,7 +1337,7 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
             for (int p = 0; p <= 126; ++p) {
                 const bool set = p < 63 ? ((l >> p) & 1) : ((m >> (p - 63)) & 1);
                 if (!set) continue;
-                const Level& L = lev[((size_t)level_block(gs, (int32_t)G) * 2 + side) * NLEV + p];
+                const Level& L = lev[((size_t)g * 2 + side) * NLEV + p];
                 if (L.head < 0 || (uint64_t)L.head >= nslots || L.tail < 0 || (uint64_t)L.tail >= nslots) {
                     problems.push_back("X level head/tail out of range");
                     continue;
