@@ -223,6 +223,35 @@ def reduce_stats(dist, torch, elapsed: float, n_orders: int, n_trades: int, ok: 
     return float(t.item()), float(sums[0].item()), float(sums[1].item()), bool(flag.item())
 
 
+def measure_router(stream, E, n_epochs=4, parts=8):
+    """The partition router that splits one MatchIn stream over N GPUs (kme_router.cpp, the front of
+    kme_multi), timed by the committed C harness (integration/host_harness.c kme_router_rate_run):
+    epochs of this stream into 8 partitions, alternately route and split, best epoch of each.
+    Host-only work on this box's CPU threads (KME_ROUTER_THREADS, default min(16, cores))."""
+    import ctypes as C
+
+    import kme
+
+    lib = C.CDLL(os.path.join(ROOT, "integration", "libkme_host_harness.so"))
+    lib.kme_router_rate_run.argtypes = [C.POINTER(kme.kme_orders), C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.POINTER(C.c_double)]
+    lib.kme_router_rate_run.restype = C.c_int
+    n_epochs = min(n_epochs, len(stream) // E)
+    if n_epochs < 2:
+        return None
+    n_rec = n_epochs * E
+    cols = {c: np.ascontiguousarray(getattr(stream, c)[:n_rec]) for c in ("action", "oid", "aid", "sid", "price", "size")}
+    ko = kme.kme_orders(*[C.c_void_p(cols[c].ctypes.data) for c in ("action", "oid", "aid", "sid", "price", "size")])
+    stats = (C.c_double * 3)()
+    rc = lib.kme_router_rate_run(C.byref(ko), E, n_epochs, parts, stats)
+    if rc:
+        raise kme.KmeError(rc, "kme_router_rate_run")
+    return {"route_records_per_s": stats[0], "split_records_per_s": stats[1], "partitions": parts,
+            "epoch_records": E, "directory": int(stats[2]),
+            "threads": int(os.environ.get("KME_ROUTER_THREADS", 0)) or min(16, os.cpu_count() or 1),
+            "path": "integration/host_harness.c kme_router_rate_run: kme_router_route / kme_router_split, C-timed"}
+
+
 def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
     """The Java processor's path at rate, timed by the committed C harness
     (integration/host_harness.c): GpuMatchingEngine.java's schedule -- records written into two
@@ -491,6 +520,7 @@ def main():
     # the host-buffer path (after the market-data check: its epochs move the books on)
     host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, cfg.max_trades) \
         if host_epochs else None
+    router = measure_router(stream, E) if world == 1 and host_epochs else None   # (host CPU only)
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)
         d = eng.debug_counters().astype(np.float64).reshape(-1)[:12]
@@ -585,6 +615,7 @@ def main():
                             "verified": md_all},
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
             "host_path": host_path,
+            "router": router,
             "exact_ledger": ledger if flags & 1 else None,
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},

@@ -138,3 +138,61 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
     stats[7] = t_expand;
     return rc;
 }
+
+/* The partition router at rate (kme_router.cpp, the front of kme_multi / GpuMatchingEngine with
+ * nDevices > 1), timed here in C: n_epochs epochs of `epoch` records of `stream` into `parts`
+ * partitions through one router (the oid directory carries over), alternately kme_router_route and
+ * kme_router_split into buffers made and touched before the clock.  Host-only work.
+ * Stats out: [0] route records/s (best epoch), [1] split records/s (best epoch), [2] directory size. */
+int kme_router_rate_run(const kme_orders* stream, uint32_t epoch, uint32_t n_epochs, uint32_t parts, double* stats) {
+    if (!stream || !epoch || !parts || parts > 64 || !stats) return KME_E_INVALID;
+    kme_router* r = NULL;
+    int rc = kme_router_create(parts, (uint64_t)epoch * n_epochs, &r);
+    if (rc != KME_OK) return rc;
+    const size_t E = epoch;
+    int32_t* dest = (int32_t*)page_alloc(4 * E);
+    kme_orders_buf bufs[64];
+    uint8_t* echo[64];
+    uint32_t* index[64];
+    uint32_t counts[64];
+    memset(bufs, 0, sizeof bufs);
+    memset(echo, 0, sizeof echo);
+    memset(index, 0, sizeof index);
+    int ok = dest != NULL;
+    for (uint32_t k = 0; k < parts && ok; ++k) {
+        bufs[k].action = (int32_t*)page_alloc(4 * E); bufs[k].price = (int32_t*)page_alloc(4 * E);
+        bufs[k].size = (int32_t*)page_alloc(4 * E);
+        bufs[k].oid = (int64_t*)page_alloc(8 * E); bufs[k].aid = (int64_t*)page_alloc(8 * E);
+        bufs[k].sid = (int64_t*)page_alloc(8 * E);
+        echo[k] = (uint8_t*)page_alloc(E); index[k] = (uint32_t*)page_alloc(4 * E);
+        ok = bufs[k].action && bufs[k].price && bufs[k].size && bufs[k].oid && bufs[k].aid && bufs[k].sid && echo[k] && index[k];
+        if (ok) {   /* first touch outside the clock */
+            memset(bufs[k].action, 0, 4 * E); memset(bufs[k].price, 0, 4 * E); memset(bufs[k].size, 0, 4 * E);
+            memset(bufs[k].oid, 0, 8 * E); memset(bufs[k].aid, 0, 8 * E); memset(bufs[k].sid, 0, 8 * E);
+            memset(echo[k], 0, E); memset(index[k], 0, 4 * E);
+        }
+    }
+    if (ok) memset(dest, 0, 4 * E);
+    double best_route = 0, best_split = 0;
+    for (uint32_t ep = 0; ep < n_epochs && ok && rc == KME_OK; ++ep) {
+        const size_t b = (size_t)ep * E;
+        const kme_orders in = {stream->action + b, stream->oid + b, stream->aid + b, stream->sid + b, stream->price + b,
+                               stream->size + b};
+        const double t0 = now_s();
+        if (ep % 2 == 0) rc = kme_router_route(r, &in, epoch, dest);
+        else rc = kme_router_split(r, &in, epoch, bufs, counts, echo, index);
+        const double rate = (double)E / (now_s() - t0);
+        if (ep % 2 == 0) { if (rate > best_route) best_route = rate; }
+        else if (rate > best_split) best_split = rate;
+    }
+    stats[0] = best_route;
+    stats[1] = best_split;
+    stats[2] = (double)kme_router_directory_size(r);
+    for (uint32_t k = 0; k < parts; ++k) {
+        free(bufs[k].action); free(bufs[k].price); free(bufs[k].size);
+        free(bufs[k].oid); free(bufs[k].aid); free(bufs[k].sid); free(echo[k]); free(index[k]);
+    }
+    free(dest);
+    kme_router_destroy(r);
+    return ok ? rc : KME_E_INVALID;
+}

@@ -139,3 +139,12 @@ def test_c4_shard_workload_is_its_partition():
         assert shards == world and len(sids) == len(W.shard_symbols(65536, world, r))
         bs = np.isin(stream.action, (W.BUY, W.SELL))
         assert np.isin(stream.sid[bs], sids).all()
+
+
+def test_router_rate_is_timed_by_the_c_harness():
+    """bench.py's `router` field: kme_router_rate_run (integration/host_harness.c) routes and splits
+    epochs of the bench stream in C and reports the best epoch of each (host CPU only)."""
+    st = W.uniform(4 * (1 << 14), n_symbols=65536, n_accounts=65536, seed=1)
+    r = bench.measure_router(st, 1 << 14)
+    assert r["route_records_per_s"] > 1e5 and r["split_records_per_s"] > 1e5
+    assert r["partitions"] == 8 and 0 < r["directory"] <= 4 * (1 << 14)
