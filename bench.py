@@ -181,9 +181,11 @@ def library_comm(dist, torch, kme, eng, world: int, rank: int, dev):
     cannot be made (RCCL not loadable by the library): the bench then all-gathers through torch's
     RCCL and says so in its line."""
     # one RCCL for both: the library dlopens the copy torch's own collectives already use
-    trccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-    if os.path.exists(trccl):
-        os.environ.setdefault("KME_RCCL_LIB", trccl)
+    trccl = kme.torch_rccl_path()
+    try:
+        kme.rccl_load(trccl)
+    except kme.KmeError as ex:   # noqa: BLE001 (reported; the all-gather falls back to torch's)
+        print(f"rank {rank}: {ex}", file=sys.stderr, flush=True)
     uid = torch.zeros(128, dtype=torch.uint8, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     if rank == 0:

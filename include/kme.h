@@ -110,7 +110,8 @@ typedef struct kme_config {
     uint64_t max_resting;      /* resting orders the Orders store holds (FUNDED adds 64 node slots per
                                   symbol for the per-group allocation chunks; total < 2^31; FUNDED:
                                   max_resting + 64 (max_symbols + 1) + max_epoch <= 2^29) */
-    uint64_t ledger_capacity;  /* EXACT: hash capacity of Balances and of Positions */
+    uint64_t ledger_capacity;  /* exact ledger: entries Balances and Positions take before their first
+                                  growth (kme_ledger_stats; the tables grow between epochs) */
     int32_t device;            /* HIP device ordinal */
     uint32_t credit_shards;    /* FUNDED: number of symbol shards an account's credit is split over
                                   (0 or 1 = one engine).  Each shard proves its own orders against
@@ -264,8 +265,8 @@ const char* kme_build_id(void);
 
 /* Persistence (SURVEY §8 row f next-3; the reference keeps its state in RocksDB stores with
  * changelogs, KP:30-49, and commits after every record, KP:125).  kme_checkpoint writes the
- * engine's whole device state -- books, buckets, resting orders, oid table, the FUNDED reservation
- * ledger or the EXACT Balances/Positions, and the input sequence number -- to a file, between
+ * engine's device state -- books, buckets, resting orders, the FUNDED reservation ledger or the
+ * EXACT Balances/Positions, and the input sequence number -- to a file, between
  * epochs (call it after the epoch whose input offsets are being committed).  kme_restore loads
  * such a file into a freshly created engine of the same configuration; processing then resumes with
  * the records after the committed offset and produces exactly the tape an uninterrupted engine
@@ -281,6 +282,36 @@ kme_status kme_restore(kme_engine* e, const char* path);
  * large enough buffer); a format-1 file restores with an empty record. */
 kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes);
 kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t app_cap, size_t* app_bytes);
+/* What the file holds is the stores' live content (format 3): group states, the price levels whose
+ * bit is set, the used node pool, the FUNDED reservation ledger, the live Balances / Positions entries;
+ * the oid table is rebuilt from the resting orders on restore, the ledger tables at the size their
+ * entries need.  Every checkpoint file (and kme_multi manifest) ends with a trailer: the application
+ * record's size and a 64-bit digest of all bytes before it.  A restore recomputes the digest over
+ * what it reads and refuses a file that does not match (KME_E_INVALID, engine untouched).
+ * kme_checkpoint_inspect reads the trailer only: a commit point records (bytes, digest) of the
+ * checkpoint it wrote in a changelogged store, and a restart checks the file it finds against that
+ * record before trusting it. */
+typedef struct kme_checkpoint_info {
+    uint64_t file_bytes;   /* the whole file */
+    uint64_t app_bytes;    /* the application record */
+    uint64_t digest;       /* of every byte before the trailer */
+} kme_checkpoint_info;
+kme_status kme_checkpoint_inspect(const char* path, kme_checkpoint_info* out);
+
+/* The exact ledger's tables (EXACT mode, FUNDED + KME_FLAG_EXACT_LEDGER; else KME_E_UNSUPPORTED).
+ * Balances and Positions grow without bound in the reference (RocksDB, KP:30-37; H2 keeps stale
+ * value-keyed positions forever, KP:283-284, 434-436).  Here they are hash tables in HBM that the
+ * engine rehashes into larger ones between epochs, before the entries in use plus the most that the
+ * epochs in flight and the next one could add (one Balances entry per record, one Positions entry per
+ * ledger effect: a record's check or refund, two fills per trade) could pass half load; ledger_capacity
+ * only sets the initial size.  KME_D_CAP_LEDGER then means the device is out of memory. */
+typedef struct kme_ledger_info {
+    uint64_t bal_slots, pos_slots;   /* table sizes */
+    uint64_t bal_used, pos_used;     /* slots in use (live entries and tombstones) */
+    uint32_t grows;                  /* rehashes so far */
+    uint32_t _pad;
+} kme_ledger_info;
+kme_status kme_ledger_stats(kme_engine* e, kme_ledger_info* out);
 
 /* Canonical text snapshots (sorted), identical in format to the reference stores' contents:
  *   books : "B <key> <msb> <lsb>" (Books), "K <bucketPtr> <firstOid> <lastOid>" (Buckets),
@@ -310,6 +341,15 @@ kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uin
  * RCCL is loaded at the first call (env KME_RCCL_LIB, default librccl.so.1): libkme itself does not
  * depend on it. */
 typedef struct kme_comm kme_comm;
+/* Loads the RCCL the kme_comm_* calls use, once per process: `path` (NULL = env KME_RCCL_LIB, else
+ * librccl.so.1).  A process that already runs an RCCL (torch's) passes that library's path, so one
+ * RCCL serves both.  KME_E_INVALID when another copy was loaded already (a kme_comm_* call without
+ * kme_rccl_load loads the default), KME_E_UNSUPPORTED when it cannot be loaded. */
+kme_status kme_rccl_load(const char* path);
+/* The last RCCL failure of this process as text (ncclGetErrorString of the result and
+ * ncclGetLastError; "" when none): every kme_comm_* call that returns KME_E_HIP for an RCCL result
+ * records it here (and prints it to stderr). */
+const char* kme_rccl_last_error(void);
 kme_status kme_comm_unique_id(void* id128);
 kme_status kme_comm_init(kme_engine* e, uint32_t n_ranks, uint32_t rank, const void* id128, kme_comm** out);
 kme_status kme_comm_destroy(kme_comm* c);

@@ -3,6 +3,7 @@
 //
 //     .addProcessor("MatchingEngine", GpuMatchingEngine::new, "Source")
 //     .addStateStore(GpuMatchingEngine.commitHook(), "MatchingEngine")
+//     .addStateStore(GpuMatchingEngine.commitLog(), "MatchingEngine")
 //
 // Like the reference's MatchingEngine (KP:63) it is a Processor<String, Order> over the reference's
 // own top-level Order class (KP:449-475), in the same (default) package; it uses only Order's public
@@ -32,6 +33,15 @@
 // therefore either forwarded or in the checkpoint; output forwarded after a checkpoint may be
 // forwarded again after a crash (at least once, as the reference).
 //
+// The file lives in the task's local state directory; what makes it trustworthy on any instance is
+// the commit log, a changelogged key-value store (logging on, as the reference's five stores,
+// KP:30-49): each commit point puts one record -- the checkpoint's generation, offset, size and digest
+// -- and Kafka Streams sends it to the changelog before it commits the offsets.  init() reads that
+// record (restored from the changelog wherever the task runs) and refuses to start when the file it
+// names is missing, older, or not the file that was committed, instead of silently starting from an
+// empty book at a committed offset.  A file newer than the record (a crash between the file's rename
+// and the changelog write; Kafka then re-delivers from the older commit) is taken.
+//
 // Faults: the records before a fault took effect and are forwarded (as the reference's per-record
 // commit would have, KP:97, 124-125); then the processor fails like the reference's stream thread.
 // The default flags (EXACT_LEDGER | SERIAL_FALLBACK) give the reference's result for any stream, so
@@ -44,11 +54,14 @@ import java.time.Duration;
 import java.util.Collections;
 import java.util.Map;
 
+import org.apache.kafka.common.serialization.Serdes;
 import org.apache.kafka.streams.processor.Processor;
 import org.apache.kafka.streams.processor.ProcessorContext;
 import org.apache.kafka.streams.processor.PunctuationType;
 import org.apache.kafka.streams.processor.StateStore;
+import org.apache.kafka.streams.state.KeyValueStore;
 import org.apache.kafka.streams.state.StoreBuilder;
+import org.apache.kafka.streams.state.Stores;
 
 public final class GpuMatchingEngine implements Processor<String, Order> {
     static { System.loadLibrary("kme_jni"); }
@@ -59,6 +72,8 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     static final int KME_OK = 0;
     static final int ROW_BYTES = 48;    // kme_row: oid, aid, sid, prev (long); action, price, size (int); kind, has_prev
     public static final String COMMIT_STORE = "MatchingEngineCommit";
+    public static final String COMMIT_LOG = "MatchingEngineCommitLog";
+    static final String COMMIT_KEY = "checkpoint";
 
     private static native long create(int mode, int maxSymbols, int maxEpoch, long maxResting, int maxTrades,
                                       int maxAccounts, int flags, int device, int nDevices, long ledgerCapacity);
@@ -69,7 +84,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     private static native int complete(long h, int slot, long[] status);
     private static native void forwarded(long h, int slot);
     private static native String statusText(int status);
-    static native int checkpoint(long h, String path, long offset);
+    static native int checkpoint(long h, String path, long offset, long generation, long[] info);
     static native int restore(long h, String path, long[] out);
 
     private final int epoch;
@@ -79,6 +94,8 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     private ProcessorContext context;
     private long h;
     private File checkpointFile;
+    private KeyValueStore<String, byte[]> commitLog;
+    private long generation = 0;                    // of the last checkpoint written or restored
     // per slot: the six Order columns (KP:451-456) and the MatchOut rows
     private final ByteBuffer[] action = new ByteBuffer[2], oid = new ByteBuffer[2], aid = new ByteBuffer[2],
             sid = new ByteBuffer[2], price = new ByteBuffer[2], size = new ByteBuffer[2], rows = new ByteBuffer[2];
@@ -97,8 +114,9 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
 
     public GpuMatchingEngine() {
         // 65,537 symbol groups: sids up to 65,536 (BASELINE C3's universe is 1..65,536)
+        // (ledger capacity: the initial size only -- Balances / Positions grow between epochs)
         this(1 << 16, 1 << 18, KME_MODE_FUNDED, KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK, 65537, 1 << 20,
-             1L << 26, 0, 1, 1L << 24);
+             1L << 26, 0, 1, 1L << 20);
     }
 
     // nDevices > 1: the symbols keyed over GPUs device .. device + nDevices - 1 behind this one processor
@@ -133,11 +151,21 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         }
         final StateStore hook = context.getStateStore(COMMIT_STORE);
         if (hook instanceof CommitHook) ((CommitHook) hook).owner = this;
+        @SuppressWarnings("unchecked")
+        final KeyValueStore<String, byte[]> log = (KeyValueStore<String, byte[]>) context.getStateStore(COMMIT_LOG);
+        commitLog = log;
         checkpointFile = new File(context.stateDir(), "kme-" + context.taskId() + ".ckpt");
+        final byte[] committed = commitLog.get(COMMIT_KEY);           // restored from the changelog
+        final ByteBuffer want = committed == null ? null : ByteBuffer.wrap(committed);   // generation, offset, bytes, digest
         if (checkpointFile.exists()) {                                  // the state of the last commit
-            final long[] r = new long[6];
+            final long[] r = new long[9];
             final int rc = restore(h, checkpointFile.getPath(), r);
             if (rc != KME_OK) throw new IllegalStateException("kme restore: " + statusText(rc));
+            if (want != null && (r[6] < want.getLong(0) ||
+                                 (r[6] == want.getLong(0) && (r[7] != want.getLong(16) || r[8] != want.getLong(24)))))
+                throw new IllegalStateException("kme: " + checkpointFile + " (generation " + r[6] + ") is not the committed "
+                                                + "checkpoint (generation " + want.getLong(0) + ", offset " + want.getLong(8) + ")");
+            generation = r[6];
             skipThrough = checkpointed = lastOffset = r[0];
             for (int k = 0; k < (int) r[1]; k++) {                      // rows not forwarded before the crash
                 final int s = (int) r[2 + 2 * k];
@@ -146,6 +174,9 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
                 busy[s] = true;
                 ready[nReady++] = s;
             }
+        } else if (want != null) {                                      // committed state, file gone
+            throw new IllegalStateException("kme: the commit log names checkpoint generation " + want.getLong(0) + " (offset "
+                                            + want.getLong(8) + ") but " + checkpointFile + " is missing: the book cannot be rebuilt");
         }
         context.schedule(Duration.ofMillis(1), PunctuationType.WALL_CLOCK_TIME, ts -> punctuate());
     }
@@ -238,8 +269,13 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         while (inflight > 0) completeOldest(false);
         for (int k = 0; k < nReady; k++)                                // a faulted epoch is not a commit point
             if (readyStatus[ready[k]][0] != KME_OK) throw new IllegalStateException(statusText((int) readyStatus[ready[k]][0]));
-        final int rc = checkpoint(h, checkpointFile.getPath(), lastOffset);
+        final long[] info = new long[2];                              // the file's size and digest
+        final int rc = checkpoint(h, checkpointFile.getPath(), lastOffset, generation + 1, info);
         if (rc != KME_OK) throw new IllegalStateException("kme checkpoint: " + statusText(rc));
+        generation += 1;
+        // the commit log's record goes to the changelog before Kafka Streams commits the offsets
+        commitLog.put(COMMIT_KEY, ByteBuffer.allocate(32).putLong(generation).putLong(lastOffset).putLong(info[0])
+                                           .putLong(info[1]).array());
         checkpointed = lastOffset;
     }
 
@@ -261,6 +297,14 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         return new CommitHookBuilder(COMMIT_STORE);
     }
 
+    // ---- the commit log: which checkpoint each commit point wrote, changelogged (logging is on by
+    // default for a persistent key-value store; caching off, so the put reaches the changelog producer
+    // inside the commit, before the offsets)
+    public static StoreBuilder<KeyValueStore<String, byte[]>> commitLog() {
+        return Stores.keyValueStoreBuilder(Stores.persistentKeyValueStore(COMMIT_LOG), Serdes.String(), Serdes.ByteArray())
+                     .withCachingDisabled();
+    }
+
     public static final class CommitHook implements StateStore {
         private final String name;
         private GpuMatchingEngine owner;
@@ -273,7 +317,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
 
         @Override
         public void init(ProcessorContext context, StateStore root) {
-            context.register(root, (key, value) -> { });              // the checkpoint file is the state
+            context.register(root, (key, value) -> { });              // holds nothing (the commit log does)
             open = true;
         }
 
@@ -286,7 +330,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         public void close() { open = false; }
 
         @Override
-        public boolean persistent() { return true; }
+        public boolean persistent() { return false; }
 
         @Override
         public boolean isOpen() { return open; }

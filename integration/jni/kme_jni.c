@@ -19,11 +19,16 @@
  *                             detail, error index, records that took effect (kme_epoch_status).  The
  *                             rows stay "ready" (not yet forwarded) until forwarded(h, slot).
  *   forwarded(h, slot)        Java has forwarded the slot's rows
- *   checkpoint(h, path, off)  the commit point: kme_checkpoint_app of the engine
- *                             state with an application record = the last input offset the state
- *                             covers and the rows of every ready slot, oldest first
+ *   checkpoint(h, path, off, gen, info)
+ *                             the commit point: kme_checkpoint_app of the engine
+ *                             state with an application record = the commit's generation, the last
+ *                             input offset the state covers and the rows of every ready slot, oldest
+ *                             first; info = the file's size and digest (kme_checkpoint_inspect), which
+ *                             the processor logs to its changelogged commit store
  *   restore(h, path, out)     kme_restore_app: the state, the offset (out[0]) and the ready rows back
- *                             in their slots (out[1] = how many, then (slot, rows) pairs, oldest first)
+ *                             in their slots (out[1] = how many, then (slot, rows) pairs, oldest first);
+ *                             out[6..8] = the file's generation, size and digest (checked by the
+ *                             processor against the commit store's record)
  *
  * On an error the rows of the records that took effect ([0, n_effective)) are still produced: the
  * reference forwards and commits every record before the one that throws (KP:97, 124-125).
@@ -63,8 +68,8 @@ typedef struct jkme {
 } jkme;
 
 /* the application record of a checkpoint (kme_checkpoint_app) */
-#define JREC_MAGIC 0x4a454d4bu   /* "KMEJ" */
-typedef struct jrec_head { uint32_t magic, n_ready; int64_t offset; } jrec_head;
+#define JREC_MAGIC 0x324a4d4bu   /* "KMJ2" */
+typedef struct jrec_head { uint32_t magic, n_ready; int64_t offset; int64_t generation; } jrec_head;
 typedef struct jrec_slot { uint32_t slot, _pad; uint64_t rows; } jrec_slot;
 
 static void throw_state(JNIEnv* env, const char* msg) {
@@ -300,22 +305,24 @@ static int ready_order(const jkme* h, int order[2]) {
     return n;
 }
 
-/* static native int checkpoint(long h, String path, long offset): the commit point (called from the
- * commit hook's StateStore.flush(), before Kafka Streams commits the consumed offsets; INTEGRATION.md
- * §3): nothing may be in flight.  The file holds the engine state after every record up to `offset`
- * and the MatchOut rows of the ready slots, so a restart loses no output of a committed record. */
+/* static native int checkpoint(long h, String path, long offset, long generation, long[] info): the
+ * commit point (called from the commit hook's StateStore.flush(), before Kafka Streams commits the
+ * consumed offsets): nothing may be in flight.  The file holds the engine state after
+ * every record up to `offset` and the MatchOut rows of the ready slots, so a restart loses no output of
+ * a committed record; info[0..1] = the file's size and digest. */
 JNIEXPORT jint JNICALL Java_GpuMatchingEngine_checkpoint(JNIEnv* env, jclass cls, jlong handle, jstring path,
-                                                           jlong offset) {
+                                                           jlong offset, jlong generation, jlongArray info) {
     (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
     if (!h || !path || h->slot[0].n || h->slot[1].n) return KME_E_INVALID;
+    if (!info || (*env)->GetArrayLength(env, info) < 2) return KME_E_INVALID;
     int order[2];
     const int nr = ready_order(h, order);
     size_t bytes = sizeof(jrec_head);
     for (int k = 0; k < nr; ++k) bytes += sizeof(jrec_slot) + sizeof(kme_row) * (size_t)h->slot[order[k]].ready_rows;
     char* rec = (char*)malloc(bytes);
     if (!rec) return KME_E_CAPACITY;
-    jrec_head hd = {JREC_MAGIC, (uint32_t)nr, (int64_t)offset};
+    jrec_head hd = {JREC_MAGIC, (uint32_t)nr, (int64_t)offset, (int64_t)generation};
     memcpy(rec, &hd, sizeof hd);
     size_t at = sizeof hd;
     for (int k = 0; k < nr; ++k) {
@@ -328,41 +335,54 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_checkpoint(JNIEnv* env, jclass cls
     }
     const char* p = (*env)->GetStringUTFChars(env, path, NULL);
     kme_status s = KME_E_INVALID;
+    kme_checkpoint_info ci;
+    memset(&ci, 0, sizeof ci);
     if (p) {
         s = h_checkpoint(h, p, rec, bytes);
+        if (s == KME_OK) s = kme_checkpoint_inspect(p, &ci);
         (*env)->ReleaseStringUTFChars(env, path, p);
     }
     free(rec);
+    jlong iv[2] = {(jlong)ci.file_bytes, (jlong)ci.digest};
+    (*env)->SetLongArrayRegion(env, info, 0, 2, iv);
     return (jint)s;
 }
 
 /* static native int restore(long h, String path, long[] out): a fresh engine takes the state of the
  * checkpoint; out[0] = the last input offset it covers, out[1] = ready slots (rows to forward before
  * anything else), then (slot, rows) per ready slot, oldest first -- their rows are back in the
- * slots' row buffers.  Returns a kme_status. */
+ * slots' row buffers; out[6..8] = the checkpoint's generation, file size and digest.  A file without
+ * the processor's record is refused before the engine is touched.  Returns a kme_status. */
 JNIEXPORT jint JNICALL Java_GpuMatchingEngine_restore(JNIEnv* env, jclass cls, jlong handle, jstring path,
                                                         jlongArray out) {
     (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || !path || !out || (*env)->GetArrayLength(env, out) < 6) return KME_E_INVALID;
+    if (!h || !path || !out || (*env)->GetArrayLength(env, out) < 9) return KME_E_INVALID;
     if (h->slot[0].n || h->slot[1].n) return KME_E_INVALID;
     const char* p = (*env)->GetStringUTFChars(env, path, NULL);
     if (!p) return KME_E_INVALID;
-    size_t bytes = 0;
-    kme_status s = h_restore(h, p, NULL, 0, &bytes);
+    kme_checkpoint_info ci;
+    memset(&ci, 0, sizeof ci);
+    kme_status s = kme_checkpoint_inspect(p, &ci);
+    /* a checkpoint without the processor's record is not this processor's: refused untouched */
+    if (s == KME_OK && ci.app_bytes < sizeof(jrec_head)) s = KME_E_INVALID;
     char* rec = NULL;
-    if (s == KME_E_CAPACITY) {
-        rec = (char*)malloc(bytes);
-        s = rec ? h_restore(h, p, rec, bytes, &bytes) : KME_E_CAPACITY;
+    size_t bytes = 0;
+    if (s == KME_OK) {
+        rec = (char*)malloc((size_t)ci.app_bytes);
+        s = rec ? h_restore(h, p, rec, (size_t)ci.app_bytes, &bytes) : KME_E_CAPACITY;
     }
     (*env)->ReleaseStringUTFChars(env, path, p);
-    jlong o[6] = {-1, 0, 0, 0, 0, 0};
+    jlong o[9] = {-1, 0, 0, 0, 0, 0, 0, 0, 0};
     if (s == KME_OK) {
         jrec_head hd;
-        if (!rec || bytes < sizeof hd || (memcpy(&hd, rec, sizeof hd), hd.magic != JREC_MAGIC) || hd.n_ready > 2) {
-            s = KME_E_INVALID;   /* a checkpoint without the processor's record: not this processor's */
+        if (bytes < sizeof hd || (memcpy(&hd, rec, sizeof hd), hd.magic != JREC_MAGIC) || hd.n_ready > 2) {
+            s = KME_E_INVALID;   /* (the state is restored already: the processor fails on this status) */
         } else {
             o[0] = hd.offset;
+            o[6] = hd.generation;
+            o[7] = (jlong)ci.file_bytes;
+            o[8] = (jlong)ci.digest;
             size_t at = sizeof hd;
             for (uint32_t k = 0; k < hd.n_ready && s == KME_OK; ++k) {
                 jrec_slot rs;
@@ -385,6 +405,6 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_restore(JNIEnv* env, jclass cls, j
         }
     }
     free(rec);
-    (*env)->SetLongArrayRegion(env, out, 0, 6, o);
+    (*env)->SetLongArrayRegion(env, out, 0, 9, o);
     return (jint)s;
 }

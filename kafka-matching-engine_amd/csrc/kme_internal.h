@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <string>
 #include <vector>
 
 #include "kme.h"
@@ -21,5 +23,81 @@ kme_status credit_adjust_enqueue(kme_engine* e, const int64_t* dev_all, uint32_t
 kme_status resting_oids(kme_engine* e, std::vector<int64_t>& out);
 // a router's oid directory entries: each oid's last BUY/SELL went to `partition` (kme_router.cpp)
 void router_seed(kme_router* r, const int64_t* oids, size_t n, uint32_t partition);
+
+// ------------------------------------------------------------------ checkpoint files
+// Every checkpoint file (an engine's, a kme_multi manifest) ends with a trailer: the application
+// record's size and a 64-bit digest of every byte before the trailer, computed while writing
+// (kme_checkpoint_inspect reads it without the rest; a restore recomputes it over what it reads).
+struct CkptTrailer {
+    uint64_t app_bytes;
+    uint64_t digest;
+    char magic[8];
+};
+constexpr char kTrailerMagic[8] = {'K', 'M', 'E', 'D', 'G', 'S', 'T', '1'};
+
+// Four independent multiply-rotate lanes over 8-byte words (a dependency chain per lane, so the
+// host hashes at several GB/s); the tail bytes of a stream are zero-padded into a last word.
+struct Digest {
+    uint64_t h[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull, 0x082efa98ec4e6c89ull};
+    uint64_t n = 0;            // bytes consumed
+    uint8_t tail[32];
+    uint32_t nt = 0;           // bytes waiting in tail
+    static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+    void block(const uint8_t* p) {
+        for (int l = 0; l < 4; ++l) {
+            uint64_t w;
+            __builtin_memcpy(&w, p + 8 * l, 8);
+            h[l] = rotl(h[l] ^ (w * 0x9e3779b97f4a7c15ull), 29) * 0xbf58476d1ce4e5b9ull;
+        }
+    }
+    void update(const void* data, size_t len) {
+        const uint8_t* p = static_cast<const uint8_t*>(data);
+        n += len;
+        if (nt) {
+            const size_t take = len < 32 - nt ? len : 32 - nt;
+            __builtin_memcpy(tail + nt, p, take);
+            nt += (uint32_t)take; p += take; len -= take;
+            if (nt < 32) return;
+            block(tail);
+            nt = 0;
+        }
+        for (; len >= 32; p += 32, len -= 32) block(p);
+        if (len) { __builtin_memcpy(tail, p, len); nt = (uint32_t)len; }
+    }
+    uint64_t final() const {
+        Digest d = *this;
+        if (d.nt) { __builtin_memset(d.tail + d.nt, 0, 32 - d.nt); d.block(d.tail); }
+        uint64_t x = d.n * 0x94d049bb133111ebull;
+        for (int l = 0; l < 4; ++l) x = rotl(x ^ d.h[l], 31) * 0x9e3779b97f4a7c15ull;
+        return x ^ (x >> 29);
+    }
+};
+
+// Writes `path`.tmp through a digest, then (commit) the trailer, fsync of the file, rename over
+// `path` and fsync of the directory: after commit() returns true the new file is the durable one.
+struct CkptWriter {
+    std::string path, tmp;
+    FILE* f = nullptr;
+    Digest dg;
+    bool ok = false;
+    explicit CkptWriter(const char* p);
+    ~CkptWriter();
+    bool write(const void* data, size_t len);
+    bool commit(uint64_t app_bytes, uint64_t* digest_out);
+};
+// Reads a checkpoint file through a digest; verify() checks the trailer against it at the end.
+struct CkptReader {
+    FILE* f = nullptr;
+    Digest dg;
+    uint64_t size = 0;         // the file's size (trailer included)
+    bool ok = false;
+    explicit CkptReader(const char* p);
+    ~CkptReader();
+    bool read(void* data, size_t len);
+    bool at_trailer() const;   // everything before the trailer consumed
+    bool verify(CkptTrailer* t);
+};
+// fsync of the directory that holds `path` (a rename is durable only then)
+bool sync_dir_of(const std::string& path);
 
 }  // namespace kme

@@ -74,6 +74,17 @@ void launch_tob(const DevState& S, void* out, hipStream_t st);
 // rows >= n: rows past n are padding (-1 / 0)
 void launch_tob_groups(const DevState& S, const uint32_t* groups, uint32_t n, void* out, hipStream_t st, uint32_t rows = 0);
 void launch_init_state(const DevState& S, hipStream_t st);
+// store maintenance between epochs (kme_maint.hip): live entries of Balances / Positions (out2[0],
+// out2[1]); the live entries of O's tables rehashed into N's (fresh, empty) tables where they differ
+void launch_ledger_live(const DevState& S, unsigned long long* out2, hipStream_t st);
+void launch_ledger_rehash(const DevState& N, const DevState& O, unsigned long long* fail2, hipStream_t st);
+// checkpoint format 3: the set levels (index in _pad[0]), live Balances (aid, value) and Positions
+// (k0, k1, v0, v1); their restore into an engine whose levels / tables are empty
+void launch_ckpt_levels(const DevState& S, Level* out, unsigned long long* cnt, hipStream_t st);
+void launch_rst_levels(const DevState& S, const Level* in, uint32_t n, hipStream_t st);
+void launch_ckpt_ledger(const DevState& S, void* bal_out, void* pos_out, unsigned long long* cnt2, hipStream_t st);
+void launch_rst_ledger(const DevState& S, const void* bal_in, uint32_t nb, const void* pos_in, uint32_t np,
+                       unsigned long long* fail, hipStream_t st);
 // credit between symbol shards: (funded bound, demand) per account out; the re-split from all shards' pairs
 void launch_credit_state(const DevState& S, int64_t* out, hipStream_t st);
 // all: n blocks of `stride` int64 words each ([0, A) bound, [A, 2A) demand, -1 = absent on that shard)

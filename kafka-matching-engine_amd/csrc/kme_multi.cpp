@@ -45,12 +45,17 @@ struct Part {
 
 enum : int { kSlotIdle = 0, kSlotQueued, kSlotCollected, kSlotDone };
 
-constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '1'};
+constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '2'};
+// the manifest: this header, n shard records (the digest and size of each shard's file: the
+// manifest's own digest covers them), the application record, the trailer (kme_internal.h)
 struct MultiHeader {
     char magic[8];
     uint32_t n, _pad;
     uint64_t generation;
     uint64_t app_bytes;
+};
+struct MultiShard {
+    uint64_t file_bytes, digest;
 };
 
 }  // namespace
@@ -235,6 +240,10 @@ static kme_status split_submit(kme_multi* m, int slot, const kme_orders* in, uin
         s = kme_submit_epoch_host(m->eng[k], &pin, p.count, &p.res);
         if (s != KME_OK) {   // the shards before k hold a part of this epoch: nothing consistent remains
             m->failed = 1;
+            // their parts land before anything can free the slot's buffers (kme_multi_destroy waits only
+            // for the epochs counted in flight)
+            kme_epoch_status st;
+            for (uint32_t j = 0; j < k; ++j) (void)kme_wait(m->eng[j], &st);
             return s;
         }
     }
@@ -462,31 +471,35 @@ kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out) {
     return KME_OK;
 }
 
-// Checkpoint: every engine into path.g<generation>.<k>, then the manifest at `path` (written to
-// path.tmp and renamed: the commit of the set), then the previous generation's files are removed.
+// Checkpoint: every engine into path.g<generation>.<k>, then the manifest at `path` (CkptWriter:
+// written to path.tmp, fsync'd, renamed, the directory fsync'd -- the commit of the set), and only then
+// are the previous generation's files removed: a crash at any point leaves a manifest whose shard
+// files all exist.
 kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* app, size_t app_bytes) {
     if (!m || !path || (app_bytes && !app)) return KME_E_INVALID;
     if (m->failed) return KME_E_FAILED;
     if (m->inflight) return KME_E_INVALID;
     const uint64_t gen = m->generation + 1;
     const std::string base(path);
+    std::vector<MultiShard> shards(m->n);
     for (uint32_t k = 0; k < m->n; ++k) {
         const std::string f = base + ".g" + std::to_string(gen) + "." + std::to_string(k);
         if (kme_status s = kme_checkpoint_app(m->eng[k], f.c_str(), nullptr, 0)) return s;
+        kme_checkpoint_info ci{};
+        if (kme_status s = kme_checkpoint_inspect(f.c_str(), &ci)) return s;
+        shards[k] = {ci.file_bytes, ci.digest};
     }
     MultiHeader h{};
     std::memcpy(h.magic, kMultiMagic, sizeof h.magic);
     h.n = m->n;
     h.generation = gen;
     h.app_bytes = app_bytes;
-    const std::string tmp = base + ".tmp";
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) return KME_E_INVALID;
-    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && (app_bytes == 0 || std::fwrite(app, 1, app_bytes, f) == app_bytes);
-    ok = std::fflush(f) == 0 && ok;
-    ok = std::fclose(f) == 0 && ok;
-    ok = ok && std::rename(tmp.c_str(), path) == 0;
-    if (!ok) return KME_E_INVALID;
+    {
+        kme::CkptWriter w(path);
+        bool ok = w.write(&h, sizeof h) && w.write(shards.data(), shards.size() * sizeof(MultiShard)) && w.write(app, app_bytes) &&
+                  w.commit(app_bytes, nullptr);
+        if (!ok) return KME_E_INVALID;
+    }
     for (uint32_t k = 0; k < m->n && m->generation; ++k)
         std::remove((base + ".g" + std::to_string(m->generation) + "." + std::to_string(k)).c_str());
     m->generation = gen;
@@ -498,24 +511,33 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
     if (m->failed) return KME_E_FAILED;
     if (m->inflight) return KME_E_INVALID;
     if (app_bytes) *app_bytes = 0;
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return KME_E_INVALID;
+    kme::CkptReader r(path);
     MultiHeader h{};
-    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 &&
-              h.n == m->n && h.app_bytes < (1ull << 40);
+    bool ok = r.read(&h, sizeof h) && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 && h.n == m->n &&
+              h.app_bytes < (1ull << 40);
+    std::vector<MultiShard> shards(ok ? m->n : 0);
     std::vector<char> rec;
-    if (ok && h.app_bytes) {
+    ok = ok && r.read(shards.data(), shards.size() * sizeof(MultiShard));
+    if (ok) {
         rec.resize(h.app_bytes);
-        ok = std::fread(rec.data(), 1, rec.size(), f) == rec.size();
+        ok = r.read(rec.data(), rec.size());
     }
-    std::fclose(f);
+    kme::CkptTrailer t{};
+    ok = ok && r.verify(&t);
     if (!ok) return KME_E_INVALID;
     if (app_bytes) *app_bytes = rec.size();
     if (rec.size() > app_cap || (rec.size() && !app)) return KME_E_CAPACITY;
+    // every shard's file is the one the manifest committed (before any engine is touched)
     const std::string base(path);
+    auto shard_path = [&](uint32_t k) { return base + ".g" + std::to_string(h.generation) + "." + std::to_string(k); };
     for (uint32_t k = 0; k < m->n; ++k) {
-        const std::string fk = base + ".g" + std::to_string(h.generation) + "." + std::to_string(k);
-        if (kme_status s = kme_restore(m->eng[k], fk.c_str())) {
+        kme_checkpoint_info ci{};
+        if (kme_checkpoint_inspect(shard_path(k).c_str(), &ci) != KME_OK || ci.file_bytes != shards[k].file_bytes ||
+            ci.digest != shards[k].digest)
+            return KME_E_INVALID;
+    }
+    for (uint32_t k = 0; k < m->n; ++k) {
+        if (kme_status s = kme_restore(m->eng[k], shard_path(k).c_str())) {
             if (k > 0) m->failed = 1;   // some shards restored, others not
             return s;
         }

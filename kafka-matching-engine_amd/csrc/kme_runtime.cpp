@@ -7,6 +7,7 @@
 //   kme_destroy           MatchingEngine.close KP:129
 //   kme_snapshot_*        the contents of Books/Buckets/Orders and Balances/Positions
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -109,6 +110,11 @@ struct kme_engine {
     bool host_epoch[2] = {};              // the epoch of this slot is a host epoch
     bool host_mapped[2] = {};             // its trades go out through the device mapping (k_export_trades)
     kme_epoch_result host_out[2] = {};    // the caller's result buffers of that epoch
+    // exact Balances / Positions (EXACT mode, FUNDED + KME_FLAG_EXACT_LEDGER): rehashed into larger
+    // tables between epochs (ledger_reserve), ledger_grows times so far
+    bool ledger = false;
+    uint32_t ledger_grows = 0;
+    unsigned long long* d_maint = nullptr;   // 4 words of maintenance-kernel results
 };
 
 #define HIP_TRY(x)                                                                          \
@@ -128,6 +134,23 @@ static kme_status dalloc(kme_engine* e, T** p, size_t count) {
     e->allocs.push_back(q);
     *p = reinterpret_cast<T*>(q);
     return KME_OK;
+}
+static void dfree(kme_engine* e, void* p) {
+    if (!p) return;
+    auto it = std::find(e->allocs.begin(), e->allocs.end(), p);
+    if (it != e->allocs.end()) e->allocs.erase(it);
+    (void)hipFree(p);
+}
+
+// ------------------------------------------------------------------ ledger table sizes
+// The most entries one epoch can add: Balances one per CREATE_BALANCE record (KP:131-138); Positions
+// one per ledger effect -- a record's checkBalance / postRemoveAdjustments, both fillOrder calls of
+// each trade (KP:167-182, 276-287, 325-333) -- each reads one key and writes at most one new one.
+static uint64_t bal_bound(const kme_config& c) { return c.max_epoch; }
+static uint64_t pos_bound(const kme_config& c) { return (uint64_t)c.max_epoch + 2ull * c.max_trades; }
+// Slots for `live` entries plus `ahead` epochs of worst-case growth at no more than half load.
+static uint64_t ledger_slots(uint64_t live, uint64_t bound, uint64_t ahead) {
+    return pow2_at_least(std::max<uint64_t>(2 * (live + ahead * bound), 2048));
 }
 
 #define ALLOC(ptr, n)                                  \
@@ -318,15 +341,20 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         }
     }
     if (exact_ledger) {
-        const uint64_t lc = pow2_at_least(std::max<uint64_t>(2 * std::max<uint64_t>(cfg->ledger_capacity, 1024), 2048));
-        if (lc > (1ull << 31)) { kme_destroy(e); return KME_E_INVALID; }
-        S.bal_mask = (uint32_t)(lc - 1);
-        S.pos_mask = (uint32_t)(lc - 1);
-        ALLOC(S.bal_state, lc);
-        ALLOC(S.bal_key, lc);
-        ALLOC(S.bal_val, lc);
-        ALLOC(S.pos, lc);
+        // ledger_capacity: the entries the tables take before their first growth; at least two
+        // epochs' worth (one in flight, the next), so that ledger_reserve can always run between them
+        e->ledger = true;
+        const uint64_t lb = ledger_slots(std::max<uint64_t>(cfg->ledger_capacity, 1024), bal_bound(*cfg), 2);
+        const uint64_t lp = ledger_slots(std::max<uint64_t>(cfg->ledger_capacity, 1024), pos_bound(*cfg), 2);
+        if (lb > (1ull << 31) || lp > (1ull << 31)) { kme_destroy(e); return KME_E_INVALID; }
+        S.bal_mask = (uint32_t)(lb - 1);
+        S.pos_mask = (uint32_t)(lp - 1);
+        ALLOC(S.bal_state, lb);
+        ALLOC(S.bal_key, lb);
+        ALLOC(S.bal_val, lb);
+        ALLOC(S.pos, lp);
     }
+    ALLOC(e->d_maint, 4);
     ALLOC(S.epos, E);
     ALLOC(S.route_grp, E);
     ALLOC(S.cancel_tgt, E);
@@ -382,9 +410,8 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         HIP_TRY(hipMemsetAsync(S.acct_demand, 0, cfg->max_accounts * sizeof(int64_t), st));
     }
     if (exact_ledger) {
-        const size_t lc = (size_t)S.bal_mask + 1;
-        HIP_TRY(hipMemsetAsync(S.bal_state, 0, lc * sizeof(uint32_t), st));
-        HIP_TRY(hipMemsetAsync(S.pos, 0, lc * sizeof(PosEntry), st));
+        HIP_TRY(hipMemsetAsync(S.bal_state, 0, ((size_t)S.bal_mask + 1) * sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(S.pos, 0, ((size_t)S.pos_mask + 1) * sizeof(PosEntry), st));
     }
     launch_init_state(S, st);
     HIP_TRY(hipGetLastError());
@@ -551,6 +578,89 @@ kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in, uint32_t
     return submit(e, in, n, out);
 }
 
+// Online growth of Balances / Positions (the reference's RocksDB stores grow without bound, KP:30-37;
+// H2 leaves stale value-keyed positions forever, KP:283-284, 434-436).  Called between epochs with the
+// tables' used slots (live entries + tombstones) after the newest completed epoch: when they plus the
+// worst case of `ahead` more epochs could pass half load, the stream is drained and the live entries
+// are rehashed (kme_maint.hip) into tables sized for them plus two epochs -- at least twice the old
+// size when the live entries are what grew, the same size when tombstones filled the old one.
+// *changed: the tables were rebuilt (the callers' copies of the used counters are stale).  A failed
+// allocation leaves the tables as they are: the device check (KME_D_CAP_LEDGER) then fires only when
+// they are really full, i.e. HBM is exhausted.
+static kme_status ledger_reserve(kme_engine* e, uint64_t bal_used, uint64_t pos_used, uint64_t ahead, bool* changed) {
+    *changed = false;
+    DevState& S = e->S;
+    const uint64_t bs = (uint64_t)S.bal_mask + 1, ps = (uint64_t)S.pos_mask + 1;
+    const uint64_t bb = bal_bound(e->cfg), pb = pos_bound(e->cfg);
+    if (2 * (bal_used + ahead * bb) <= bs && 2 * (pos_used + ahead * pb) <= ps) return KME_OK;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long live[2];
+    launch_ledger_live(S, e->d_maint, e->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(live, e->d_maint, sizeof live, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    auto target = [](uint64_t slots, uint64_t lv, uint64_t used, uint64_t bound) -> uint64_t {
+        const uint64_t need = ledger_slots(lv, bound, 2);
+        if (need > slots) return std::max(need, 2 * slots);
+        return 2 * (used + 2 * bound) > slots ? slots : 0;   // tombstones: same size; 0 = keep the table
+    };
+    const uint64_t nb = target(bs, live[0], bal_used, bb), np = target(ps, live[1], pos_used, pb);
+    if (nb > (1ull << 31) || np > (1ull << 31)) return KME_OK;   // (the tables' masks are 32-bit: full means full)
+    DevState N = S;
+    bool alloc_ok = true;
+    auto tryalloc = [&](void** p, size_t bytes) {
+        if (!alloc_ok) return;
+        if (hipMalloc(p, bytes) != hipSuccess) { (void)hipGetLastError(); alloc_ok = false; *p = nullptr; }
+    };
+    if (nb) {
+        tryalloc((void**)&N.bal_state, nb * sizeof(uint32_t));
+        tryalloc((void**)&N.bal_key, nb * sizeof(int64_t));
+        tryalloc((void**)&N.bal_val, nb * sizeof(int64_t));
+        N.bal_mask = (uint32_t)(nb - 1);
+    }
+    if (np) {
+        tryalloc((void**)&N.pos, np * sizeof(PosEntry));
+        N.pos_mask = (uint32_t)(np - 1);
+    }
+    if (!alloc_ok) {   // out of HBM: free what was taken, keep the old tables
+        if (nb) { (void)hipFree(N.bal_state); (void)hipFree(N.bal_key); (void)hipFree(N.bal_val); }
+        if (np) (void)hipFree(N.pos);
+        std::fprintf(stderr, "kme: ledger tables cannot grow (HBM): %llu / %llu slots kept\n", (unsigned long long)bs,
+                     (unsigned long long)ps);
+        return KME_OK;
+    }
+    if (nb) HIP_TRY(hipMemsetAsync(N.bal_state, 0, nb * sizeof(uint32_t), e->stream));
+    if (np) HIP_TRY(hipMemsetAsync(N.pos, 0, np * sizeof(PosEntry), e->stream));
+    launch_ledger_rehash(N, S, e->d_maint + 2, e->stream);
+    HIP_TRY(hipGetLastError());
+    unsigned long long fail[2];
+    HIP_TRY(hipMemcpyAsync(fail, e->d_maint + 2, sizeof fail, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (fail[0] || fail[1]) return KME_E_CAPACITY;   // (cannot happen: the new tables are at most half full)
+    for (auto& a : e->allocs) {   // the new tables take the old ones' places in the allocation list
+        if (nb && a == (void*)S.bal_state) a = N.bal_state;
+        else if (nb && a == (void*)S.bal_key) a = N.bal_key;
+        else if (nb && a == (void*)S.bal_val) a = N.bal_val;
+        else if (np && a == (void*)S.pos) a = N.pos;
+    }
+    if (nb) { HIP_TRY(hipFree(S.bal_state)); HIP_TRY(hipFree(S.bal_key)); HIP_TRY(hipFree(S.bal_val)); }
+    if (np) HIP_TRY(hipFree(S.pos));
+    S = N;
+    // used = live after a rehash (no tombstones)
+    const unsigned long long bu = nb ? live[0] : bal_used, pu = np ? live[1] : pos_used;
+    HIP_TRY(hipMemcpyAsync(&e->S.ctr[ci(C_BAL_USED)], &bu, sizeof bu, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(&e->S.ctr[ci(C_POS_USED)], &pu, sizeof pu, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_S, &e->S, sizeof(DevState), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int s = 0; s < 3; ++s) {   // the counter copies of completed epochs not yet waited for
+        e->h_ctr[s * (size_t)C_NCTR * CTR_STRIDE + ci(C_BAL_USED)] = bu;
+        e->h_ctr[s * (size_t)C_NCTR * CTR_STRIDE + ci(C_POS_USED)] = pu;
+    }
+    ++e->ledger_grows;
+    *changed = true;
+    return KME_OK;
+}
+
 kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     if (!e) return KME_E_INVALID;
     kme_epoch_status s{};
@@ -635,6 +745,13 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
         if (rc[ci(C_REBUILD_FAIL)] != 0 || rc[ci(C_OTAB_USED)] * 4 > e->otab_cap * 3) {
             e->failed = 1; e->fail_status = KME_E_CAPACITY; e->fail_detail = KME_D_CAP_OIDTAB;
         }
+    }
+    // the ledger tables: room for the epochs in flight and the next one (the newest counters known:
+    // an epoch still in flight adds at most one epoch's bound on top of these)
+    if (!e->failed && e->ledger) {
+        bool changed = false;
+        const kme_status r = ledger_reserve(e, c[ci(C_BAL_USED)], c[ci(C_POS_USED)], (uint64_t)1 + e->inflight, &changed);
+        if (r != KME_OK) { e->failed = 1; e->fail_status = r; e->fail_detail = KME_D_CAP_LEDGER; }
     }
     if (st) *st = s;
     return (kme_status)s.status;
@@ -765,34 +882,66 @@ kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in, uint32_t n
 
 // ------------------------------------------------------------------ multi-GPU: RCCL
 namespace {
-// RCCL through dlopen: libkme has no link-time dependency on it, and a process that already loaded
-// an RCCL (torch's) can point KME_RCCL_LIB at that copy so that one RCCL serves both.
+// RCCL through dlopen: libkme has no link-time dependency on it.  The copy is chosen explicitly
+// (kme_rccl_load: a process that already loaded an RCCL -- torch's -- hands its path, so that one RCCL
+// serves both); a kme_comm_* call before that loads the default (env KME_RCCL_LIB, else
+// librccl.so.1).  Every RCCL failure is kept as text (kme_rccl_last_error) and printed.
 struct Rccl {
     void* h = nullptr;
+    std::string path;
     decltype(&ncclGetUniqueId) get_id = nullptr;
     decltype(&ncclCommInitRank) init = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllGather) allgather = nullptr;
+    decltype(&ncclGetErrorString) err_str = nullptr;
+    decltype(&ncclGetLastError) last_err = nullptr;
 };
-Rccl* rccl() {
-    static Rccl r;
-    static bool tried = false;
-    if (!tried) {
-        tried = true;
-        const char* path = std::getenv("KME_RCCL_LIB");
-        r.h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (r.h) {
-            r.get_id = (decltype(r.get_id))dlsym(r.h, "ncclGetUniqueId");
-            r.init = (decltype(r.init))dlsym(r.h, "ncclCommInitRank");
-            r.destroy = (decltype(r.destroy))dlsym(r.h, "ncclCommDestroy");
-            r.allgather = (decltype(r.allgather))dlsym(r.h, "ncclAllGather");
-        }
-        if (!r.get_id || !r.init || !r.destroy || !r.allgather) {
-            std::fprintf(stderr, "kme: RCCL not available (%s)\n", r.h ? "missing symbols" : dlerror());
-            r.h = nullptr;
-        }
+Rccl g_rccl;
+std::string g_rccl_error;
+kme_status rccl_open(const char* path) {
+    Rccl& r = g_rccl;
+    const std::string want = path && *path ? path : "librccl.so.1";
+    if (r.h) return r.path == want ? KME_OK : KME_E_INVALID;
+    void* h = dlopen(want.c_str(), RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        g_rccl_error = std::string("dlopen ") + want + ": " + dlerror();
+        std::fprintf(stderr, "kme: RCCL not available (%s)\n", g_rccl_error.c_str());
+        return KME_E_UNSUPPORTED;
     }
-    return r.h ? &r : nullptr;
+    r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
+    r.init = (decltype(r.init))dlsym(h, "ncclCommInitRank");
+    r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+    r.allgather = (decltype(r.allgather))dlsym(h, "ncclAllGather");
+    r.err_str = (decltype(r.err_str))dlsym(h, "ncclGetErrorString");
+    r.last_err = (decltype(r.last_err))dlsym(h, "ncclGetLastError");
+    if (!r.get_id || !r.init || !r.destroy || !r.allgather) {
+        g_rccl_error = want + ": missing symbols";
+        std::fprintf(stderr, "kme: RCCL not available (%s)\n", g_rccl_error.c_str());
+        dlclose(h);
+        r = Rccl{};
+        return KME_E_UNSUPPORTED;
+    }
+    r.h = h;
+    r.path = want;
+    return KME_OK;
+}
+Rccl* rccl() {
+    if (!g_rccl.h) {
+        const char* env = std::getenv("KME_RCCL_LIB");
+        if (rccl_open(env) != KME_OK) return nullptr;
+    }
+    return &g_rccl;
+}
+// an RCCL call's result: OK, or KME_E_HIP with the library's own account of it kept and printed
+kme_status rccl_check(ncclResult_t res, const char* what, ncclComm_t comm) {
+    if (res == ncclSuccess) return KME_OK;
+    const Rccl& r = g_rccl;
+    g_rccl_error = std::string(what) + ": " + (r.err_str ? r.err_str(res) : "rccl error") + " (ncclResult_t " +
+                   std::to_string((int)res) + ")";
+    const char* last = r.last_err ? r.last_err(comm) : nullptr;
+    if (last && *last) g_rccl_error += std::string("; ") + last;
+    std::fprintf(stderr, "kme: %s\n", g_rccl_error.c_str());
+    return KME_E_HIP;
 }
 }  // namespace
 
@@ -805,13 +954,16 @@ struct kme_comm {
     size_t credit_accounts = 0;
 };
 
+kme_status kme_rccl_load(const char* path) { return rccl_open(path); }
+const char* kme_rccl_last_error(void) { return g_rccl_error.c_str(); }
+
 kme_status kme_comm_unique_id(void* id128) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId");
     if (!id128) return KME_E_INVALID;
     Rccl* r = rccl();
     if (!r) return KME_E_UNSUPPORTED;
     ncclUniqueId id;
-    if (r->get_id(&id) != ncclSuccess) return KME_E_HIP;
+    if (kme_status s = rccl_check(r->get_id(&id), "ncclGetUniqueId", nullptr)) return s;
     std::memcpy(id128, &id, sizeof id);
     return KME_OK;
 }
@@ -825,7 +977,10 @@ kme_status kme_comm_init(kme_engine* e, uint32_t n_ranks, uint32_t rank, const v
     std::memcpy(&id, id128, sizeof id);
     kme_comm* c = new kme_comm();
     c->n = n_ranks; c->rank = rank; c->device = e->device;
-    if (r->init(&c->comm, (int)n_ranks, id, (int)rank) != ncclSuccess) { delete c; return KME_E_HIP; }
+    if (kme_status s = rccl_check(r->init(&c->comm, (int)n_ranks, id, (int)rank), "ncclCommInitRank", nullptr)) {
+        delete c;
+        return s;
+    }
     *out = c;
     return KME_OK;
 }
@@ -850,8 +1005,9 @@ kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t*
     kme_tob* mine = dev_all + (size_t)c->rank * rows_per_rank;
     launch_tob_groups(e->S, dev_groups, n_groups, mine, e->stream, rows_per_rank);
     HIP_TRY(hipGetLastError());
-    if (r->allgather(mine, dev_all, (size_t)rows_per_rank * sizeof(kme_tob), ncclUint8, c->comm, e->stream) != ncclSuccess)
-        return KME_E_HIP;
+    if (kme_status s = rccl_check(r->allgather(mine, dev_all, (size_t)rows_per_rank * sizeof(kme_tob), ncclUint8, c->comm, e->stream),
+                                  "ncclAllGather (market data)", c->comm))
+        return s;
     return KME_OK;
 }
 
@@ -902,8 +1058,9 @@ kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c) {
     else HIP_TRY(hipMemsetAsync(mine, 0, 2 * A * sizeof(int64_t), e->stream));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(mine + 2 * A, &c->h_status[c->n], sizeof(int64_t), hipMemcpyHostToDevice, e->stream));
-    if (r->allgather(mine, c->d_credit, stride * sizeof(int64_t), ncclUint8, c->comm, e->stream) != ncclSuccess)
-        return KME_E_HIP;
+    if (kme_status s = rccl_check(r->allgather(mine, c->d_credit, stride * sizeof(int64_t), ncclUint8, c->comm, e->stream),
+                                  "ncclAllGather (credit)", c->comm))
+        return s;
     HIP_TRY(hipMemcpy2DAsync(c->h_status, sizeof(int64_t), c->d_credit + 2 * A, stride * sizeof(int64_t), sizeof(int64_t),
                              c->n, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -958,83 +1115,198 @@ extern "C" {
 const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
+// Format 3: header, then the stores in their compact form -- group states, the set price levels
+// (kme_maint.hip), the used prefix of the node pool, the FUNDED reservation ledger, the live Balances
+// and Positions entries -- then the application record, then the trailer (size of that record and
+// the digest of everything before it; kme_internal.h).  The oid table is not stored: a restore
+// rebuilds it from the resting orders (an entry of an order that no longer rests is only ever a stale
+// fact), and the ledger tables are rebuilt at the size their live entries need.
 namespace {
-constexpr char kCkptMagic[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '1'};    // format 1: no application record
-constexpr char kCkptMagic2[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '2'};
-struct CkptHeader {
+constexpr char kCkptMagic3[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '3'};
+struct CkptHeader3 {
     char magic[8];
     kme_config cfg;
     int64_t seq_base;
-    uint64_t pool_used, otab_used, bal_used, pos_used;
+    uint64_t pool_used, n_levels, bal_live, pos_live, app_bytes;
+    uint64_t _reserved[3];
 };
-struct Blob { void* dev; size_t bytes; };
+constexpr size_t kChunk = 64ull << 20;   // device <-> host staging per copy
 
-std::vector<Blob> state_blobs(kme_engine* e, uint64_t pool_used) {
-    const DevState& S = e->S;
-    const size_t G = e->cfg.max_symbols;
-    std::vector<Blob> b = {
-        {S.grp, G * sizeof(GroupState)},
-        {S.lev, G * 2 * NLEV * sizeof(Level)},
-        {S.pool, pool_used * sizeof(Node)},
-        {S.otab, e->otab_cap * sizeof(uint64_t)},
-    };
-    if (e->cfg.mode == KME_MODE_FUNDED) {
-        b.push_back({S.acct_since, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
-        b.push_back({S.acct_lb, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
-        b.push_back({S.acct_demand, (size_t)e->cfg.max_accounts * sizeof(int64_t)});
+// n bytes of device memory at `dev` into the writer, through a host staging buffer
+bool put_dev(kme::CkptWriter& w, const void* dev, size_t n, std::vector<char>& stage) {
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t c = std::min(kChunk, n - off);
+        stage.resize(std::max(stage.size(), c));
+        if (hipMemcpy(stage.data(), (const char*)dev + off, c, hipMemcpyDeviceToHost) != hipSuccess) return false;
+        if (!w.write(stage.data(), c)) return false;
     }
-    if (e->cfg.mode == KME_MODE_EXACT || S.ledger_replay) {
-        const size_t lc = (size_t)S.bal_mask + 1;
-        b.push_back({S.bal_state, lc * sizeof(uint32_t)});
-        b.push_back({S.bal_key, lc * sizeof(int64_t)});
-        b.push_back({S.bal_val, lc * sizeof(int64_t)});
-        b.push_back({S.pos, lc * sizeof(PosEntry)});
-    }
-    return b;
+    return true;
 }
 }  // namespace
+}  // extern "C"
 
-// Format: header, the state blobs (u64 size + bytes each), then the application record (u64 size +
-// bytes; format 2).  Written to `path`.tmp, flushed to disk, then renamed over `path`: a crash while
-// writing leaves the previous checkpoint whole.
+namespace kme {
+CkptWriter::CkptWriter(const char* p) : path(p), tmp(std::string(p) + ".tmp") {
+    f = std::fopen(tmp.c_str(), "wb");
+    ok = f != nullptr;
+}
+CkptWriter::~CkptWriter() {
+    if (f) { std::fclose(f); std::remove(tmp.c_str()); }
+}
+bool CkptWriter::write(const void* data, size_t len) {
+    if (!ok) return false;
+    dg.update(data, len);
+    ok = len == 0 || std::fwrite(data, 1, len, f) == len;
+    return ok;
+}
+bool CkptWriter::commit(uint64_t app_bytes, uint64_t* digest_out) {
+    if (!ok) return false;
+    CkptTrailer t{};
+    t.app_bytes = app_bytes;
+    t.digest = dg.final();
+    std::memcpy(t.magic, kTrailerMagic, sizeof t.magic);
+    ok = std::fwrite(&t, sizeof t, 1, f) == 1;
+    ok = std::fflush(f) == 0 && ok;
+    ok = fsync(fileno(f)) == 0 && ok;
+    ok = std::fclose(f) == 0 && ok;
+    f = nullptr;
+    ok = ok && std::rename(tmp.c_str(), path.c_str()) == 0;
+    if (!ok) { std::remove(tmp.c_str()); return false; }
+    ok = sync_dir_of(path);
+    if (digest_out) *digest_out = t.digest;
+    return ok;
+}
+CkptReader::CkptReader(const char* p) {
+    f = std::fopen(p, "rb");
+    if (!f) return;
+    ok = std::fseek(f, 0, SEEK_END) == 0;
+    const long sz = ok ? std::ftell(f) : -1;
+    ok = ok && sz >= (long)sizeof(CkptTrailer) && std::fseek(f, 0, SEEK_SET) == 0;
+    size = sz > 0 ? (uint64_t)sz : 0;
+}
+CkptReader::~CkptReader() {
+    if (f) std::fclose(f);
+}
+bool CkptReader::read(void* data, size_t len) {
+    if (!ok) return false;
+    if (dg.n + len + sizeof(CkptTrailer) > size) { ok = false; return false; }   // (never into the trailer)
+    ok = len == 0 || std::fread(data, 1, len, f) == len;
+    if (ok) dg.update(data, len);
+    return ok;
+}
+bool CkptReader::at_trailer() const { return ok && dg.n + sizeof(CkptTrailer) == size; }
+bool CkptReader::verify(CkptTrailer* t) {
+    if (!at_trailer()) return false;
+    ok = std::fread(t, sizeof *t, 1, f) == 1 && std::memcmp(t->magic, kTrailerMagic, sizeof t->magic) == 0 &&
+         t->digest == dg.final();
+    return ok;
+}
+bool sync_dir_of(const std::string& path) {
+    const size_t slash = path.find_last_of('/');
+    const std::string dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : path.substr(0, slash));
+    const int fd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+    if (fd < 0) return false;
+    const bool r = fsync(fd) == 0;
+    close(fd);
+    return r;
+}
+}  // namespace kme
+
+extern "C" {
+
+kme_status kme_checkpoint_inspect(const char* path, kme_checkpoint_info* out) {
+    if (!path || !out) return KME_E_INVALID;
+    *out = kme_checkpoint_info{};
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return KME_E_INVALID;
+    kme::CkptTrailer t{};
+    bool ok = std::fseek(f, 0, SEEK_END) == 0;
+    const long sz = ok ? std::ftell(f) : -1;
+    ok = ok && sz >= (long)sizeof t && std::fseek(f, sz - (long)sizeof t, SEEK_SET) == 0 && std::fread(&t, sizeof t, 1, f) == 1 &&
+         std::memcmp(t.magic, kme::kTrailerMagic, sizeof t.magic) == 0;
+    std::fclose(f);
+    if (!ok) return KME_E_INVALID;
+    out->file_bytes = (uint64_t)sz;
+    out->app_bytes = t.app_bytes;
+    out->digest = t.digest;
+    return KME_OK;
+}
+
 kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes) {
     if (!e || !path || (app_bytes && !app)) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (e->inflight) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    const DevState& S = e->S;
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
-    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ctr, S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
     // the last epoch faulted: its state is not a checkpoint (an epoch refused with KME_E_UNFUNDED
     // changed nothing: the engine's state is the one before it)
     if (ctr[ci(C_ERR)] != ~0ull && (ctr[ci(C_ERR)] & 0xFF) != KME_E_UNFUNDED) return KME_E_FAILED;
-    CkptHeader h{};
-    std::memcpy(h.magic, kCkptMagic2, sizeof h.magic);
+    const size_t G = e->cfg.max_symbols, A = e->cfg.max_accounts;
+    const bool funded = e->cfg.mode == KME_MODE_FUNDED;
+    CkptHeader3 h{};
+    std::memcpy(h.magic, kCkptMagic3, sizeof h.magic);
     h.cfg = e->cfg;
     h.seq_base = e->seq_base;
-    h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
-    h.otab_used = ctr[ci(C_OTAB_USED)];
-    h.bal_used = ctr[ci(C_BAL_USED)];
-    h.pos_used = ctr[ci(C_POS_USED)];
-    const std::string tmp = std::string(path) + ".tmp";
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) return KME_E_INVALID;
-    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
-    std::vector<char> host;
-    for (const Blob& b : state_blobs(e, h.pool_used)) {
-        if (!ok) break;
-        host.resize(b.bytes);
-        if (b.bytes && hipMemcpy(host.data(), b.dev, b.bytes, hipMemcpyDeviceToHost) != hipSuccess) { ok = false; break; }
-        const uint64_t n = b.bytes;
-        ok = std::fwrite(&n, sizeof n, 1, f) == 1 && (n == 0 || std::fwrite(host.data(), 1, n, f) == n);
+    h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], S.pool_cap);
+    h.app_bytes = app_bytes;
+    // the compact stores on the device first: the set levels (counted from the group bitmaps) and
+    // the live ledger entries (counted by k_ledger_live), into scratch of exactly that size
+    std::vector<GroupState> grp(G);
+    HIP_TRY(hipMemcpy(grp.data(), S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
+    uint64_t nlev = 0;
+    for (const GroupState& gs : grp)
+        nlev += (uint64_t)(__builtin_popcountll(gs.bm0_lsb) + __builtin_popcountll(gs.bm0_msb) + __builtin_popcountll(gs.bm1_lsb) +
+                           __builtin_popcountll(gs.bm1_msb));
+    unsigned long long live[2] = {0, 0}, cnt[3] = {0, 0, 0};
+    if (e->ledger) {
+        launch_ledger_live(S, e->d_maint, e->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(live, e->d_maint, sizeof live, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
     }
-    const uint64_t an = app_bytes;
-    ok = ok && std::fwrite(&an, sizeof an, 1, f) == 1 && (an == 0 || std::fwrite(app, 1, an, f) == an);
-    ok = std::fflush(f) == 0 && ok;
-    ok = fsync(fileno(f)) == 0 && ok;
-    ok = std::fclose(f) == 0 && ok;
-    ok = ok && std::rename(tmp.c_str(), path) == 0;
-    if (!ok) std::remove(tmp.c_str());
+    Level* d_lev = nullptr;
+    void *d_bal = nullptr, *d_pos = nullptr;
+    bool ok = hipMalloc((void**)&d_lev, std::max<uint64_t>(nlev, 1) * sizeof(Level)) == hipSuccess &&
+              hipMalloc(&d_bal, std::max<uint64_t>(live[0], 1) * 16) == hipSuccess &&
+              hipMalloc(&d_pos, std::max<uint64_t>(live[1], 1) * 32) == hipSuccess;
+    if (ok) {
+        launch_ckpt_levels(S, d_lev, e->d_maint, e->stream);
+        if (e->ledger) launch_ckpt_ledger(S, d_bal, d_pos, e->d_maint + 1, e->stream);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(cnt, e->d_maint, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+             hipStreamSynchronize(e->stream) == hipSuccess;
+        if (!e->ledger) cnt[1] = cnt[2] = 0;
+        ok = ok && cnt[0] == nlev && cnt[1] == live[0] && cnt[2] == live[1];
+    }
+    (void)hipGetLastError();
+    h.n_levels = cnt[0];
+    h.bal_live = cnt[1];
+    h.pos_live = cnt[2];
+    std::vector<char> stage;
+    {
+        kme::CkptWriter w(path);
+        ok = ok && w.write(&h, sizeof h);
+        ok = ok && w.write(grp.data(), G * sizeof(GroupState));
+        ok = ok && put_dev(w, d_lev, h.n_levels * sizeof(Level), stage);
+        ok = ok && put_dev(w, S.pool, h.pool_used * sizeof(Node), stage);
+        if (funded) {
+            ok = ok && put_dev(w, S.acct_since, A * sizeof(int64_t), stage);
+            ok = ok && put_dev(w, S.acct_lb, A * sizeof(int64_t), stage);
+            ok = ok && put_dev(w, S.acct_demand, A * sizeof(int64_t), stage);
+        }
+        if (e->ledger) {
+            ok = ok && put_dev(w, d_bal, h.bal_live * 16, stage);
+            ok = ok && put_dev(w, d_pos, h.pos_live * 32, stage);
+        }
+        ok = ok && w.write(app, app_bytes);
+        ok = ok && w.commit(app_bytes, nullptr);
+    }
+    (void)hipFree(d_lev);
+    if (d_bal) (void)hipFree(d_bal);
+    if (d_pos) (void)hipFree(d_pos);
     return ok ? KME_OK : KME_E_INVALID;
 }
 
@@ -1046,88 +1318,153 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     if (e->inflight) return KME_E_INVALID;
     if (app_bytes) *app_bytes = 0;
     HIP_TRY(hipSetDevice(e->device));
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return KME_E_INVALID;
-    CkptHeader h{};
-    bool ok = std::fread(&h, sizeof h, 1, f) == 1;
-    const bool v2 = ok && std::memcmp(h.magic, kCkptMagic2, sizeof h.magic) == 0;
-    ok = ok && (v2 || std::memcmp(h.magic, kCkptMagic, sizeof h.magic) == 0);
-    // the same store geometry (device, stream and timing choices may differ; max_epoch sizes the
-    // oid table, whose blob size is checked below)
+    kme::CkptReader r(path);
+    CkptHeader3 h{};
+    bool ok = r.read(&h, sizeof h) && std::memcmp(h.magic, kCkptMagic3, sizeof h.magic) == 0;
+    // the same store geometry (device, stream, timing and the ledger tables' initial size may differ)
     ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
          h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
-         h.cfg.max_resting == e->cfg.max_resting && h.cfg.ledger_capacity == e->cfg.ledger_capacity &&
+         h.cfg.max_resting == e->cfg.max_resting && h.cfg.max_epoch == e->cfg.max_epoch &&
          h.cfg.credit_shards == e->cfg.credit_shards && h.cfg.flags == e->cfg.flags &&
-         h.pool_used <= e->S.pool_cap;
-    // the whole file is read and checked before anything reaches the device: a mismatched or
-    // truncated checkpoint leaves the engine untouched
-    const std::vector<Blob> blobs = ok ? state_blobs(e, h.pool_used) : std::vector<Blob>{};
-    if (ok && v2) {   // the record's size first (it follows the blobs): a buffer too small costs no read of the state
-        long off = (long)sizeof h;
-        for (const Blob& b : blobs) off += (long)(sizeof(uint64_t) + b.bytes);
-        uint64_t an = 0;
-        ok = std::fseek(f, off, SEEK_SET) == 0 && std::fread(&an, sizeof an, 1, f) == 1 && an < (1ull << 40);
-        if (ok && app_bytes) *app_bytes = (size_t)an;
-        if (ok && (an > app_cap || (an && !app))) { std::fclose(f); return KME_E_CAPACITY; }
-        ok = ok && std::fseek(f, (long)sizeof h, SEEK_SET) == 0;
-    }
-    std::vector<std::vector<char>> host(blobs.size());
-    for (size_t k = 0; ok && k < blobs.size(); ++k) {
-        uint64_t n = 0;
-        ok = std::fread(&n, sizeof n, 1, f) == 1 && n == blobs[k].bytes;
-        if (!ok) break;
-        host[k].resize(n);
-        ok = n == 0 || std::fread(host[k].data(), 1, n, f) == n;
-    }
-    std::vector<char> rec;
-    if (ok && v2) {
-        uint64_t an = 0;
-        ok = std::fread(&an, sizeof an, 1, f) == 1 && an < (1ull << 40);
-        if (ok) {
-            rec.resize(an);
-            ok = an == 0 || std::fread(rec.data(), 1, an, f) == an;
-        }
-    }
-    ok = ok && std::fgetc(f) == EOF;   // nothing after the last blob
-    std::fclose(f);
+         h.pool_used <= e->S.pool_cap && h.n_levels <= (uint64_t)e->cfg.max_symbols * 2 * NLEV &&
+         h.app_bytes < (1ull << 40) && h.bal_live < (1ull << 31) && h.pos_live < (1ull << 31) &&
+         (e->ledger || (h.bal_live == 0 && h.pos_live == 0));
+    if (ok && app_bytes) *app_bytes = (size_t)h.app_bytes;
+    if (ok && (h.app_bytes > app_cap || (h.app_bytes && !app))) return KME_E_CAPACITY;   // nothing else read
+    // the whole file is read and its digest checked before anything reaches the device: a mismatched,
+    // truncated or corrupted checkpoint leaves the engine untouched
+    const size_t G = e->cfg.max_symbols, A = e->cfg.max_accounts;
+    const bool funded = e->cfg.mode == KME_MODE_FUNDED;
+    std::vector<char> grp, lev, pool, acct, bal, pos, rec;
+    auto take = [&](std::vector<char>& v, uint64_t n) {
+        if (!ok) return;
+        v.resize(n);
+        ok = r.read(v.data(), n);
+    };
+    take(grp, G * sizeof(GroupState));
+    take(lev, h.n_levels * sizeof(Level));
+    take(pool, h.pool_used * sizeof(Node));
+    if (funded) take(acct, 3 * A * sizeof(int64_t));
+    take(bal, h.bal_live * 16);
+    take(pos, h.pos_live * 32);
+    take(rec, h.app_bytes);
+    kme::CkptTrailer t{};
+    ok = ok && r.verify(&t) && t.app_bytes == h.app_bytes;
     if (!ok) {
         if (app_bytes) *app_bytes = 0;
         return KME_E_INVALID;
     }
-    if (app_bytes) *app_bytes = rec.size();
-    // from here on a failure leaves a mix of old and restored state: the engine is dead
-    for (size_t k = 0; k < blobs.size(); ++k) {
-        if (hipMemcpy(blobs[k].dev, host[k].data(), blobs[k].bytes, hipMemcpyHostToDevice) != hipSuccess) {
-            e->failed = 1; e->fail_status = KME_E_HIP; e->fail_detail = KME_D_NONE;
-            return KME_E_HIP;
+    // ledger tables large enough for the live entries and two epochs (a fresh engine's may be smaller)
+    DevState& S = e->S;
+    if (e->ledger) {
+        const uint64_t nb = ledger_slots(h.bal_live, bal_bound(e->cfg), 2), np = ledger_slots(h.pos_live, pos_bound(e->cfg), 2);
+        if (nb > (1ull << 31) || np > (1ull << 31)) return KME_E_CAPACITY;
+        if (nb > (uint64_t)S.bal_mask + 1) {
+            uint32_t* st = nullptr; int64_t *k = nullptr, *v = nullptr;
+            if (hipMalloc((void**)&st, nb * 4) != hipSuccess || hipMalloc((void**)&k, nb * 8) != hipSuccess ||
+                hipMalloc((void**)&v, nb * 8) != hipSuccess) {
+                (void)hipGetLastError(); (void)hipFree(st); (void)hipFree(k); (void)hipFree(v);
+                return KME_E_CAPACITY;
+            }
+            dfree(e, S.bal_state); dfree(e, S.bal_key); dfree(e, S.bal_val);
+            e->allocs.push_back(st); e->allocs.push_back(k); e->allocs.push_back(v);
+            S.bal_state = st; S.bal_key = k; S.bal_val = v;
+            S.bal_mask = (uint32_t)(nb - 1);
+        }
+        if (np > (uint64_t)S.pos_mask + 1) {
+            PosEntry* p = nullptr;
+            if (hipMalloc((void**)&p, np * sizeof(PosEntry)) != hipSuccess) { (void)hipGetLastError(); return KME_E_CAPACITY; }
+            dfree(e, S.pos);
+            e->allocs.push_back(p);
+            S.pos = p;
+            S.pos_mask = (uint32_t)(np - 1);
         }
     }
+    // from here on a failure leaves a mix of old and restored state: the engine is dead
+    auto dead = [&](kme_status s) {
+        e->failed = 1; e->fail_status = s; e->fail_detail = KME_D_NONE;
+        return s;
+    };
+    hipStream_t st = e->stream;
+    void *d_lev = nullptr, *d_bal = nullptr, *d_pos = nullptr;
+    bool dok = hipMemcpy(S.grp, grp.data(), grp.size(), hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemsetAsync(S.lev, 0, G * 2 * NLEV * sizeof(Level), st) == hipSuccess &&
+               hipMalloc(&d_lev, std::max<size_t>(lev.size(), 16)) == hipSuccess &&
+               hipMemcpy(d_lev, lev.data(), lev.size(), hipMemcpyHostToDevice) == hipSuccess &&
+               (pool.empty() || hipMemcpy(S.pool, pool.data(), pool.size(), hipMemcpyHostToDevice) == hipSuccess);
+    if (dok) launch_rst_levels(S, (const Level*)d_lev, (uint32_t)h.n_levels, st);
+    if (dok && funded) {
+        const int64_t* a = reinterpret_cast<const int64_t*>(acct.data());
+        dok = hipMemcpy(S.acct_since, a, A * 8, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(S.acct_lb, a + A, A * 8, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(S.acct_demand, a + 2 * A, A * 8, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    unsigned long long fail = 0;
+    if (dok && e->ledger) {
+        dok = hipMemsetAsync(S.bal_state, 0, ((size_t)S.bal_mask + 1) * sizeof(uint32_t), st) == hipSuccess &&
+              hipMemsetAsync(S.pos, 0, ((size_t)S.pos_mask + 1) * sizeof(PosEntry), st) == hipSuccess &&
+              hipMalloc(&d_bal, std::max<size_t>(bal.size(), 16)) == hipSuccess &&
+              hipMalloc(&d_pos, std::max<size_t>(pos.size(), 16)) == hipSuccess &&
+              hipMemcpy(d_bal, bal.data(), bal.size(), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_pos, pos.data(), pos.size(), hipMemcpyHostToDevice) == hipSuccess;
+        if (dok) {
+            launch_rst_ledger(S, d_bal, (uint32_t)h.bal_live, d_pos, (uint32_t)h.pos_live, e->d_maint, st);
+            dok = hipMemcpyAsync(&fail, e->d_maint, sizeof fail, hipMemcpyDeviceToHost, st) == hipSuccess;
+        }
+    }
+    // the oid table from the resting orders of the used pool prefix
+    if (dok) launch_otab_rebuild(S, (uint32_t)h.pool_used, st);
+    dok = dok && hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+    if (d_lev) (void)hipFree(d_lev);
+    if (d_bal) (void)hipFree(d_bal);
+    if (d_pos) (void)hipFree(d_pos);
+    if (!dok) return dead(KME_E_HIP);
+    if (fail) return dead(KME_E_CAPACITY);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
-    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (hipMemcpy(ctr, S.ctr, sizeof ctr, hipMemcpyDeviceToHost) != hipSuccess) return dead(KME_E_HIP);
+    if (ctr[ci(C_REBUILD_FAIL)] != 0 || ctr[ci(C_OTAB_USED)] * 4 > e->otab_cap * 3) return dead(KME_E_CAPACITY);
     ctr[ci(C_POOL_BUMP)] = h.pool_used;
-    ctr[ci(C_OTAB_USED)] = h.otab_used;
-    ctr[ci(C_BAL_USED)] = h.bal_used;
-    ctr[ci(C_POS_USED)] = h.pos_used;
+    ctr[ci(C_BAL_USED)] = h.bal_live;
+    ctr[ci(C_POS_USED)] = h.pos_live;
+    ctr[ci(C_ERR)] = ~0ull;
     {   // a restored book may hold size-0 makers: then the fast segments stay off (C_SIZE0)
-        const Node* nodes = reinterpret_cast<const Node*>(host[2].data());
+        const Node* nodes = reinterpret_cast<const Node*>(pool.data());
         ctr[ci(C_SIZE0)] = 0;
         for (uint64_t k = 0; k < h.pool_used; ++k)
             if (nodes[k].live && nodes[k].size == 0) { ctr[ci(C_SIZE0)] = 1; break; }
     }
-    HIP_TRY(hipMemcpy(e->S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
+    if (hipMemcpy(S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_S, &e->S, sizeof(DevState), hipMemcpyHostToDevice) != hipSuccess)
+        return dead(KME_E_HIP);
     e->seq_base = h.seq_base;
-    if (rec.size()) std::memcpy(app, rec.data(), rec.size());
+    if (!rec.empty()) std::memcpy(app, rec.data(), rec.size());
     return KME_OK;
 }
 
 kme_status kme_restore(kme_engine* e, const char* path) {
     size_t n = 0;
     kme_status s = kme_restore_app(e, path, nullptr, 0, &n);
-    if (s == KME_E_CAPACITY) {   // (an application record this caller does not want)
+    if (s == KME_E_CAPACITY && n) {   // (an application record this caller does not want)
         std::vector<char> sink(n);
         s = kme_restore_app(e, path, sink.data(), sink.size(), &n);
     }
     return s;
+}
+
+kme_status kme_ledger_stats(kme_engine* e, kme_ledger_info* out) {
+    if (!e || !out) return KME_E_INVALID;
+    *out = kme_ledger_info{};
+    if (!e->ledger) return KME_E_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long ctr[C_NCTR * CTR_STRIDE];
+    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    out->bal_slots = (uint64_t)e->S.bal_mask + 1;
+    out->pos_slots = (uint64_t)e->S.pos_mask + 1;
+    out->bal_used = ctr[ci(C_BAL_USED)];
+    out->pos_used = ctr[ci(C_POS_USED)];
+    out->grows = e->ledger_grows;
+    return KME_OK;
 }
 
 kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,
@@ -1399,19 +1736,19 @@ kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
     if (e->cfg.mode != KME_MODE_EXACT && !e->S.ledger_replay) return KME_E_UNSUPPORTED;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    const size_t lc = (size_t)e->S.bal_mask + 1;
-    std::vector<uint32_t> bst(lc);
-    std::vector<int64_t> bk(lc), bv(lc);
-    std::vector<PosEntry> pos(lc);
-    HIP_TRY(hipMemcpy(bst.data(), e->S.bal_state, lc * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(bk.data(), e->S.bal_key, lc * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(bv.data(), e->S.bal_val, lc * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(pos.data(), e->S.pos, lc * sizeof(PosEntry), hipMemcpyDeviceToHost));
+    const size_t lb = (size_t)e->S.bal_mask + 1, lp = (size_t)e->S.pos_mask + 1;
+    std::vector<uint32_t> bst(lb);
+    std::vector<int64_t> bk(lb), bv(lb);
+    std::vector<PosEntry> pos(lp);
+    HIP_TRY(hipMemcpy(bst.data(), e->S.bal_state, lb * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(bk.data(), e->S.bal_key, lb * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(bv.data(), e->S.bal_val, lb * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(pos.data(), e->S.pos, lp * sizeof(PosEntry), hipMemcpyDeviceToHost));
     std::vector<std::pair<int64_t, int64_t>> bal;
-    for (size_t h = 0; h < lc; ++h) if (bst[h] == 1) bal.push_back({bk[h], bv[h]});
+    for (size_t h = 0; h < lb; ++h) if (bst[h] == 1) bal.push_back({bk[h], bv[h]});
     std::sort(bal.begin(), bal.end());
     std::vector<PosEntry> ps;
-    for (size_t h = 0; h < lc; ++h) if (pos[h].state == 1) ps.push_back(pos[h]);
+    for (size_t h = 0; h < lp; ++h) if (pos[h].state == 1) ps.push_back(pos[h]);
     std::sort(ps.begin(), ps.end(), [](const PosEntry& a, const PosEntry& b) { return a.k0 != b.k0 ? a.k0 < b.k0 : a.k1 < b.k1; });
     std::string out;
     char line[256];

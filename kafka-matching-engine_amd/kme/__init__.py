@@ -61,6 +61,15 @@ class kme_epoch_status(C.Structure):
                 ("ledger_serial", C.c_uint32)]
 
 
+class kme_checkpoint_info(C.Structure):
+    _fields_ = [("file_bytes", C.c_uint64), ("app_bytes", C.c_uint64), ("digest", C.c_uint64)]
+
+
+class kme_ledger_info(C.Structure):
+    _fields_ = [("bal_slots", C.c_uint64), ("pos_slots", C.c_uint64), ("bal_used", C.c_uint64),
+                ("pos_used", C.c_uint64), ("grows", C.c_uint32), ("_pad", C.c_uint32)]
+
+
 FORWARD_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t)
 COMMIT_FN = C.CFUNCTYPE(None, C.c_void_p)
 
@@ -69,12 +78,12 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_top_of_book_groups", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_checkpoint_app", "kme_restore_app", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
+    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_checkpoint_app", "kme_restore_app", "kme_checkpoint_inspect", "kme_ledger_stats", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
     "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_expand_rows_mt", "kme_build_id",
-    "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
+    "kme_rccl_load", "kme_rccl_last_error", "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
     "kme_credit_adjust", "kme_credit_rebalance",
     "kme_multi_create", "kme_multi_destroy", "kme_multi_submit_epoch_host", "kme_multi_poll", "kme_multi_wait",
     "kme_multi_checkpoint_app", "kme_multi_restore_app", "kme_multi_engine",
@@ -125,6 +134,8 @@ def lib():
         "kme_restore": (st, [vp, C.c_char_p]),
         "kme_checkpoint_app": (st, [vp, C.c_char_p, vp, C.c_size_t]),
         "kme_restore_app": (st, [vp, C.c_char_p, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
+        "kme_checkpoint_inspect": (st, [C.c_char_p, C.POINTER(kme_checkpoint_info)]),
+        "kme_ledger_stats": (st, [vp, C.POINTER(kme_ledger_info)]),
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
         "kme_shard_of": (u32, [i64, u32]),
@@ -151,6 +162,8 @@ def lib():
         "kme_expand_rows_mt": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                     C.POINTER(C.c_size_t), u32]),
         "kme_build_id": (C.c_char_p, []),
+        "kme_rccl_load": (st, [C.c_char_p]),
+        "kme_rccl_last_error": (C.c_char_p, []),
         "kme_comm_unique_id": (st, [vp]),
         "kme_comm_init": (st, [vp, u32, u32, vp, C.POINTER(vp)]),
         "kme_comm_destroy": (st, [vp]),
@@ -430,6 +443,14 @@ class Engine:
             raise KmeError(rc, "kme_restore_app")
         return b""
 
+    def ledger_stats(self) -> dict:
+        """kme_ledger_stats: the exact ledger's table sizes, slots in use and rehashes so far."""
+        info = kme_ledger_info()
+        rc = self._L.kme_ledger_stats(self._h, C.byref(info))
+        if rc:
+            raise KmeError(rc, "kme_ledger_stats")
+        return {k: int(getattr(info, k)) for k in ("bal_slots", "pos_slots", "bal_used", "pos_used", "grows")}
+
     def tape_json_device_into(self, ptrs: dict, n: int, out_ptr: int, cap: int) -> int:
         """kme_tape_json_device into a caller device buffer; returns the text length (nothing is
         written when it exceeds cap)."""
@@ -465,12 +486,31 @@ class Engine:
         return self._text(self._L.kme_snapshot_ledger)
 
 
+def rccl_load(path: str | None = None):
+    """kme_rccl_load: the RCCL the kme_comm_* calls use (None: env KME_RCCL_LIB, else librccl.so.1)."""
+    rc = lib().kme_rccl_load(path.encode() if path else None)
+    if rc:
+        raise KmeError(rc, f"kme_rccl_load({path}): {rccl_last_error()}")
+
+
+def rccl_last_error() -> str:
+    return (lib().kme_rccl_last_error() or b"").decode()
+
+
+def torch_rccl_path() -> str | None:
+    """The RCCL torch's collectives use (its wheel's own copy), if there is one."""
+    import torch
+
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
 def comm_unique_id() -> bytes:
     """kme_comm_unique_id: 128 bytes for kme_comm_init, made on one rank and sent to all."""
     buf = C.create_string_buffer(128)
     rc = lib().kme_comm_unique_id(buf)
     if rc:
-        raise KmeError(rc, "kme_comm_unique_id")
+        raise KmeError(rc, f"kme_comm_unique_id: {rccl_last_error()}")
     return buf.raw
 
 
@@ -483,19 +523,19 @@ class Comm:
         b = C.create_string_buffer(bytes(uid), 128)
         rc = self._L.kme_comm_init(eng.handle, n_ranks, rank, b, C.byref(h))
         if rc:
-            raise KmeError(rc, "kme_comm_init")
+            raise KmeError(rc, f"kme_comm_init: {rccl_last_error()}")
         self._h = h
 
     def market_data_allgather(self, groups_ptr: int, n_groups: int, rows_per_rank: int, dev_all_ptr: int):
         rc = self._L.kme_market_data_allgather(self.eng.handle, self._h, C.c_void_p(int(groups_ptr)), n_groups,
                                                rows_per_rank, C.c_void_p(int(dev_all_ptr)))
         if rc:
-            raise KmeError(rc, "kme_market_data_allgather")
+            raise KmeError(rc, f"kme_market_data_allgather: {rccl_last_error()}")
 
     def credit_rebalance(self):
         rc = self._L.kme_credit_rebalance(self.eng.handle, self._h)
         if rc:
-            raise KmeError(rc, "kme_credit_rebalance")
+            raise KmeError(rc, f"kme_credit_rebalance: {rccl_last_error()}")
 
     def close(self):
         if getattr(self, "_h", None):
@@ -554,6 +594,15 @@ class Processor:
 
     def tape_text(self) -> str:
         return "".join(f"{k} {v}\n" for k, v in self.records)
+
+
+def checkpoint_inspect(path) -> dict:
+    """kme_checkpoint_inspect: (file_bytes, app_bytes, digest) from a checkpoint file's trailer."""
+    info = kme_checkpoint_info()
+    rc = lib().kme_checkpoint_inspect(str(path).encode(), C.byref(info))
+    if rc:
+        raise KmeError(rc, "kme_checkpoint_inspect")
+    return {"file_bytes": int(info.file_bytes), "app_bytes": int(info.app_bytes), "digest": int(info.digest)}
 
 
 def order_from_json(value: str):

@@ -108,7 +108,7 @@ def _lib():
     lib.Java_GpuMatchingEngine_buffer.restype = P
     lib.Java_GpuMatchingEngine_forwarded.argtypes = [P, P, L, I]
     lib.Java_GpuMatchingEngine_forwarded.restype = None
-    lib.Java_GpuMatchingEngine_checkpoint.argtypes = [P, P, L, P, L]
+    lib.Java_GpuMatchingEngine_checkpoint.argtypes = [P, P, L, P, L, L, P]
     lib.Java_GpuMatchingEngine_checkpoint.restype = I
     lib.Java_GpuMatchingEngine_restore.argtypes = [P, P, L, P, P]
     lib.Java_GpuMatchingEngine_restore.restype = I
@@ -274,14 +274,21 @@ def test_jni_forwards_the_records_before_a_fault(oracle_mod):
     lib.Java_GpuMatchingEngine_destroy(j.env, None, h)
 
 
+class IllegalState(Exception):
+    """java.lang.IllegalStateException thrown by the processor (the stream thread dies)."""
+
+
 class JavaProcessor:
     """GpuMatchingEngine.java statement for statement (init / process / flush / completeOldest /
     forwardReady / punctuate / commitPoint / close) over the JNI glue.  Each record carries its Kafka
     offset (context.offset()); forwarded rows are collected in `out`; commit_point() is the commit
-    hook's StateStore.flush(), which Kafka Streams calls before it commits the consumed offsets."""
+    hook's StateStore.flush(), which Kafka Streams calls before it commits the consumed offsets.
+    `commit_log` is the changelogged commit-log store (a dict that survives the process: Kafka
+    Streams restores it from its changelog wherever the task runs)."""
 
-    def __init__(self, lib, j, path, epoch, max_trades, create_args):
+    def __init__(self, lib, j, path, epoch, max_trades, create_args, commit_log=None):
         self.lib, self.j, self.path, self.epoch = lib, j, str(path), epoch
+        self.commit_log = {} if commit_log is None else commit_log
         self.h = lib.Java_GpuMatchingEngine_create(j.env, None, *create_args)
         assert self.h and not j.thrown, j.thrown
         self.cols, self.rows = slot_views(lib, j, self.h)
@@ -289,12 +296,18 @@ class JavaProcessor:
         self.ready, self.ready_rows = [], [0, 0]
         self.ready_status = [j.arr(np.zeros(4, np.int64)) for _ in range(2)]
         self.last_offset = self.skip_through = self.checkpointed = -1
+        self.generation = 0
         self.out = []
+        want = self.commit_log.get("checkpoint")          # (generation, offset, bytes, digest)
         if os.path.exists(self.path):
-            r = j.arr(np.zeros(6, np.int64))
+            r = j.arr(np.zeros(9, np.int64))
             rc = lib.Java_GpuMatchingEngine_restore(j.env, None, self.h, _jstr(j, self.path), r)
-            assert rc == 0, rc
+            if rc != 0:
+                self._fail(f"kme restore: {rc}")
             o = j.objs[r]
+            if want is not None and (o[6] < want[0] or (o[6] == want[0] and (o[7] != want[2] or o[8] != want[3]))):
+                self._fail(f"checkpoint generation {o[6]} is not the committed one {want}")
+            self.generation = int(o[6])
             self.skip_through = self.checkpointed = self.last_offset = int(o[0])
             for k in range(int(o[1])):
                 s = int(o[2 + 2 * k])
@@ -302,6 +315,14 @@ class JavaProcessor:
                 j.objs[self.ready_status[s]][:] = 0
                 self.busy[s] = True
                 self.ready.append(s)
+        elif want is not None:
+            self._fail(f"the commit log names checkpoint generation {want[0]} but {self.path} is missing")
+
+    def _fail(self, msg):
+        """init() throws; the task is torn down (close -> destroy)."""
+        self.lib.Java_GpuMatchingEngine_destroy(self.j.env, None, self.h)
+        self.h = 0
+        raise IllegalState(msg)
 
     def process(self, offset, rec):
         self.forward_ready()
@@ -369,8 +390,14 @@ class JavaProcessor:
         self.flush()
         while self.inflight > 0:
             self.complete_oldest(False)
-        rc = self.lib.Java_GpuMatchingEngine_checkpoint(self.j.env, None, self.h, _jstr(self.j, self.path), self.last_offset)
+        info = self.j.arr(np.zeros(2, np.int64))
+        rc = self.lib.Java_GpuMatchingEngine_checkpoint(self.j.env, None, self.h, _jstr(self.j, self.path), self.last_offset,
+                                                        self.generation + 1, info)
         assert rc == 0, rc
+        self.generation += 1
+        fb, dg = (int(x) for x in self.j.objs[info])
+        assert fb == os.path.getsize(self.path)
+        self.commit_log["checkpoint"] = (self.generation, self.last_offset, fb, dg)
         self.checkpointed = self.last_offset
 
     def close(self):
@@ -425,7 +452,8 @@ def test_crash_after_commit_restarts_without_losing_output(oracle_mod, tmp_path,
         args = (0, 8, epoch, 1 << 14, max_trades, 0, 0, 0, 1, 1 << 16)
     n = len(orders)
     ckpt = tmp_path / "kme-0_0.ckpt"
-    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    log = {}
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
     c0, c1, crash_at = int(n * 0.3) + 17, int(n * 0.55) + 5, int(n * 0.8) + 3
     committed = {}
     for k in range(crash_at):
@@ -438,8 +466,8 @@ def test_crash_after_commit_restarts_without_losing_output(oracle_mod, tmp_path,
             assert p.ready or p.count[p.fill] == 0
     first = p.rows_out()
     p.crash()
-    q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
-    assert q.skip_through == c1
+    q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
+    assert q.skip_through == c1 and q.generation == 2
     start = (c1 if redeliver == "committed" else c0) + 1
     for k in range(start, n):
         q.process(k, _records(orders, k))
@@ -492,7 +520,7 @@ def test_checkpoint_of_another_processor_is_refused(kme_mod, tmp_path):
                                                 ledger_capacity=1 << 12))
     bare = tmp_path / "bare.ckpt"
     eng.checkpoint(str(bare))
-    r = j.arr(np.zeros(6, np.int64))
+    r = j.arr(np.zeros(9, np.int64))
     assert lib.Java_GpuMatchingEngine_restore(j.env, None, h, _jstr(j, str(bare)), r) == 1     # KME_E_INVALID
     other = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=17, max_epoch=1 << 10,
                                                   max_resting=1 << 12, max_trades=1 << 12, max_accounts=16))
@@ -543,7 +571,7 @@ def test_multi_gpu_drop_in_equals_the_single_partition_tape(oracle_mod, tmp_path
         _drive(p, orders, c1 + 1, crash_at)
         first = p.rows_out()
         p.crash()
-        q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+        q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, p.commit_log)
         assert q.skip_through == c1
         _drive(q, orders, c1 + 1, n)
         q.close()
@@ -587,3 +615,83 @@ def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, r
     o = oracle_mod.Oracle()
     o.process(orders)
     _cmp_fields(_as_tape(p.rows_out(), oracle_mod.REC_DTYPE), o.tape())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("damage", ["missing", "stale", "foreign"])
+def test_restart_refuses_a_checkpoint_the_commit_log_does_not_name(oracle_mod, tmp_path, damage):
+    """Round-4 verdict: a commit point that cannot diverge silently.  Each commit point logs (generation,
+    offset, size, digest) of its checkpoint to the changelogged commit log; a restart whose file is
+    missing (task moved without its state directory), older (a stale copy) or another file of the same
+    generation fails the processor loudly instead of starting from an empty or wrong book at a committed
+    offset.  A file newer than the log's record is taken (the crash fell between the file's rename and
+    the changelog write)."""
+    import shutil
+
+    lib = _lib()
+    j = FakeJni()
+    setup = W.funded_setup(64, range(1, 17))
+    orders = W.Orders.concat([setup, W.uniform(20_000, n_symbols=16, n_accounts=64, seed=41)])
+    epoch, max_trades = 1 << 11, 1 << 13
+    args = (1, 17, epoch, 1 << 15, max_trades, 64, 3, 0, 1, 1 << 12)
+    ckpt = tmp_path / "kme-0_1.ckpt"
+    log = {}
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
+    n = len(orders)
+    _drive(p, orders, 0, n // 3)
+    p.commit_point()
+    shutil.copy(ckpt, tmp_path / "gen1.ckpt")
+    _drive(p, orders, n // 3, 2 * n // 3)
+    p.commit_point()
+    assert log["checkpoint"][0] == 2
+    p.crash()
+    if damage == "missing":
+        os.remove(ckpt)
+    elif damage == "stale":
+        shutil.copy(tmp_path / "gen1.ckpt", ckpt)
+    else:   # a file of the same generation written by another run: same name, other content
+        other = JavaProcessor(lib, j, tmp_path / "other.ckpt", epoch, max_trades, args, {})
+        _drive(other, orders, 0, n // 3)
+        other.commit_point()
+        _drive(other, orders, n // 3, n // 2)
+        other.commit_point()
+        other.crash()
+        shutil.copy(tmp_path / "other.ckpt", ckpt)
+    with pytest.raises(IllegalState):
+        JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
+    # the intact file restarts (control), and a file one generation ahead of the log is taken
+    q = JavaProcessor(lib, j, tmp_path / "gen1.ckpt", epoch, max_trades, args, {"checkpoint": (0, -1, 0, 0)})
+    assert q.generation == 1 and q.skip_through == n // 3 - 1
+    q.crash()
+
+
+@pytest.mark.gpu
+def test_corrupted_checkpoint_is_refused_untouched(kme_mod, oracle_mod, tmp_path):
+    """The digest in a checkpoint's trailer is recomputed over everything a restore reads: one flipped
+    byte in the stores is refused (KME_E_INVALID) before anything reaches the device."""
+    setup = W.funded_setup(32, range(1, 9))
+    part = W.uniform(3000, n_symbols=8, n_accounts=32, seed=6)
+    cfg = kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=9, max_epoch=1 << 12, max_resting=1 << 14,
+                                 max_accounts=32, flags=3)
+    a = kme_mod.Engine(cfg)
+    a.process(setup)
+    a.process(part)
+    ck = tmp_path / "a.ckpt"
+    a.checkpoint_app(str(ck), b"rec")
+    info = kme_mod.checkpoint_inspect(ck)
+    assert info["file_bytes"] == os.path.getsize(ck) and info["app_bytes"] == 3
+    raw = bytearray(ck.read_bytes())
+    raw[len(raw) // 2] ^= 0x40
+    bad = tmp_path / "bad.ckpt"
+    bad.write_bytes(bytes(raw))
+    b = kme_mod.Engine(cfg)
+    b.process(setup)
+    before = b.snapshot_books()
+    with pytest.raises(kme_mod.KmeError) as ke:
+        b.restore_app(str(bad))
+    assert kme_mod.STATUS[ke.value.status] == "INVALID"
+    assert b.snapshot_books() == before
+    assert b.restore_app(str(ck)) == b"rec"
+    assert b.snapshot_books() == a.snapshot_books() and b.snapshot_ledger() == a.snapshot_ledger()
+    a.close()
+    b.close()
