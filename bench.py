@@ -288,6 +288,30 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
                     "two epochs in flight; PCIe- and host-inclusive, not the headline value"}
 
 
+def measure_checkpoint(kme, eng, cfg, directory):
+    """The commit point's cost at this shape: kme_checkpoint_app of the engine's
+    state (format 3: the live stores, a digest trailer; fsync'd and renamed) and its restore into a
+    fresh engine of the same configuration; both books must then agree."""
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, "bench.ckpt")
+    t0 = time.perf_counter()
+    eng.checkpoint_app(path, b"offset")
+    t1 = time.perf_counter()
+    info = kme.checkpoint_inspect(path)
+    other = kme.Engine(cfg)
+    t2 = time.perf_counter()
+    assert other.restore_app(path) == b"offset"
+    t3 = time.perf_counter()
+    same = other.snapshot_books() == eng.snapshot_books()
+    if cfg.flags & 1:
+        same = same and other.snapshot_ledger() == eng.snapshot_ledger()
+    other.close()
+    os.remove(path)
+    return {"file_bytes": info["file_bytes"], "write_ms": (t1 - t0) * 1e3, "restore_ms": (t3 - t2) * 1e3,
+            "restored_state_equal": same,
+            "path": "kme_checkpoint_app (device compaction, D2H, digest, fsync, rename) / kme_restore_app into a new engine"}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,9 +331,17 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline", action="store_true",
                     help="queue epoch k+1 before waiting for epoch k (+1.3% orders/s measured, p99 epoch "
                          "latency 1.9 -> 3.7 ms: an epoch then waits behind the previous one)")
-    ap.add_argument("--host-path-epochs", type=int, default=3,
+    ap.add_argument("--host-path-epochs", type=int, default=-1,
                     help="N = 1: epochs of the host-buffer path (pinned H2D + kernels + D2H, pipelined) "
-                         "measured after the device-resident ones (0 = skip)")
+                         "measured after the device-resident ones (0 = skip; default: 3, or 2^24 records' "
+                         "worth of smaller epochs)")
+    ap.add_argument("--java-defaults", action="store_true",
+                    help="the engine configuration of GpuMatchingEngine() (integration/jni): 65,536-record epochs, "
+                         "max_trades 2^18, 65,537 symbols, 2^20 accounts, 2^26 resting orders, exact ledger + serial "
+                         "fallback, initial ledger capacity 2^20")
+    ap.add_argument("--checkpoint", default="",
+                    help="directory: after the timed epochs, time a commit point's checkpoint (kme_checkpoint_app) "
+                         "of the engine and its restore into a fresh engine; the line gets bytes and ms")
     ap.add_argument("--flags", default="",
                     help="kme_config.flags, comma-separated: exact_ledger, serial_fallback (the drop-in's own "
                          "configuration, GpuMatchingEngine.java: exact_ledger,serial_fallback; N = 1 only)")
@@ -356,7 +388,11 @@ def main():
         assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local_rank)
 
+    if args.java_defaults:
+        args.epoch, args.flags = 1 << 16, "exact_ledger,serial_fallback"
     E = args.epoch
+    if args.host_path_epochs < 0:
+        args.host_path_epochs = max(3, (1 << 24) // E)
     host_epochs = args.host_path_epochs if world == 1 else 0
     # + 1: the phase-breakdown epoch; then the host-path epochs
     total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs) * E)
@@ -378,8 +414,13 @@ def main():
                              max_accounts=nacc, device=local_rank, light_max=args.light_max)
     cfg.credit_shards = shards
     cfg.flags = flags
-    if flags:   # a Positions entry per (account, symbol) filled, none ever removed by a fill (KP:283, H2)
-        cfg.ledger_capacity = args.ledger_capacity or max(1 << 20, total + nacc)
+    if flags:   # the tables' initial size (they grow between epochs: kme_ledger_stats)
+        cfg.ledger_capacity = args.ledger_capacity or (1 << 20)
+    if args.java_defaults:   # GpuMatchingEngine() (integration/jni/GpuMatchingEngine.java)
+        cfg.max_trades, cfg.max_symbols, cfg.max_accounts, cfg.max_resting = 1 << 18, 65537, 1 << 20, 1 << 26
+        cfg.ledger_capacity = 1 << 20
+        if max_sid + 1 > cfg.max_symbols or nacc > cfg.max_accounts:
+            raise SystemExit("bench.py --java-defaults: the workload exceeds GpuMatchingEngine()'s configuration")
     eng = kme.Engine(cfg)
     # one explicit stream for the engine and every torch / collective op of this rank, so they are
     # ordered (the default stream's handle is 0, which would leave the engine on its own
@@ -523,6 +564,8 @@ def main():
     host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, cfg.max_trades) \
         if host_epochs else None
     router = measure_router(stream, E) if world == 1 and host_epochs else None   # (host CPU only)
+    ckpt = measure_checkpoint(kme, eng, cfg, args.checkpoint) if args.checkpoint and world == 1 else None
+    ledger_tables = eng.ledger_stats() if flags & 1 else None
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)
         d = eng.debug_counters().astype(np.float64).reshape(-1)[:12]
@@ -603,7 +646,8 @@ def main():
                        "mode": "FUNDED (symbol groups in parallel)" + (" + exact ledger" if flags & 1 else "")
                                + (" + serial fallback" if flags & 2 else ""),
                        "parallelism": f"symbol-keyed x{world} (murmur2, Kafka's keyed partitioner)",
-                       "credit_shards": shards, "flags": args.flags or "none"},
+                       "credit_shards": shards, "flags": args.flags or "none",
+                       "engine": "GpuMatchingEngine() defaults" if args.java_defaults else "bench"},
             "build_id": build_id,
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),
@@ -618,7 +662,8 @@ def main():
             "phase_ms_last_epoch": {k: round(v, 4) for k, v in phases_all.items()},   # (the epoch after the timed ones)
             "host_path": host_path,
             "router": router,
-            "exact_ledger": ledger if flags & 1 else None,
+            "exact_ledger": dict(ledger, tables=ledger_tables) if flags & 1 else None,
+            "checkpoint": ckpt,
             "match_ms_per_step": [round(v, 3) for v in match_ms],
             "events_per_epoch_rank0": {k: v / args.steps for k, v in mix.items()},
             # cancels that removed a resting order (KP:289-323) / cancels in the timed epochs

@@ -3021,6 +3021,9 @@ constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBL
 #ifndef KME_DIAG_NO_OUT
 #define KME_DIAG_NO_OUT 0       // diagnostic builds only: skip the OUT echo stores of k_match_lanes
 #endif
+#ifndef KME_DIAG_NO_RESTSLOT
+#define KME_DIAG_NO_RESTSLOT 0  // diagnostic builds only: skip k_match_lanes's rest-slot stores
+#endif
 #ifndef KME_DIAG_NO_TRADE
 #define KME_DIAG_NO_TRADE 0     // diagnostic builds only: skip the trade-record stores of k_match_lanes
 #endif
@@ -3281,7 +3284,7 @@ struct GroupLane {
         nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
         nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
         nd[3] = make_int4(p, r.action, 1, 0);
-        S.rest_slot[r.i] = slot;
+        if (!KME_DIAG_NO_RESTSLOT) S.rest_slot[r.i] = slot;
         o.rested = true;
     }
 

@@ -252,7 +252,7 @@ static kme_status route(kme_router* r, const kme_orders* in, uint32_t n, int32_t
     // (3) each directory shard applies its records in arrival order (a BUY/SELL records its
     // partition, a CANCEL takes it; unknown oid: 0), prefetching the probe slots a few ahead
     std::atomic<bool> oom{false};
-    parallel(D, [&](uint32_t d) {
+    auto apply = [&](uint32_t d) {
         Directory& dir = r->dir[d];
         constexpr uint32_t AHEAD = 16;
         const uint32_t a = start[d], b = start[d + 1];
@@ -279,7 +279,14 @@ static kme_status route(kme_router* r, const kme_orders* in, uint32_t n, int32_t
                 sl.val = (uint32_t)it.p;
             }
         }
-    });
+    };
+    // a small batch (kme_multi splits an epoch at its account-record runs: many small calls) applies
+    // the shards inline, with no thread start-up, as passes 1 and 2 do
+    if (T == 1) {
+        for (uint32_t d = 0; d < D; ++d) apply(d);
+    } else {
+        parallel(D, apply);
+    }
     return oom.load() ? KME_E_CAPACITY : KME_OK;
 }
 

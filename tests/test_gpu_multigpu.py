@@ -130,6 +130,8 @@ def test_rebalance_of_a_failed_engine_still_takes_part(kme_mod):
     join the all-gather (else its peers wait forever) and every rank must skip the adjust.  One rank
     here: the call returns KME_E_FAILED instead of returning before the collective, and the
     communicator still works afterwards (a market-data all-gather completes)."""
+    import torch
+
     trccl = kme_mod.torch_rccl_path()
     if trccl:
         kme_mod.rccl_load(trccl)

@@ -59,13 +59,17 @@ def test_c3_uniform_at_scale(kme_mod, oracle_mod):
     _check(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, 0)
 
 
-@pytest.mark.timeout(600)
-def test_c3_bench_stream_at_bench_shape(kme_mod, oracle_mod):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("flags", [0, 3])
+def test_c3_bench_stream_at_bench_shape(kme_mod, oracle_mod, flags):
     """The bench's own C3 stream (bench.make_workload: seed 1000, 65,536 symbols and accounts) in
     its own epoch size, 2^22 records, for six epochs: ~64 records per group per epoch, free-list
     blocks recycled across epochs, and an oid-table rebuild (kme_wait: (used + max_epoch) * 2 >
     capacity) between epochs 5 and 6.  Every epoch's tape is compared in binary (tests/tapes.py)
-    with the oracle's, the books at the end line by line."""
+    with the oracle's, the books at the end line by line.  flags = 3: the drop-in's configuration
+    (KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK, bench.py --flags exact_ledger,serial_fallback),
+    Balances / Positions compared with the oracle's after every epoch, from the default initial
+    ledger size (the tables grow between epochs)."""
     import bench
     import tapes
 
@@ -73,7 +77,7 @@ def test_c3_bench_stream_at_bench_shape(kme_mod, oracle_mod):
     setup, stream, sids, nacc, _, _ = bench.make_workload("c3", n_ep * E22, 0, 1)
     eng = kme_mod.Engine(kme_mod.default_config(kme_mod.MODE_FUNDED, max_symbols=int(sids.max()) + 1, max_epoch=E22,
                                                 max_resting=max_resting, max_trades=2 * E22 + (1 << 16),
-                                                max_accounts=nacc))
+                                                max_accounts=nacc, flags=flags))
     # the oid table's capacity (kme_create) and the epoch after which kme_wait rebuilds it
     pool = max_resting + (int(sids.max()) + 2) * 64
     cap = 1 << (2 * (pool + E22) - 1).bit_length()
@@ -93,6 +97,9 @@ def test_c3_bench_stream_at_bench_shape(kme_mod, oracle_mod):
         d = tapes.first_difference(got, want)
         assert d is None, f"epoch {k}: tape row {d}: got {got[d] if d < len(got) else None} want {want[d] if d < len(want) else None}"
         assert r.status.n_trades > 1_000_000
+        if flags:
+            assert r.status.serial_fallback == 0 and r.status.ledger_serial == 0   # the parallel ledger pass kept it
+            assert eng.snapshot_ledger() == o.dump_ledger(), f"epoch {k}: ledger"
     assert eng.snapshot_books() == o.dump_books()
     eng.close()
 
