@@ -547,6 +547,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     const int32_t a = io.action[i];
     int32_t grp = -1, vlev = 0;
     int64_t tgt = -1;
+    uint32_t vpos = 0;
     S.rest_slot[i] = (a == BUY || a == SELL) ? RS_PENDING : -1;
     io.n_trades[i] = 0;
     if (funded && (a == BUY || a == SELL)) {   // routed by k_emap (acct_ok again: k_acct_refresh)
@@ -582,6 +583,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         const int64_t oid = io.oid[i];
         uint32_t hpos = 0;
         const int64_t t = otab_cancel_target(S, io, oid, i, hpos);
+        if (t <= -2) vpos = hpos;
         if (t <= -2) {
             const uint32_t j = (uint32_t)(-(t + 2));
             const int64_t sj = io.sid[j];
@@ -613,12 +615,15 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
     if (grp >= 0) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
-        // word 6: a cancel's target (a same-epoch order j: -(j + 2), its final slot read from
-        // rest_slot[j]); a FUNDED BUY/SELL's packed record is k_emap's, with its own entry's position
-        // there
+        // word 6: a cancel's target (a same-epoch order j: -(j + 2)); a FUNDED BUY/SELL's packed record
+        // is k_emap's, with its own entry's position there.  Word 1 of a cancel of a same-epoch order:
+        // that order's oid-table entry position instead of the cancel's size (the OUT echo of a cancel
+        // keeps the input's size: k_unsort takes it from the input) -- k_match_lanes reads the entry
+        // the order's rest finalised there, k_match reads rest_slot[j]
         const int32_t w0 = (a & 0xFF) | ((io.price[i] & 0xFF) << 8) | ((acct_ok ? 1 : 0) << 16) | ((io.sid[i] < 0 ? 1 : 0) << 17);
         KG int4* p = &S.prec[2 * (size_t)i];
-        p[0] = make_int4(w0, io.size[i], (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
+        const int32_t w1 = (a == CANCEL && tgt <= -2) ? (int32_t)vpos : io.size[i];
+        p[0] = make_int4(w0, w1, (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
         p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), (int32_t)tgt, vlev);
     }
 }
@@ -3021,9 +3026,6 @@ constexpr int LFS = 16;           // per-lane free-slot stack in LDS (spills FBL
 #ifndef KME_DIAG_NO_OUT
 #define KME_DIAG_NO_OUT 0       // diagnostic builds only: skip the OUT echo stores of k_match_lanes
 #endif
-#ifndef KME_DIAG_NO_RESTSLOT
-#define KME_DIAG_NO_RESTSLOT 0  // diagnostic builds only: skip k_match_lanes's rest-slot stores
-#endif
 #ifndef KME_DIAG_NO_TRADE
 #define KME_DIAG_NO_TRADE 0     // diagnostic builds only: skip the trade-record stores of k_match_lanes
 #endif
@@ -3284,7 +3286,10 @@ struct GroupLane {
         nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
         nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
         nd[3] = make_int4(p, r.action, 1, 0);
-        if (!KME_DIAG_NO_RESTSLOT) S.rest_slot[r.i] = slot;
+        // its oid-table entry (k_emap's pending one: r.tgt of a BUY/SELL is its position) becomes the
+        // rest slot here, one 4-B store -- no rest_slot store and no pass in k_unsort (k_match's
+        // groups store rest_slot, which k_unsort copies)
+        otab_final(S.otab, (int32_t)r.tgt, slot);
         o.rested = true;
     }
 
@@ -3415,8 +3420,11 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                     vslot = (int32_t)r.tgt;
                     const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                     c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
-                } else if (r.tgt <= -2) {
-                    vslot = S.rest_slot[-(r.tgt + 2)];   // final (arrival order); < 0: did not rest
+                } else if (r.tgt <= -2) {   // an order of this epoch (earlier in arrival order, so decided):
+                    // the low word of its oid-table entry (position in the size word, k_route) -- its rest
+                    // slot, or still pending if it did not rest
+                    const uint32_t v = reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)(uint32_t)r.size];
+                    vslot = (v & OT_PENDING) ? -1 : (int32_t)v;
                 }
             }
             if (order) w.request_spare();
@@ -3662,15 +3670,17 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
     const uint32_t lim = err_limit(S.ctr, io.n);          // from a fault on: no trades (trade_off stays in bounds)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t g = S.route_grp[i];
-        {   // k_table's work for a BUY/SELL that rested: its oid-table entry becomes the rest slot
-            // (rest_slot, stored by the matcher).  The entry of one that did not stays pending
-            // (OT_PENDING | i): a reader takes a pending entry only where it names a BUY/SELL of the
-            // epoch it reads in with this oid, a fact either way (otab_cancel_target, k_emap).
-            const int32_t act = io.action[i];
-            if ((act == BUY || act == SELL) && g >= 0 && i < lim) {
-                const int32_t rs = S.rest_slot[i];
+        // k_table's work for a BUY/SELL k_match rested (rest_slot; k_match_lanes finalises its own
+        // orders' entries at the rest): the oid-table entry becomes the rest slot.  The entry of one
+        // that did not rest stays pending (OT_PENDING | i): a reader takes a pending entry only where it
+        // names a BUY/SELL of the epoch it reads in with this oid, a fact either way
+        // (otab_cancel_target, k_emap).
+        const int32_t act = io.action[i];
+        if ((act == BUY || act == SELL) && g >= 0 && i < lim) {
+            const int32_t rs = S.rest_slot[i];
+            if (rs >= 0) {
                 const uint32_t h = S.epos[i];
-                if (rs >= 0 && h != OT_DEAD) otab_final(S.otab, (int32_t)h, rs);
+                if (h != OT_DEAD) otab_final(S.otab, (int32_t)h, rs);
             }
         }
         if (g < 0) continue;
@@ -3678,7 +3688,7 @@ __global__ void __launch_bounds__(256) k_unsort(DevState S, EpochIO io) {
         const int4 a = S.osort[i];
         io.out_action[i] = a.x & 0xFF;
         io.out_flags[i] = (uint8_t)((a.x >> 8) & KME_OUT_HAS_PREV);
-        io.out_size[i] = a.y;
+        io.out_size[i] = act == CANCEL ? io.size[i] : a.y;   // (removeOrder leaves the size, KP:289-333)
         io.out_prev[i] = mk64(a.z, a.w);
         io.n_trades[i] = (uint32_t)a.x >> 9;
     }
