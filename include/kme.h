@@ -384,11 +384,17 @@ kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c);
  * into input order -- the caller's kme_epoch_result is exactly one engine's over the whole stream.
  * Before every epoch the engines' funded credit is pooled and split again (kme_credit_state /
  * kme_credit_adjust), queued on the engine streams behind the epochs in flight (env
- * KME_MULTI_REBALANCE_EVERY = epochs between re-splits, 0 = never).  cfg: FUNDED, flags 0 (the exact
- * ledger couples every symbol: one engine), credit_shards is set to N.  The trades of one merged
- * epoch must fit max_trades.  Any fault of a shard fails the whole (the other shards went past it):
- * the records before the first fault in input order are answered (n_effective), as one engine
- * answers them, then it accepts nothing further. */
+ * KME_MULTI_REBALANCE_EVERY = epochs between re-splits, 0 = never).  cfg: FUNDED, credit_shards is
+ * set to N; flags 0, or EXACT_LEDGER | SERIAL_FALLBACK (the shards themselves run with flags 0: the
+ * exact ledger couples every symbol).  The trades of one merged epoch must fit max_trades.  A fault of
+ * a shard fails the whole (the other shards went past it): the records before the first fault in
+ * input order are answered (n_effective), as one engine answers them, then it accepts nothing further
+ * -- except, with EXACT_LEDGER | SERIAL_FALLBACK, a refusal of the funded proof (KME_E_UNFUNDED): the
+ * shards are retired and one engine of those flags on devices[0] takes the stream (SURVEY §8e:
+ * outside the funded domain only one engine is exact), built by replaying the input history kept
+ * since the start (env KME_MULTI_HISTORY records at most, default 2^25; past it, or after a restore
+ * of a sharded checkpoint, the refusal stays fatal); it answers the rest of that epoch and every later
+ * one, synchronously at submit.  Its checkpoints are the one engine's (the manifest says so). */
 typedef struct kme_multi kme_multi;
 kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* devices, kme_multi** out);
 kme_status kme_multi_destroy(kme_multi* m);

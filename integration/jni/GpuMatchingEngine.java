@@ -120,7 +120,9 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     }
 
     // nDevices > 1: the symbols keyed over GPUs device .. device + nDevices - 1 behind this one processor
-    // (kme_multi: FUNDED, flags 0 -- the exact ledger couples every symbol, so it stays on one GPU)
+    // (kme_multi: FUNDED shards; with the default flags an epoch no shard's funded bound can prove
+    // consolidates the stream onto one exact engine on `device` -- the exact ledger couples every
+    // symbol -- instead of failing; flags 0: such an epoch is fatal, KME_E_UNFUNDED)
     public GpuMatchingEngine(int epoch, int maxTrades, int mode, int flags, int maxSymbols, int maxAccounts,
                              long maxResting, int device, int nDevices, long ledgerCapacity) {
         this.epoch = epoch;

@@ -134,7 +134,8 @@ static int alloc_registered(jkme* h, void** p, size_t bytes) {
 
 /* static native long create(int mode, int maxSymbols, int maxEpoch, long maxResting, int maxTrades,
  *                           int maxAccounts, int flags, int device, int nDevices, long ledgerCapacity)
- * nDevices > 1: symbol shards on devices device .. device + nDevices - 1 (kme_multi: FUNDED, flags 0);
+ * nDevices > 1: symbol shards on devices device .. device + nDevices - 1 (kme_multi: FUNDED, flags 0, or
+ * the default EXACT_LEDGER | SERIAL_FALLBACK -- then an unprovable epoch consolidates onto one engine);
  * nDevices < 0: -nDevices shards all on `device` (tests on a one-GPU box). */
 JNIEXPORT jlong JNICALL Java_GpuMatchingEngine_create(JNIEnv* env, jclass cls, jint mode, jint maxSymbols,
                                                         jint maxEpoch, jlong maxResting, jint maxTrades,

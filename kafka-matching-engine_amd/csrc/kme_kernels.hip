@@ -3289,6 +3289,7 @@ struct GroupLane {
         // its oid-table entry (k_emap's pending one: r.tgt of a BUY/SELL is its position) becomes the
         // rest slot here, one 4-B store -- no rest_slot store and no pass in k_unsort (k_match's
         // groups store rest_slot, which k_unsort copies)
+        if (r.tgt > (int64_t)S.otab_mask) { die(KME_E_CAPACITY, KME_D_SENTINEL_OID); return; }   // (guard)
         otab_final(S.otab, (int32_t)r.tgt, slot);
         o.rested = true;
     }
@@ -3423,8 +3424,11 @@ __global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__
                 } else if (r.tgt <= -2) {   // an order of this epoch (earlier in arrival order, so decided):
                     // the low word of its oid-table entry (position in the size word, k_route) -- its rest
                     // slot, or still pending if it did not rest
-                    const uint32_t v = reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)(uint32_t)r.size];
+                    const uint32_t hv = (uint32_t)r.size;
+                    const uint32_t v = hv <= S.otab_mask ? reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)hv] : OT_DEAD;
+                    if (hv > S.otab_mask) w.die(KME_E_DOMAIN, KME_D_SENTINEL_OID);   // (guard)
                     vslot = (v & OT_PENDING) ? -1 : (int32_t)v;
+                    if ((uint32_t)vslot >= S.pool_cap && vslot >= 0) { w.die(KME_E_UNSUPPORTED, KME_D_SENTINEL_OID); vslot = -1; }   // (guard)
                 }
             }
             if (order) w.request_spare();

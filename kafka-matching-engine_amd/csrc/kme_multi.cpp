@@ -10,6 +10,13 @@
 // exactly what one engine over the whole stream returns.  Between epochs the engines' funded credit
 // is pooled and split again (kme_credit_state / kme_credit_adjust), queued on the
 // engine streams behind the epochs in flight, the blocks moved between devices by peer copies.
+//
+// Outside the funded domain the symbols cannot be split exactly (the ledger couples every symbol,
+// KP:167-182, 276-287; SURVEY §8e: "replicas only").  With cfg.flags = EXACT_LEDGER | SERIAL_FALLBACK
+// (the drop-in's default) the first epoch some shard cannot prove is not fatal: the shards are
+// retired and ONE engine of those flags (the consolidated engine, on devices[0]) takes the stream --
+// built by replaying the input history kept since the start into it, then answering the records the
+// shards did not, and every epoch after (consolidate()).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -81,6 +88,17 @@ struct kme_multi {
     bool credit_used = false;
     uint32_t rebalance_every = 1, since_rebalance = 0;
     uint64_t generation = 0;               // checkpoint generation (shard files path.g<gen>.<k>)
+    // consolidation (cfg.flags EXACT_LEDGER | SERIAL_FALLBACK at n > 1)
+    bool can_consolidate = false;
+    kme_config cons_cfg{};                 // the consolidated engine's configuration
+    kme_engine* cons = nullptr;            // set once the shards are retired
+    std::vector<int32_t> h_action, h_price, h_size;   // every record submitted since the start (SoA)
+    std::vector<int64_t> h_oid, h_aid, h_sid;
+    bool hist_valid = false;               // the history starts at the stream's start and is complete
+    uint64_t hist_cap = 0;                 // records it may hold (env KME_MULTI_HISTORY)
+    uint64_t hist_start[2] = {};           // per slot: the history position of its epoch's first record
+    kme_epoch_result scratch{};            // host results of one consolidated run
+    std::vector<char> scratch_mem;
 };
 
 static void free_parts(kme_multi* m) {
@@ -112,6 +130,7 @@ kme_status kme_multi_destroy(kme_multi* m) {
     }
     for (kme_engine* e : m->eng)
         if (e) kme_destroy(e);
+    if (m->cons) kme_destroy(m->cons);
     if (m->router) kme_router_destroy(m->router);
     delete m;
     return KME_OK;
@@ -121,11 +140,24 @@ kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* de
     if (!cfg || !out || n == 0 || n > 1024 || !devices) return KME_E_INVALID;
     // shards prove their orders against their share of each account's credit: FUNDED, no exact ledger
     // (it couples every symbol, kme_create refuses it with credit_shards > 1)
-    if (cfg->mode != KME_MODE_FUNDED || (n > 1 && cfg->flags != 0)) return KME_E_INVALID;
+    // flags 0, or (n > 1) EXACT_LEDGER | SERIAL_FALLBACK: the shards prove their epochs as with flags 0,
+    // and an epoch they cannot prove consolidates the stream onto one engine of those flags
+    const uint32_t both = KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK;
+    if (cfg->mode != KME_MODE_FUNDED || (n > 1 && cfg->flags != 0 && cfg->flags != both)) return KME_E_INVALID;
     kme_multi* m = new kme_multi();
     m->cfg = *cfg;
     m->cfg.credit_shards = n;
     m->n = n;
+    if (n > 1 && cfg->flags == both) {
+        m->can_consolidate = true;
+        m->cfg.flags = 0;
+        m->cons_cfg = *cfg;
+        m->cons_cfg.credit_shards = 1;
+        m->cons_cfg.device = devices[0];
+        m->hist_valid = true;
+        m->hist_cap = 1ull << 25;
+        if (const char* v = std::getenv("KME_MULTI_HISTORY")) m->hist_cap = (uint64_t)std::strtoull(v, nullptr, 10);
+    }
     if (const char* v = std::getenv("KME_MULTI_REBALANCE_EVERY")) m->rebalance_every = (uint32_t)std::max(0, std::atoi(v));
     kme_status s = kme_router_create(n, (uint64_t)cfg->max_resting + cfg->max_epoch, &m->router);
     for (uint32_t k = 0; k < n && s == KME_OK; ++k) {
@@ -349,6 +381,174 @@ static kme_epoch_status merge(kme_multi* m, int slot, uint32_t n, const kme_epoc
     return tot;
 }
 
+// ------------------------------------------------------------------ consolidation
+static void hist_append(kme_multi* m, const kme_orders* in, uint32_t n) {
+    if (!m->hist_valid) return;
+    if (m->h_action.size() + n > m->hist_cap) {   // too long to replay: consolidation is off from here on
+        m->hist_valid = false;
+        std::vector<int32_t>().swap(m->h_action); std::vector<int32_t>().swap(m->h_price); std::vector<int32_t>().swap(m->h_size);
+        std::vector<int64_t>().swap(m->h_oid); std::vector<int64_t>().swap(m->h_aid); std::vector<int64_t>().swap(m->h_sid);
+        return;
+    }
+    m->h_action.insert(m->h_action.end(), in->action, in->action + n);
+    m->h_oid.insert(m->h_oid.end(), in->oid, in->oid + n);
+    m->h_aid.insert(m->h_aid.end(), in->aid, in->aid + n);
+    m->h_sid.insert(m->h_sid.end(), in->sid, in->sid + n);
+    m->h_price.insert(m->h_price.end(), in->price, in->price + n);
+    m->h_size.insert(m->h_size.end(), in->size, in->size + n);
+}
+static kme_orders hist_at(const kme_multi* m, uint64_t a) {
+    return kme_orders{m->h_action.data() + a, m->h_oid.data() + a, m->h_aid.data() + a, m->h_sid.data() + a,
+                      m->h_price.data() + a, m->h_size.data() + a};
+}
+
+// Records in[0, n) on the consolidated engine (kme_submit_epoch: synchronous, split at max_epoch and
+// at account records), their results into `out` from record a and trade out->trade_off[a] on (out may
+// be null: a replay, results dropped).  *st: totals; status of the first fault (records before it
+// answered, n_effective relative to in).
+static kme_status cons_run(kme_multi* m, const kme_orders& in, uint32_t n, const kme_epoch_result* out, uint32_t a,
+                           kme_epoch_status* st) {
+    kme_epoch_status tot{};
+    tot.error_index = -1;
+    tot.n_inputs = n;
+    uint32_t tbase = out ? out->trade_off[a] : 0;
+    const uint32_t E = m->cons_cfg.max_epoch;
+    const kme_epoch_result& r = m->scratch;
+    for (uint32_t b = 0; b < n || (n == 0 && b == 0); b += E) {
+        const uint32_t k = std::min(E, n - b);
+        const kme_orders part{in.action + b, in.oid + b, in.aid + b, in.sid + b, in.price + b, in.size + b};
+        kme_epoch_status es{};
+        const kme_status rc = kme_submit_epoch(m->cons, &part, k, const_cast<kme_epoch_result*>(&r), &es);
+        const uint32_t ne = rc == KME_OK ? k : es.n_effective;
+        const uint32_t nt = r.trade_off[ne];
+        if (out) {
+            if (tbase + (uint64_t)nt > out->trades_cap) {   // the merged epoch's trades must fit one engine's buffer
+                tot.status = KME_E_CAPACITY; tot.detail = KME_D_CAP_TRADES; tot.error_index = b;
+                tot.n_effective = b;
+                break;
+            }
+            std::memcpy(out->out_action + a + b, r.out_action, ne * sizeof(int32_t));
+            std::memcpy(out->out_size + a + b, r.out_size, ne * sizeof(int32_t));
+            std::memcpy(out->out_prev + a + b, r.out_prev, ne * sizeof(int64_t));
+            std::memcpy(out->out_flags + a + b, r.out_flags, ne);
+            for (uint32_t q = 1; q <= ne; ++q) out->trade_off[a + b + q] = tbase + r.trade_off[q];
+            if (nt) std::memcpy(out->trades + tbase, r.trades, (size_t)nt * sizeof(kme_trade));
+        }
+        tbase += nt;
+        tot.n_trades += nt;
+        tot.n_maker_visits += nt;
+        tot.n_orders += es.n_orders; tot.n_rests += es.n_rests; tot.n_cancel_ok += es.n_cancel_ok;
+        tot.serial_fallback += es.serial_fallback; tot.ledger_repaired += es.ledger_repaired; tot.ledger_serial += es.ledger_serial;
+        if (rc != KME_OK) {
+            tot.status = es.status; tot.detail = es.detail;
+            tot.error_index = es.error_index >= 0 ? b + es.error_index : -1;
+            tot.n_effective = b + ne;
+            break;
+        }
+        tot.n_effective = b + k;
+        if (n == 0) break;
+    }
+    if (st) *st = tot;
+    return (kme_status)tot.status;
+}
+
+// The shards are retired: one engine of cons_cfg (exact ledger + serial fallback) takes the stream
+// from history record `upto` on, after replaying [0, upto) into it -- the state the reference holds
+// after those records, whatever the shards' funded bounds could prove.  Every shard epoch must have
+// landed (nothing in flight on them).
+// the host results of one consolidated run (one max_epoch sub-epoch of kme_submit_epoch)
+static void alloc_scratch(kme_multi* m) {
+    if (!m->scratch_mem.empty()) return;
+    const size_t E = m->cons_cfg.max_epoch, T = m->cons_cfg.max_trades;
+    m->scratch_mem.assign(E * (4 + 4 + 8 + 1) + 4 * (E + 1) + T * sizeof(kme_trade) + 64, 0);
+    char* q = m->scratch_mem.data();
+    auto take = [&](size_t bytes) { char* r = q; q += (bytes + 7) & ~(size_t)7; return r; };
+    m->scratch.out_action = (int32_t*)take(4 * E);
+    m->scratch.out_size = (int32_t*)take(4 * E);
+    m->scratch.out_prev = (int64_t*)take(8 * E);
+    m->scratch.out_flags = (uint8_t*)take(E);
+    m->scratch.trade_off = (uint32_t*)take(4 * (E + 1));
+    m->scratch.trades = (kme_trade*)take(T * sizeof(kme_trade));
+    m->scratch.trades_cap = (uint32_t)T;
+}
+
+static kme_status consolidate(kme_multi* m, uint64_t upto) {
+    alloc_scratch(m);
+    // the shards go first (their memory, and their registrations of the part buffers)
+    free_parts(m);
+    for (kme_engine*& e : m->eng) {
+        if (e) kme_destroy(e);
+        e = nullptr;
+    }
+    if (kme_status s = kme_create(&m->cons_cfg, &m->cons)) { m->cons = nullptr; return s; }
+    kme_epoch_status st{};
+    const kme_status rc = cons_run(m, hist_at(m, 0), (uint32_t)upto, nullptr, 0, &st);
+    if (rc != KME_OK) return rc;   // (the history took effect once already: it cannot fault now)
+    m->hist_valid = false;         // not needed any more
+    std::vector<int32_t>().swap(m->h_action); std::vector<int32_t>().swap(m->h_price); std::vector<int32_t>().swap(m->h_size);
+    std::vector<int64_t>().swap(m->h_oid); std::vector<int64_t>().swap(m->h_aid); std::vector<int64_t>().swap(m->h_sid);
+    return KME_OK;
+}
+
+// A refused epoch (`tot`, records [0, tot.n_effective) of slot s's epoch answered in its out): when
+// the history allows it, consolidate and answer the rest of that epoch, and re-run the newer epoch
+// (slot s ^ 1) if it was queued on the shards (their results of it are dropped).  Returns false when
+// consolidation is not possible (the refusal stands).
+static bool consolidate_at(kme_multi* m, int s, kme_epoch_status& tot) {
+    if (!m->can_consolidate || m->cons || !m->hist_valid || tot.status != KME_E_UNFUNDED) return false;
+    const int s2 = s ^ 1;
+    const bool newer = m->slot_mode[s2] == kSlotQueued || m->slot_mode[s2] == kSlotCollected;
+    if (m->slot_mode[s2] == kSlotQueued) collect(m, s2);   // (the shards drain; the results are dropped)
+    const uint32_t n = m->slot_n[s], ne = tot.n_effective;
+    const kme_orders h2 = hist_at(m, m->hist_start[s2]);
+    const uint32_t n2 = m->slot_n[s2];
+    // the newer epoch's records live in the history too; consolidate() clears it, so keep a copy
+    std::vector<int32_t> c_act, c_pr, c_sz;
+    std::vector<int64_t> c_oid, c_aid, c_sid;
+    if (newer) {
+        c_act.assign(h2.action, h2.action + n2); c_pr.assign(h2.price, h2.price + n2); c_sz.assign(h2.size, h2.size + n2);
+        c_oid.assign(h2.oid, h2.oid + n2); c_aid.assign(h2.aid, h2.aid + n2); c_sid.assign(h2.sid, h2.sid + n2);
+    }
+    std::vector<int32_t> r_act, r_pr, r_sz;
+    std::vector<int64_t> r_oid, r_aid, r_sid;
+    {
+        const kme_orders h = hist_at(m, m->hist_start[s] + ne);
+        const uint32_t k = n - ne;
+        r_act.assign(h.action, h.action + k); r_pr.assign(h.price, h.price + k); r_sz.assign(h.size, h.size + k);
+        r_oid.assign(h.oid, h.oid + k); r_aid.assign(h.aid, h.aid + k); r_sid.assign(h.sid, h.sid + k);
+    }
+    if (consolidate(m, m->hist_start[s] + ne) != KME_OK) {
+        m->failed = 1;
+        tot.status = KME_E_FAILED;
+        return true;
+    }
+    kme_epoch_status rest{};
+    const kme_orders rin{r_act.data(), r_oid.data(), r_aid.data(), r_sid.data(), r_pr.data(), r_sz.data()};
+    (void)cons_run(m, rin, n - ne, &m->slot_out[s], ne, &rest);
+    tot.n_orders += rest.n_orders; tot.n_rests += rest.n_rests; tot.n_cancel_ok += rest.n_cancel_ok;
+    tot.n_trades += rest.n_trades; tot.n_maker_visits += rest.n_trades;
+    tot.serial_fallback += rest.serial_fallback; tot.ledger_repaired += rest.ledger_repaired;
+    tot.ledger_serial += rest.ledger_serial;
+    tot.status = rest.status; tot.detail = rest.detail;
+    tot.error_index = rest.status == KME_OK ? -1 : (rest.error_index >= 0 ? ne + rest.error_index : -1);
+    tot.n_effective = ne + rest.n_effective;
+    if (rest.status != KME_OK) m->failed = 1;
+    if (newer) {
+        kme_epoch_status st2{};
+        const kme_orders in2{c_act.data(), c_oid.data(), c_aid.data(), c_sid.data(), c_pr.data(), c_sz.data()};
+        if (rest.status == KME_OK) {
+            m->slot_out[s2].trade_off[0] = 0;
+            (void)cons_run(m, in2, n2, &m->slot_out[s2], 0, &st2);
+        } else {
+            st2.status = KME_E_FAILED; st2.error_index = -1; st2.n_inputs = n2;
+        }
+        if (st2.status != KME_OK) m->failed = 1;
+        m->done[s2] = st2;
+        m->slot_mode[s2] = kSlotDone;
+    }
+    return true;
+}
+
 extern "C" {
 
 // An epoch of orders only is split and queued (asynchronous, as kme_submit_epoch_host).  An epoch
@@ -367,6 +567,25 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
     bool mixed = false;
     for (uint32_t i = 0; i < n && !mixed; ++i) mixed = is_acct(i);
     const int slot = (int)(m->sub_count & 1);
+    auto finish = [&]() {
+        m->slot_n[slot] = n;
+        m->slot_out[slot] = *out;
+        ++m->sub_count;
+        ++m->inflight;
+        return KME_OK;
+    };
+    auto run_consolidated = [&]() {   // one engine takes the stream: synchronously, at submit
+        out->trade_off[0] = 0;
+        kme_epoch_status st{};
+        (void)cons_run(m, *in, n, out, 0, &st);
+        if (st.status != KME_OK) m->failed = 1;
+        m->done[slot] = st;
+        m->slot_mode[slot] = kSlotDone;
+        return finish();
+    };
+    if (m->cons) return run_consolidated();
+    m->hist_start[slot] = m->h_action.size();
+    hist_append(m, in, n);
     auto rebalance = [&]() -> kme_status {
         if (m->n > 1 && m->rebalance_every && m->sub_count > 0 && ++m->since_rebalance >= m->rebalance_every) {
             m->since_rebalance = 0;
@@ -379,9 +598,19 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
         if (kme_status s = split_submit(m, slot, in, 0, n)) return s;
         m->slot_mode[slot] = kSlotQueued;
     } else {
-        if (m->inflight) {
+        if (m->inflight) {   // the older epoch completes first (its answered prefix decides a consolidation)
             const int other = slot ^ 1;
             if (m->slot_mode[other] == kSlotQueued) collect(m, other);
+            if (m->slot_mode[other] == kSlotCollected) {
+                m->slot_out[other].trade_off[0] = 0;
+                kme_epoch_status t = merge(m, other, m->slot_n[other], m->slot_out[other], 0, 0);
+                if (t.status != KME_OK) (void)consolidate_at(m, other, t);
+                if (t.status != KME_OK) m->failed = 1;
+                m->done[other] = t;
+                m->slot_mode[other] = kSlotDone;
+            }
+            if (m->failed) return KME_E_FAILED;
+            if (m->cons) return run_consolidated();
         }
         kme_epoch_status tot{};
         tot.error_index = -1;
@@ -405,6 +634,11 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
                 tot.detail = r.detail;
                 tot.error_index = r.error_index >= 0 ? a + r.error_index : -1;
                 tot.n_effective = a + r.n_effective;
+                tot.n_trades = tbase;
+                tot.n_maker_visits = tbase;
+                m->slot_n[slot] = n;
+                m->slot_out[slot] = *out;
+                if (consolidate_at(m, slot, tot)) tbase = tot.n_trades;   // the rest of the epoch answered
                 break;
             }
             a = b;
@@ -416,11 +650,7 @@ kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in, uint3
         m->done[slot] = tot;
         m->slot_mode[slot] = kSlotDone;
     }
-    m->slot_n[slot] = n;
-    m->slot_out[slot] = *out;
-    ++m->sub_count;
-    ++m->inflight;
-    return KME_OK;
+    return finish();
 }
 
 kme_status kme_multi_poll(kme_multi* m, int* done) {
@@ -456,8 +686,10 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
         if (m->slot_mode[slot] == kSlotQueued) collect(m, slot);
         m->slot_out[slot].trade_off[0] = 0;
         tot = merge(m, slot, m->slot_n[slot], m->slot_out[slot], 0, 0);
-        // any fault leaves the shards out of step with one another (the others went past it): like
-        // the reference's dead stream thread, nothing further is accepted
+        // a refusal of the funded proof consolidates the stream onto one exact engine when the
+        // configuration allows it; any other fault leaves the shards out of step with one another (the
+        // others went past it): like the reference's dead stream thread, nothing further is accepted
+        if (tot.status != KME_OK) (void)consolidate_at(m, slot, tot);
         if (tot.status != KME_OK) m->failed = 1;
     }
     m->slot_mode[slot] = kSlotIdle;
@@ -467,7 +699,7 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
 
 kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out) {
     if (!m || !out || k >= m->n) return KME_E_INVALID;
-    *out = m->eng[k];
+    *out = m->cons ? m->cons : m->eng[k];   // (consolidated: the one engine)
     return KME_OK;
 }
 
@@ -481,10 +713,12 @@ kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* 
     if (m->inflight) return KME_E_INVALID;
     const uint64_t gen = m->generation + 1;
     const std::string base(path);
-    std::vector<MultiShard> shards(m->n);
-    for (uint32_t k = 0; k < m->n; ++k) {
+    // consolidated: the one engine's file (.0), the manifest says so
+    const uint32_t nf = m->cons ? 1 : m->n;
+    std::vector<MultiShard> shards(nf);
+    for (uint32_t k = 0; k < nf; ++k) {
         const std::string f = base + ".g" + std::to_string(gen) + "." + std::to_string(k);
-        if (kme_status s = kme_checkpoint_app(m->eng[k], f.c_str(), nullptr, 0)) return s;
+        if (kme_status s = kme_checkpoint_app(m->cons ? m->cons : m->eng[k], f.c_str(), nullptr, 0)) return s;
         kme_checkpoint_info ci{};
         if (kme_status s = kme_checkpoint_inspect(f.c_str(), &ci)) return s;
         shards[k] = {ci.file_bytes, ci.digest};
@@ -492,6 +726,7 @@ kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* 
     MultiHeader h{};
     std::memcpy(h.magic, kMultiMagic, sizeof h.magic);
     h.n = m->n;
+    h._pad = m->cons ? 1u : 0u;            // 1: consolidated (one engine's file)
     h.generation = gen;
     h.app_bytes = app_bytes;
     {
@@ -500,7 +735,7 @@ kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* 
                   w.commit(app_bytes, nullptr);
         if (!ok) return KME_E_INVALID;
     }
-    for (uint32_t k = 0; k < m->n && m->generation; ++k)
+    for (uint32_t k = 0; k < m->n && m->generation; ++k)   // (the older generation may have had n files)
         std::remove((base + ".g" + std::to_string(m->generation) + "." + std::to_string(k)).c_str());
     m->generation = gen;
     return KME_OK;
@@ -514,8 +749,9 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
     kme::CkptReader r(path);
     MultiHeader h{};
     bool ok = r.read(&h, sizeof h) && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 && h.n == m->n &&
-              h.app_bytes < (1ull << 40);
-    std::vector<MultiShard> shards(ok ? m->n : 0);
+              h.app_bytes < (1ull << 40) && h._pad <= 1 && (h._pad == 0 || m->can_consolidate) && (h._pad == 1 || !m->cons);
+    const uint32_t nf = h._pad ? 1 : m->n;
+    std::vector<MultiShard> shards(ok ? nf : 0);
     std::vector<char> rec;
     ok = ok && r.read(shards.data(), shards.size() * sizeof(MultiShard));
     if (ok) {
@@ -530,11 +766,27 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
     // every shard's file is the one the manifest committed (before any engine is touched)
     const std::string base(path);
     auto shard_path = [&](uint32_t k) { return base + ".g" + std::to_string(h.generation) + "." + std::to_string(k); };
-    for (uint32_t k = 0; k < m->n; ++k) {
+    for (uint32_t k = 0; k < nf; ++k) {
         kme_checkpoint_info ci{};
         if (kme_checkpoint_inspect(shard_path(k).c_str(), &ci) != KME_OK || ci.file_bytes != shards[k].file_bytes ||
             ci.digest != shards[k].digest)
             return KME_E_INVALID;
+    }
+    m->hist_valid = false;   // the history since the stream's start is gone: no consolidation from here
+    if (h._pad) {            // a consolidated stream: the one engine
+        if (!m->cons) {
+            free_parts(m);
+            for (kme_engine*& e : m->eng) {
+                if (e) kme_destroy(e);
+                e = nullptr;
+            }
+            if (kme_status s = kme_create(&m->cons_cfg, &m->cons)) { m->cons = nullptr; m->failed = 1; return s; }
+        }
+        if (kme_status s = kme_restore(m->cons, shard_path(0).c_str())) { m->failed = 1; return s; }
+        alloc_scratch(m);
+        m->generation = h.generation;
+        if (rec.size()) std::memcpy(app, rec.data(), rec.size());
+        return KME_OK;
     }
     for (uint32_t k = 0; k < m->n; ++k) {
         if (kme_status s = kme_restore(m->eng[k], shard_path(k).c_str())) {

@@ -371,7 +371,7 @@ class JavaProcessor:
             self.lib.Java_GpuMatchingEngine_forwarded(self.j.env, None, self.h, s)
             self.busy[s] = False
             self.count[s] = 0
-            assert self.j.objs[self.ready_status[s]][0] == 0
+            assert self.j.objs[self.ready_status[s]][0] == 0, self.j.objs[self.ready_status[s]]
 
     def punctuate(self):
         self.forward_ready()
@@ -582,15 +582,17 @@ def test_multi_gpu_drop_in_equals_the_single_partition_tape(oracle_mod, tmp_path
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rebalance", [True, False])
-def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, rebalance):
+@pytest.mark.parametrize("rebalance,funding,flags", [(True, 1.5, 0), (False, 1.5, 0), (True, 1.25, 3), (False, 1.25, 3)])
+def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, rebalance, funding, flags):
     """Every account funded with 1.5x its single-engine need over the whole stream, booked as a
     quarter on each of four shards.  The drop-in re-splits the pooled credit before every epoch, so
     every epoch stays provable and the tape is the oracle's; with re-splitting off
     (KME_MULTI_REBALANCE_EVERY=0) some shard's share runs dry and the processor fails (UNFUNDED).
     (A numpy model of the proof over this stream: the static split fails from epoch 6 at 1.5x, the
     re-split holds at 1.5x; at 1.25x the 2^14-record epochs leave too few orders per account and
-    shard for the demand weights to follow, and a few pairs run dry.)"""
+    shard for the demand weights to follow, and a few pairs run dry.)  At 1.25x with the drop-in's
+    default flags (exact ledger + serial fallback) a shard running dry is not fatal: the stream
+    consolidates onto one exact engine and the tape is still the oracle's, re-split or not."""
     monkeypatch.setenv("KME_MULTI_REBALANCE_EVERY", "1" if rebalance else "0")
     lib = _lib()
     j = FakeJni()
@@ -598,14 +600,14 @@ def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, r
     body = W.uniform(8 * E, n_symbols=n_sym, n_accounts=n_acc, seed=77)
     risk = np.where(body.action == W.BUY, body.size.astype(np.int64) * body.price,
                     np.where(body.action == W.SELL, body.size.astype(np.int64) * (100 - body.price.astype(np.int64)), 0))
-    credit = np.floor(np.bincount(body.aid, weights=risk, minlength=n_acc) * 1.5).astype(np.int64)
+    credit = np.floor(np.bincount(body.aid, weights=risk, minlength=n_acc) * funding).astype(np.int64)
     rows = [(W.CREATE_BALANCE, 0, a, 0, 0, 0) for a in range(n_acc)]
     rows += [(W.TRANSFER, 0, a, 0, 0, int(credit[a])) for a in range(n_acc)]
     rows += [(W.ADD_SYMBOL, 0, 0, s, 0, 0) for s in range(1, n_sym + 1)]
     orders = W.Orders.concat([W.Orders.from_rows(rows), body])
-    args = (1, n_sym + 1, E, 1 << 20, 4 * E, n_acc, 0, 0, -4, 1 << 12)
+    args = (1, n_sym + 1, E, 1 << 20, 4 * E, n_acc, flags, 0, -4, 1 << 12)
     p = JavaProcessor(lib, j, tmp_path / "m.ckpt", E, 4 * E, args)
-    if not rebalance:
+    if not rebalance and not flags:
         with pytest.raises(AssertionError):        # a shard's epoch refused: status UNFUNDED in the rows' epoch
             _drive(p, orders, punct=1 << 30)
             p.close()
@@ -695,3 +697,51 @@ def test_corrupted_checkpoint_is_refused_untouched(kme_mod, oracle_mod, tmp_path
     assert b.snapshot_books() == a.snapshot_books() and b.snapshot_ledger() == a.snapshot_ledger()
     a.close()
     b.close()
+
+
+def _exchange_in_domain(n, seed):
+    """exchange_test.js's stream (W.exchange_test) up to its first BUY/SELL priced outside the funded
+    mode's 0..100 (KME_D_FUNDED_RANGE)."""
+    orders = W.exchange_test(n, seed=seed)
+    out = np.nonzero(((orders.action == W.BUY) | (orders.action == W.SELL)) & ((orders.price < 0) | (orders.price > 100)))[0]
+    return orders.slice(0, int(out[0])) if len(out) else orders
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crash", [False, True])
+def test_multi_gpu_drop_in_consolidates_an_unprovable_stream(oracle_mod, tmp_path, crash):
+    """Round-4 verdict (What's missing 2): the drop-in's default flags (exact ledger + serial fallback)
+    at nDevices > 1.  The reference's own harness stream (exchange_test.js: nearly every order is a
+    balance reject, KP:167-182) cannot be proven by any shard's funded bound, so the first epoch that
+    fails the proof consolidates the stream onto one exact engine (the history replayed into it; SURVEY
+    §8e "replicas only") instead of failing with KME_E_UNFUNDED: the MatchOut rows equal the oracle's,
+    and across a commit point, crash and restart from the consolidated checkpoint."""
+    lib = _lib()
+    j = FakeJni()
+    orders = _exchange_in_domain(30_000, seed=13)
+    assert len(orders) > 10_000
+    epoch, max_trades = 1 << 11, 1 << 13
+    args = (1, 8, epoch, 1 << 15, max_trades, 64, 3, 0, -4, 1 << 12)   # FUNDED, exact ledger + fallback, 4 shards
+    ckpt = tmp_path / "cons.ckpt"
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    n = len(orders)
+    if not crash:
+        _drive(p, orders)
+        p.close()
+        got = p.rows_out()
+    else:
+        c1, crash_at = int(n * 0.6) + 7, int(n * 0.8) + 3
+        _drive(p, orders, 0, c1 + 1)
+        p.commit_point()
+        F = sum(len(x) for x in p.out)
+        _drive(p, orders, c1 + 1, crash_at)
+        first = p.rows_out()
+        p.crash()
+        q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, p.commit_log)
+        assert q.skip_through == c1
+        _drive(q, orders, c1 + 1, n)
+        q.close()
+        got = np.concatenate([first[:F], q.rows_out()])
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
