@@ -200,8 +200,11 @@ KDEV int32_t otab_lookup(const DevState& S, int64_t oid) {
     return -1;
 }
 // removeOrder's orders.get(oid) at input i (KP:290): an order of this epoch submitted before i
-// (returns -(j + 2)), else a resting order's slot, else -1.
-KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oid, uint32_t i, uint32_t& pos) {
+// (returns -(j + 2)), else a resting order's slot, else -1.  What the caller needs of the target comes
+// with the check that finds it, one round trip per probe: a resting order's whole node (nd), an
+// order of this epoch's sid and price (jsid, jprice).
+KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oid, uint32_t i, uint32_t& pos, Node& nd,
+                                int64_t& jsid, int32_t& jprice) {
     const uint32_t fp = oid_fp(oid);
     uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
     for (uint32_t probes = 0; probes <= S.otab_mask; ++probes) {
@@ -211,9 +214,16 @@ KDEV int64_t otab_cancel_target(const DevState& S, const EpochIO& io, int64_t oi
         if ((uint32_t)(e >> 32) == fp && v != OT_DEAD) {
             if (v & OT_PENDING) {   // (possibly an earlier epoch's: it counts only as a fact of this one)
                 const uint32_t j = v & ~OT_PENDING;
-                if (j < i && io.oid[j] == oid && (io.action[j] == BUY || io.action[j] == SELL)) { pos = h; return -((int64_t)j + 2); }
-            } else if (S.pool[v].live && S.pool[v].oid == oid) {
-                return (int64_t)v;
+                if (j < i) {
+                    const int64_t joid = io.oid[j];
+                    const int32_t ja = io.action[j];
+                    jsid = io.sid[j];
+                    jprice = io.price[j];
+                    if (joid == oid && (ja == BUY || ja == SELL)) { pos = h; return -((int64_t)j + 2); }
+                }
+            } else if (v < S.pool_cap) {
+                nd = S.pool[v];
+                if (nd.live && nd.oid == oid) return (int64_t)v;
             }
         }
         h = (h + 1) & S.otab_mask;
@@ -582,19 +592,20 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
         // fetches the node and its level in one step (checked against the node there)
         const int64_t oid = io.oid[i];
         uint32_t hpos = 0;
-        const int64_t t = otab_cancel_target(S, io, oid, i, hpos);
+        Node nd;
+        int64_t sj = 0;
+        int32_t pj = 0;
+        const int64_t t = otab_cancel_target(S, io, oid, i, hpos, nd, sj, pj);
         if (t <= -2) vpos = hpos;
         if (t <= -2) {
             const uint32_t j = (uint32_t)(-(t + 2));
-            const int64_t sj = io.sid[j];
             const int32_t gj = group_of(sj, S.G);
             if (gj >= 0) {
                 grp = gj; tgt = t;
                 const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
-                vlev = (io.price[j] & 0xFF) | (side << 8) | (1 << 9);
+                vlev = (pj & 0xFF) | (side << 8) | (1 << 9);
             }
         } else if (t >= 0) {
-            const Node nd = S.pool[t];
             grp = nd.group; tgt = t;
             const int side = (nd.sid != 0 && ((nd.sid < 0) != (nd.action != BUY))) ? 1 : 0;
             vlev = (nd.price & 0xFF) | (side << 8) | (1 << 9);

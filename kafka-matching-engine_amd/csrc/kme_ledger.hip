@@ -295,14 +295,30 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 
 // ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
 // (the ops themselves were gathered into sorted order by the sort's last pass: lsrt)
+// lseg[a] = the number of sorted ops of accounts below a, for a in [0, A]: a merge of the accounts
+// 0..A with the ops' accounts, LSEG_ITEMS merged items per thread (a merge-path search for the
+// thread's start, then a sequential walk).  Per op, a loop over the accounts up to the next op's
+// was one thread's serial tail when the ops name a few of many accounts (the last op's thread
+// walked to A: 13 ms at A = 2^20 with 65,536 accounts in use).
+constexpr uint32_t LSEG_ITEMS = 16;
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > n || n == 0) return;      // (no ops: lseg stays zero)
+    const uint64_t na = (uint64_t)S.A + 1, tot = na + n;
+    const uint64_t d = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * LSEG_ITEMS;
+    if (d >= tot) return;
     const KG uint32_t* K = skeys(S);
-    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
-    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
-    for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
+    const uint32_t hb = S.lhbits;
+    // i accounts and d - i ops come first: account m precedes op j iff aid(op j) >= m
+    uint64_t lo = d > n ? d - n : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)(K[d - 1 - mid] >> hb) >= mid) lo = mid + 1; else hi = mid;
+    }
+    uint64_t i = lo, j = d - lo;
+    for (uint32_t s = 0; s < LSEG_ITEMS && i + j < tot; ++s) {
+        if (j < n && (i >= na || (uint64_t)(K[j] >> hb) < i)) ++j;
+        else { S.lseg[i] = (uint32_t)j; ++i; }
+    }
 }
 
 // ---------------------------------------------------------------- 3. chains: one thread per sorted op
@@ -703,7 +719,6 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
     (void)hipMemsetAsync(S.lposc, 0, sizeof(unsigned long long) * LPOSC_LINES * CTR_STRIDE, st);
     // (lvw_meta and lxmark of the epoch's ops are cleared by k_lgen: the ops fill [0, count) exactly)
-    (void)hipMemsetAsync(S.lseg, 0, sizeof(uint32_t) * ((size_t)S.A + 2), st);
     (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
     (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
     if (n == 0) return;
@@ -725,7 +740,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.n_dev = S.lctr + ci(LC_OPS);
     R.passes = S.lpasses;
     launch_radix(R, st);
-    hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lseg, dim3(cdiv(cdiv((uint64_t)S.A + 1 + nops, LSEG_ITEMS), 256)), dim3(256), 0, st, S);
     // grid of k_lchains / k_linsert: more blocks (their work per thread is a chain of dependent loads:
     // more threads in flight hide it; 8,192 -> 32,768 blocks: k_lchains 0.52 -> 0.42 ms).
     // KME_LEDGER_GRID: A/B runs.
