@@ -99,20 +99,22 @@ static_assert(sizeof(PosEntry) == 64, "PosEntry");
 
 // kme_ledger.hip: one position chain of an epoch (the ops on Positions key (aid, sid)), stored at the
 // sorted position of its first op (aid -1 there: that op is not a chain's first)
-struct alignas(16) LChain {
-    int64_t sid;
-    int64_t ia, iv;                // the entry at the epoch's start (ipres)
+struct alignas(64) LChain {         // one 64-byte line: the head's store is one whole-line write
     int64_t fa, fv;                // after the chain's last effect (fpres)
     int64_t delta;                 // the balance change of its effects
     uint64_t late;                 // (1 + arrival number) << 32 | op position of the latest value write
                                    // into it after its last effect (0: none)
+    int32_t sid, aid;
     uint32_t last_seq;             // arrival number of its last effect
     uint32_t dirty;                // in the repair rounds' run list (a value write into it preceded one of its reads)
     uint32_t rix;                  // 1 + the coupling list index of its first incoming value write (this round)
-    int32_t aid, islot;            // islot: the entry's table slot at the start (-1: absent)
-    uint8_t ipres, fpres, _p[2];
+    int32_t islot;                 // the entry's table slot at the start (its value there then: the chain's
+                                   // start state, unchanged until k_lcommit); absent (ipres 0): the first
+                                   // free slot of its probe sequence (-1: none), fst that slot's state
+    uint8_t ipres, fpres, fst, _p;
+    uint32_t _pad;
 };
-static_assert(sizeof(LChain) == 80, "LChain");
+static_assert(sizeof(LChain) == 64, "LChain");
 // One ledger effect of the epoch (kme_ledger.hip): checkBalance, a fill, or postRemoveAdjustments on
 // the position (aid, sid) -- the account is the op's sort key -- with its arrival number.  FUNDED
 // sids are symbol groups (|sid| < max_symbols < 2^30) and prices 0..126, so both fit narrow fields.
@@ -125,7 +127,7 @@ struct LOp {
 };
 static_assert(sizeof(LOp) == 16 && offsetof(LOp, price) == 12 && offsetof(LOp, flags) == 14, "LOp (k_lgen packs it)");
 // the ledger pass's counters (DevState::lctr, one line each)
-enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_N = 8 };
+enum LCtr : int { LC_OPS = 0, LC_DIRTY, LC_CROSS, LC_FALLBACK, LC_REPAIRED, LC_CHG, LC_DONE, LC_GAPS, LC_N = 8 };
 
 // Counters block: one u64 per 128-byte line (ci(k) = word index), so that atomics on different
 // counters never contend for one L2 line.
@@ -229,6 +231,7 @@ struct DevState {
     KG uint32_t* lvw_meta;            //   kind | writer chain << 2
     KG int32_t* lvw_tgt;              //   the chain it writes into (-1: none)
     KG uint32_t* lseg;                // per account: its first sorted op
+    KG uint4* lgap;                   // k_lseg: account gaps longer than LSEG_RUN (first, last, op position)
     KG int64_t* ldelta;               // per account: the epoch's balance change
     KG ulonglong4* lvk;               // value-key table: hash, 1 + latest arrival, key
     KG uint32_t* lx;                  // couplings: the ops whose value writes go into chains that read later

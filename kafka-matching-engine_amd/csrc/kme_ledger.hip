@@ -51,6 +51,10 @@ namespace {
 constexpr uint32_t OP_CHECK = 0u, OP_FILL = 1u, OP_CANCEL = 2u;   // LOp::flags & 3 (bit 2: buy / bought)
 constexpr uint32_t VW_PUT = 1u, VW_DEL = 2u;
 constexpr int32_t VT_NONE = -1, VT_INSERT = -2;     // lvw_tgt: into no chain of the epoch / a winner to create
+// a winner to create whose key's first free slot (state 0 or 2) is known: -(3 + 2 slot + (state == 2))
+KDEV int32_t vt_insert(int32_t free, uint32_t fst) {
+    return free >= 0 && free < (1 << 29) ? -(3 + 2 * free + (fst == 2 ? 1 : 0)) : VT_INSERT;
+}
 
 KDEV uint32_t lkey_of(const DevState& S, int64_t aid, int64_t sid) {
     return (uint32_t)aid << S.lhbits | (uint32_t)(mix64((uint64_t)sid ^ 0x632be59bd9b4e019ull) >> (64 - S.lhbits));
@@ -72,11 +76,16 @@ KDEV uint32_t pos_hash(const DevState& S, int64_t k0, int64_t k1) {
 }
 // positions.get(UUID(k0, k1)): the slot of a live entry, or -1.  The ledger pass never inserts and
 // reads the table in one kernel (updates in place and deletes in k_lcommit, inserts in k_linsert), so
-// plain loads see every earlier kernel's writes.
-KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
+// plain loads see every earlier kernel's writes.  For an absent key also the first free slot (empty or
+// tombstone) of its probe sequence and that slot's state then (free = -1: none) -- where its insert
+// will go unless another key's takes it first (k_linsert tries it before probing again: one claim
+// instead of a probe and a claim).
+KDEV int32_t pos_lookup_free(const DevState& S, int64_t k0, int64_t k1, int32_t& free, uint32_t& fst) {
     uint32_t h = pos_hash(S, k0, k1);
+    free = -1; fst = 0;
     for (uint32_t p = 0; p <= S.pos_mask; ++p) {
         const uint32_t st = S.pos[h].state;
+        if (st != 1 && free < 0) { free = (int32_t)h; fst = st; }
         if (st == 0) return -1;
         if (st == 1 && S.pos[h].k0 == k0 && S.pos[h].k1 == k1) return (int32_t)h;
         h = (h + 1) & S.pos_mask;
@@ -84,9 +93,14 @@ KDEV int32_t pos_lookup(const DevState& S, int64_t k0, int64_t k1) {
     return -1;
 }
 // positions.put of a key known to be absent (k_linsert: every key inserted by one thread, no reader
-// in the kernel): the first free slot (empty or tombstone) of its probe sequence, claimed by CAS.
+// in the kernel): the first free slot (empty or tombstone) of its probe sequence, claimed by CAS --
+// first at `hint` (pos_lookup_free's slot, in state hst), then along the probe sequence.
 // Returns 1 when it took an empty slot (the table's load grows), 0 for a tombstone, -1: no room.
-KDEV int pos_insert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1) {
+KDEV int pos_insert(const DevState& S, int64_t k0, int64_t k1, int64_t v0, int64_t v1, int32_t hint = -1, uint32_t hst = 0) {
+    if (hint >= 0 && atomicCAS((unsigned int*)&S.pos[hint].state, hst, 1u) == hst) {
+        S.pos[hint].k0 = k0; S.pos[hint].k1 = k1; S.pos[hint].v0 = v0; S.pos[hint].v1 = v1;
+        return hst == 0 ? 1 : 0;
+    }
     uint32_t h = pos_hash(S, k0, k1);
     for (uint32_t p = 0; p <= S.pos_mask; ++p) {
         const uint32_t st = S.pos[h].state;
@@ -295,29 +309,31 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 
 // ---------------------------------------------------------------- 2. accounts' ranges of the sorted ops
 // (the ops themselves were gathered into sorted order by the sort's last pass: lsrt)
-// lseg[a] = the number of sorted ops of accounts below a, for a in [0, A]: a merge of the accounts
-// 0..A with the ops' accounts, LSEG_ITEMS merged items per thread (a merge-path search for the
-// thread's start, then a sequential walk).  Per op, a loop over the accounts up to the next op's
-// was one thread's serial tail when the ops name a few of many accounts (the last op's thread
-// walked to A: 13 ms at A = 2^20 with 65,536 accounts in use).
-constexpr uint32_t LSEG_ITEMS = 16;
+// lseg[a] = the number of sorted ops of accounts below a, for a in [0, A]: thread k (an op, or k = n)
+// writes k for the accounts after op k - 1's up to op k's.  A gap longer than LSEG_RUN accounts goes
+// to a list that k_lseg_gaps fills a workgroup per gap: one thread walking it was the serial tail when
+// the ops name a few of many accounts (the last op's thread walked to A: 13 ms per epoch at A = 2^20
+// with 65,536 accounts in use).
+constexpr uint32_t LSEG_RUN = 256;
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
-    const uint64_t na = (uint64_t)S.A + 1, tot = na + n;
-    const uint64_t d = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * LSEG_ITEMS;
-    if (d >= tot) return;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > n) return;
     const KG uint32_t* K = skeys(S);
-    const uint32_t hb = S.lhbits;
-    // i accounts and d - i ops come first: account m precedes op j iff aid(op j) >= m
-    uint64_t lo = d > n ? d - n : 0, hi = d < na ? d : na;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if ((uint64_t)(K[d - 1 - mid] >> hb) >= mid) lo = mid + 1; else hi = mid;
+    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
+    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
+    if (cur - prev <= (int64_t)LSEG_RUN) {
+        for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
+    } else {
+        const unsigned long long x = atomicAdd(lc(S, LC_GAPS), 1ull);   // < (A + 1) / LSEG_RUN + 1 entries
+        S.lgap[x] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
     }
-    uint64_t i = lo, j = d - lo;
-    for (uint32_t s = 0; s < LSEG_ITEMS && i + j < tot; ++s) {
-        if (j < n && (i >= na || (uint64_t)(K[j] >> hb) < i)) ++j;
-        else { S.lseg[i] = (uint32_t)j; ++i; }
+}
+__global__ void __launch_bounds__(256) k_lseg_gaps(DevState S) {
+    const uint32_t ng = (uint32_t)__hip_atomic_load(lc(S, LC_GAPS), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t x = blockIdx.x; x < ng; x += gridDim.x) {
+        const uint4 g = S.lgap[x];
+        for (uint32_t a = g.x + threadIdx.x; a <= g.y; a += blockDim.x) S.lseg[a] = g.z;
     }
 }
 
@@ -345,14 +361,16 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
             for (uint32_t p = j; p > 0 && K[p - 1] == bj; --p)
                 if (S.lsrt[p - 1].sid == sid) { head = false; break; }
             if (head) {
-                LChain c;                        // built in registers, stored as five 16-B writes
-                const int32_t slot = pos_lookup(S, aid, sid);
+                LChain c;                        // built in registers, stored as four 16-B writes (one line)
+                int32_t free;
+                uint32_t fst;
+                const int32_t slot = pos_lookup_free(S, aid, sid, free, fst);
                 PState P;
                 P.present = slot >= 0;
                 P.a = P.present ? S.pos[slot].v0 : 0;
                 P.v = P.present ? S.pos[slot].v1 : 0;
-                c.sid = sid; c.aid = (int32_t)aid; c.islot = slot;
-                c.ipres = P.present ? 1 : 0; c.ia = P.a; c.iv = P.v;
+                c.sid = sid; c.aid = (int32_t)aid; c.islot = slot >= 0 ? slot : free;
+                c.ipres = P.present ? 1 : 0;
                 uint32_t last = 0;
                 for (uint32_t p = j; p < no && K[p] == bj; ++p) {
                     const LOp op = S.lsrt[p];
@@ -367,7 +385,7 @@ __global__ void __launch_bounds__(256) k_lchains(DevState S) {
                 }
                 c.fpres = P.present ? 1 : 0; c.fa = P.a; c.fv = P.v;
                 c.delta = cd; c.last_seq = last; c.late = 0; c.rix = 0; c.dirty = 0;   // (the array persists across epochs)
-                c._p[0] = c._p[1] = 0;
+                c.fst = slot >= 0 ? 0 : (uint8_t)fst; c._p = 0; c._pad = 0;
                 const uint4* src = reinterpret_cast<const uint4*>(&c);
                 KG uint4* dst = reinterpret_cast<KG uint4*>(&S.lchain[j]);
 #pragma unroll
@@ -465,9 +483,10 @@ KDEV void lr_run_chain(const DevState& S, uint32_t head) {
         in[k] = e;
     }
     __hip_atomic_store(&c.rix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t sid = (int32_t)c.sid;
+    const int32_t sid = c.sid;
     const int64_t aid = c.aid;
-    PState P{c.ia, c.iv, c.ipres != 0};
+    PState P{0, 0, c.ipres != 0};                 // the start state: the entry at islot (unchanged until k_lcommit)
+    if (P.present) { P.a = S.pos[c.islot].v0; P.v = S.pos[c.islot].v1; }
     int64_t cd = 0;
     int q = 0;
     for (uint32_t p = head; p < no && K[p] == K[head]; ++p) {
@@ -644,13 +663,15 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         const long4 w = S.lvw[p];
         const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
         if (v < 0 || S.lvk[v].y != (unsigned long long)S.lsrt[p].es + 1) continue;
-        const int32_t h = pos_lookup(S, w.x, w.y);
+        int32_t free;
+        uint32_t fst;
+        const int32_t h = pos_lookup_free(S, w.x, w.y, free, fst);
         if ((meta & 3u) == VW_DEL) {
             if (h >= 0) S.pos[h].state = 2u;
         } else if (h >= 0) {
             S.pos[h].v0 = w.z; S.pos[h].v1 = w.w;
         } else {
-            S.lvw_tgt[p] = VT_INSERT;
+            S.lvw_tgt[p] = vt_insert(free, fst);
         }
     }
     // every chain's final entry (its own last state, or a later value write into it)
@@ -660,7 +681,7 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         if (!c.ipres) continue;
         int64_t fa, fv;
         const bool fp = chain_final(S, c, fa, fv);
-        if (fp && fa == c.ia && fv == c.iv) continue;
+        if (fp && fa == S.pos[c.islot].v0 && fv == S.pos[c.islot].v1) continue;
         if (fp) { S.pos[c.islot].v0 = fa; S.pos[c.islot].v1 = fv; }
         else S.pos[c.islot].state = 2u;
     }
@@ -674,9 +695,11 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
     bool full = false;
     const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t p = t0; p < no; p += stride) {
-        if (!(S.lvw_meta[p] & 3u) || S.lvw_tgt[p] != VT_INSERT) continue;
+        const int32_t tgt = S.lvw_tgt[p];
+        if (!(S.lvw_meta[p] & 3u) || tgt > VT_INSERT) continue;
         const long4 w = S.lvw[p];
-        const int r = pos_insert(S, w.x, w.y, w.z, w.w);
+        const int32_t hint = tgt == VT_INSERT ? -1 : (-(tgt + 3)) >> 1;
+        const int r = pos_insert(S, w.x, w.y, w.z, w.w, hint, (uint32_t)(-(tgt + 3)) & 1u ? 2u : 0u);
         full |= r < 0;
         grew += r > 0;
     }
@@ -686,7 +709,7 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
         if (c.ipres) continue;
         int64_t fa, fv;
         if (!chain_final(S, c, fa, fv)) continue;
-        const int r = pos_insert(S, (int64_t)c.aid, c.sid, fa, fv);
+        const int r = pos_insert(S, (int64_t)c.aid, c.sid, fa, fv, c.islot, c.fst);
         full |= r < 0;
         grew += r > 0;
     }
@@ -740,7 +763,8 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.n_dev = S.lctr + ci(LC_OPS);
     R.passes = S.lpasses;
     launch_radix(R, st);
-    hipLaunchKernelGGL(k_lseg, dim3(cdiv(cdiv((uint64_t)S.A + 1 + nops, LSEG_ITEMS), 256)), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lseg_gaps, dim3(std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024)), dim3(256), 0, st, S);
     // grid of k_lchains / k_linsert: more blocks (their work per thread is a chain of dependent loads:
     // more threads in flight hide it; 8,192 -> 32,768 blocks: k_lchains 0.52 -> 0.42 ms).
     // KME_LEDGER_GRID: A/B runs.
