@@ -11,9 +11,12 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
-#include <algorithm>
 
 #include "kme.h"
 
@@ -106,6 +109,78 @@ kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_res
     return KME_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Workers kme_expand_rows_mt hands its record ranges to: created once (per process, on first use)
+// and parked on a condition variable between calls.  Starting threads per call cost ~0.5 ms per
+// 65,536-record epoch (the drop-in's default), most of its expand time.  One call at a time uses the
+// pool; a concurrent caller (another engine's completion) starts threads of its own as before.
+struct ExpandPool {
+    std::mutex use;                          // held by the call using the pool
+    std::mutex m;                            // everything below; tasks are picked under it
+    std::condition_variable wake, done;
+    std::vector<std::thread> th;
+    uint64_t gen = 0;                        // one generation per call
+    uint32_t ntask = 0, next = 0, nleft = 0;
+    const kme_orders* in = nullptr;
+    const kme_epoch_result* r = nullptr;
+    kme_row* rows = nullptr;
+    uint32_t n = 0;
+    // take the call's tasks until none is left (a task: its record range, read under the lock)
+    void drain() {
+        for (;;) {
+            uint32_t a, b;
+            const kme_orders* tin;
+            const kme_epoch_result* tr;
+            kme_row* tw;
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (next >= ntask) return;
+                const uint32_t t = next++;
+                a = (uint32_t)((uint64_t)n * t / ntask); b = (uint32_t)((uint64_t)n * (t + 1) / ntask);
+                tin = in; tr = r;
+                tw = rows + 2 * (size_t)a + 2 * (size_t)(r->trade_off[a] - r->trade_off[0]);
+            }
+            expand_range(tin, a, b, tr, tw);
+            std::lock_guard<std::mutex> g(m);
+            if (--nleft == 0) done.notify_all();
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(m);
+                wake.wait(g, [&] { return gen != seen; });
+                seen = gen;
+            }
+            drain();
+        }
+    }
+    void run(const kme_orders* in_, uint32_t n_, const kme_epoch_result* r_, kme_row* rows_, uint32_t T) {
+        while (th.size() + 1 < T) { th.emplace_back([this] { worker(); }); th.back().detach(); }
+        {
+            std::lock_guard<std::mutex> g(m);
+            in = in_; n = n_; r = r_; rows = rows_;
+            ntask = T; next = 0; nleft = T;
+            ++gen;
+        }
+        wake.notify_all();
+        drain();
+        std::unique_lock<std::mutex> g(m);
+        done.wait(g, [&] { return nleft == 0; });
+        ntask = 0;                           // (a late worker finds nothing to take)
+    }
+};
+ExpandPool& expand_pool() {
+    static ExpandPool* p = new ExpandPool;   // (never destroyed: its detached workers outlive static teardown)
+    return *p;
+}
+}  // namespace
+
+extern "C" {
+
 kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
                               size_t* n_rows, uint32_t n_threads) {
     if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
@@ -115,6 +190,12 @@ kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_
     uint32_t T = n_threads ? n_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     T = std::min<uint32_t>(std::min<uint32_t>(T, 64), std::max<uint32_t>(1, n / 4096));   // >= 4,096 records each
     if (T <= 1) { expand_range(in, 0, n, r, rows); return KME_OK; }
+    ExpandPool& pool = expand_pool();
+    if (pool.use.try_lock()) {
+        pool.run(in, n, r, rows, T);
+        pool.use.unlock();
+        return KME_OK;
+    }
     std::vector<std::thread> th;
     th.reserve(T - 1);
     for (uint32_t t = 0; t < T; ++t) {

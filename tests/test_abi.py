@@ -217,3 +217,39 @@ def test_expand_rows_threads_equal_one_thread(kme_mod, threads):
     many = kme_mod.expand_rows(orders, res, threads=threads)
     assert len(one) == 2 * n + 2 * int(off[-1])
     assert one.tobytes() == many.tobytes()
+
+
+def test_expand_rows_pool_under_concurrent_calls(kme_mod):
+    """kme_expand_rows_mt's persistent workers: back-to-back calls and calls from several host threads
+    at once (one uses the pool, the others start threads of their own) give kme_expand_rows's rows."""
+    import threading
+
+    import numpy as np
+
+    from kme import workloads as W
+
+    n = 40_000
+    rng = np.random.Generator(np.random.PCG64(11))
+    orders = W.uniform(n, n_symbols=64, n_accounts=128, seed=11)
+    counts = np.where(rng.random(n) < 0.4, rng.integers(1, 4, n), 0).astype(np.uint32)
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum(counts)
+    res = kme_mod.new_result(n, int(off[-1]))
+    res.out_action[:] = orders.action
+    res.out_size[:] = rng.integers(0, 100, n)
+    res.trade_off[:] = off
+    res.trades["maker_oid"] = rng.integers(1, 1 << 40, len(res.trades))
+    want = kme_mod.expand_rows(orders, res).tobytes()
+    bad = []
+
+    def run():
+        for _ in range(12):
+            if kme_mod.expand_rows(orders, res, threads=8).tobytes() != want:
+                bad.append(1)
+
+    th = [threading.Thread(target=run) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not bad

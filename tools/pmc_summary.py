@@ -1,11 +1,15 @@
 """Per-launch HBM traffic of one kernel from rocprofv3 --pmc passes (tools/pmc_round.sh output).
 
 FETCH_SIZE and WRITE_SIZE (KiB per dispatch) come from separate passes (FETCH_SIZE uses 3 of the 4
-TCC slots, WRITE_SIZE 2).  Following MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950 tallies 128-B
-memory requests at 64 B, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is taken as reported.  Both
-count Infinity-Cache (MALL) hits too, so this is L2-miss traffic, an upper bound on HBM bytes.
+TCC slots, WRITE_SIZE 2).  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a
+WIDE COALESCED STREAMING read (128-B requests tallied at 64 B).  The matching kernels' reads are random
+gathers instead, and for those FETCH_SIZE is the bytes the line fills move, as reported: calibrated with
+tools/pmc_randcal.sh (profiles/r05_randcal.json: random 16 / 32 / 64-B gathers over a 2 GiB table give
+FETCH_SIZE = 4.0 / 2.0 / 1.05 x the bytes named = one 64-B fill per gather, TCC_EA0_RDREQ = 1.00 / 1.00
+/ 1.05 per gather).  So read bytes = FETCH_SIZE (x2 only with --streaming); WRITE_SIZE as reported.
+Both count Infinity-Cache (MALL) hits too, so this is L2-miss traffic, an upper bound on HBM bytes.
 
-usage: python tools/pmc_summary.py <pmc dir> <kernel regex> <out.json> [skip_first_n]
+usage: python tools/pmc_summary.py <pmc dir> <kernel regex> <out.json> [skip_first_n] [--streaming]
 """
 import csv
 import glob
@@ -70,8 +74,10 @@ def build_id_of(d):
 
 
 def main():
-    d, kre, out = sys.argv[1], sys.argv[2], sys.argv[3]
-    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    args = [a for a in sys.argv[1:] if a != "--streaming"]
+    streaming = "--streaming" in sys.argv[1:]
+    d, kre, out = args[0], args[1], args[2]
+    skip = int(args[3]) if len(args) > 3 else 0
     allv = {}
     for sub in sorted(glob.glob(os.path.join(d, "p*"))):
         if os.path.isdir(sub):
@@ -92,10 +98,13 @@ def main():
     f = res.get("FETCH_SIZE", {}).get("mean_per_dispatch")
     w = res.get("WRITE_SIZE", {}).get("mean_per_dispatch")
     if f is not None and w is not None:
-        res["read_bytes_per_launch"] = 2 * f * 1024
+        k = 2 if streaming else 1
+        res["read_bytes_per_launch"] = k * f * 1024
         res["write_bytes_per_launch"] = w * 1024
-        res["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
-        res["note"] = "FETCH_SIZE doubled per the gfx950 calibration; MALL hits included (upper bound)"
+        res["hbm_bytes_per_launch"] = k * f * 1024 + w * 1024
+        res["note"] = ("FETCH_SIZE doubled (wide coalesced streaming reads)" if streaming else
+                       "FETCH_SIZE as reported (random gathers: one 64-B fill each, tools/pmc_randcal.sh)") + \
+                      "; MALL hits included (upper bound)"
     res["per_kernel_derived"] = derived(res)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
