@@ -258,8 +258,8 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
     """The Java processor's path at rate, timed by the committed C harness
     (integration/host_harness.c): GpuMatchingEngine.java's schedule -- records written into two
     slots of registered host columns, kme_submit_epoch_host (H2D, kernels, D2H queued), kme_wait +
-    kme_expand_rows_async into the slot's row buffer with the pass over the rows reading each chunk
-    as it is written (kme_expand_rows_wait) -- over exactly the C ABI calls kme_jni.c makes.  PCIe- and host-inclusive: a secondary field, never the headline value."""
+    kme_expand_rows into the slot's row buffer and a pass over the rows -- over exactly the C ABI
+    calls kme_jni.c makes.  PCIe- and host-inclusive: a secondary field, never the headline value."""
     import ctypes as C
 
     import kme
@@ -282,10 +282,9 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
             "rows": int(stats[1]), "trades": int(stats[5]), "rows_per_s": stats[1] / dt, "h2d_bytes_per_epoch": h2d_b, "d2h_bytes_per_epoch": int(d2h_b),
             "pcie_GBps_each_way": round(max(h2d_b, d2h_b) * n_epochs / dt / 1e9, 2),
             "host_s": {"fill": round(stats[2], 4), "wait": round(stats[3], 4), "rows": round(stats[4], 4),
-                       "rows_expand_start": round(stats[7], 4), "rows_read": round(stats[4] - stats[7], 4), "total": round(dt, 4)},
+                       "rows_expand": round(stats[7], 4), "rows_read": round(stats[4] - stats[7], 4), "total": round(dt, 4)},
             "path": "integration/host_harness.c: GpuMatchingEngine.java's schedule over kme_jni.c's C ABI calls "
-                    "(registered host columns -> kme_submit_epoch_host -> kme_wait + kme_expand_rows_async -> rows read "
-                    "chunk by chunk as the host workers write them), "
+                    "(registered host columns -> kme_submit_epoch_host -> kme_wait + kme_expand_rows -> rows read), "
                     "two epochs in flight; PCIe- and host-inclusive, not the headline value"}
 
 

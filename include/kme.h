@@ -258,22 +258,6 @@ kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_res
  * consumer (the JNI glue).  n_threads 0 = the machine's hardware threads, at most 16; at most 64. */
 kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_result* res, kme_row* rows,
                               size_t cap, size_t* n_rows, uint32_t n_threads);
-/* The same rows, written in the background while the caller consumes them in order: host threads
- * expand the epoch in chunks of records, first chunk first, and kme_expand_rows_wait hands out the
- * prefix of rows that is complete -- so the one thread that forwards rows (Kafka Streams' stream
- * thread, KP:97-124) reads each chunk while it is still in the host caches, instead of after the
- * whole epoch was written.  *n_rows = rows of the epoch (KME_E_CAPACITY and no job when they do not
- * fit).  The inputs and results must stay untouched until kme_expand_rows_free.  When the background
- * workers are busy with another job the rows are written before this returns (then every wait
- * returns at once).  Replaces KProcessor's per-record forward loop feed (KP:96-126) on the drop-in's
- * host path. */
-typedef struct kme_expand_job kme_expand_job;
-kme_status kme_expand_rows_async(const kme_orders* in, uint32_t n, const kme_epoch_result* res, kme_row* rows,
-                                 size_t cap, size_t* n_rows, uint32_t n_threads, kme_expand_job** job);
-/* Blocks until at least min(want, rows of the job) rows are written; *ready = rows written so far. */
-kme_status kme_expand_rows_wait(kme_expand_job* job, size_t want, size_t* ready);
-/* Waits for the job to finish and releases it (NULL: no-op). */
-void kme_expand_rows_free(kme_expand_job* job);
 
 /* Identifies the sources libkme was built from (a hash of csrc/ and include/): the test session
  * rebuilds the library when it differs from the tree's. */

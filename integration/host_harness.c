@@ -4,11 +4,9 @@
  *   fill     the epoch's records go into the slot's registered input columns (Java's absolute
  *            ByteBuffer puts, one per field and record);
  *   submit   kme_submit_epoch_host: H2D, kernels, D2H queued, returns at once;
- *   complete kme_wait + kme_expand_rows_async into the slot's registered row buffer (exactly what
- *            Java_GpuMatchingEngine_complete does: up to 16 native threads write the rows chunk by
- *            chunk), and one pass over the rows on the calling thread, each chunk read as soon as it
- *            is written (kme_expand_rows_wait; Java's stream thread builds an Order per row, asking
- *            rowsReady() at each chunk boundary).
+ *   complete kme_wait + kme_expand_rows_mt into the slot's registered row buffer (exactly what
+ *            Java_GpuMatchingEngine_complete does: up to 16 native threads), then one pass over the
+ *            rows on the calling thread (Java's stream thread builds an Order per row from them).
  * Two slots and at most two epochs in flight: the schedule of GpuMatchingEngine.process / flush /
  * completeOldest.  The clock runs from the first fill to the last completed epoch, so the figure is
  * PCIe- and host-inclusive; it is reported beside the device-resident value, never as it.
@@ -41,8 +39,7 @@ static void* page_alloc(size_t bytes) {
 }
 
 /* Stats out: [0] seconds, [1] rows forwarded, [2] fill seconds, [3] complete (wait) seconds,
- * [4] expand + row-read seconds, [5] trades, [6] checksum of the rows read, [7] seconds to start the
- * expansion (the rest of [4] is the pass, overlapped with the expansion). */
+ * [4] expand + row-read seconds, [5] trades, [6] checksum of the rows read, [7] expand seconds. */
 int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, uint32_t n_epochs, uint32_t max_trades,
                       double* stats) {
     if (!e || !stream || !epoch || !stats) return KME_E_INVALID;
@@ -88,17 +85,12 @@ int kme_host_path_run(kme_engine* e, const kme_orders* stream, uint32_t epoch, u
             t_wait += b - a;
             if (rc != KME_OK) break;
             const kme_orders in = {h->action, h->oid, h->aid, h->sid, h->price, h->size};
-            size_t nr = 0, avail = 0;
-            kme_expand_job* job = NULL;
-            rc = kme_expand_rows_async(&in, h->n, &h->res, h->rows, h->rows_cap, &nr, 0, &job);
+            size_t nr = 0;
+            rc = kme_expand_rows_mt(&in, h->n, &h->res, h->rows, h->rows_cap, &nr, 0);
             if (rc != KME_OK) break;
             t_expand += now_s() - b;
-            for (size_t q = 0; q < nr; ++q) {   /* the JVM reads every row (one Order each), as they are written */
-                if (q == avail && kme_expand_rows_wait(job, q + 1, &avail) != KME_OK) { rc = KME_E_INVALID; break; }
+            for (size_t q = 0; q < nr; ++q)   /* the JVM reads every row (one Order each) */
                 check += (uint64_t)h->rows[q].oid + (uint64_t)h->rows[q].size + h->rows[q].kind;
-            }
-            kme_expand_rows_free(job);
-            if (rc != KME_OK) break;
             t_rows += now_s() - b;
             rows_total += nr;
             trades += st.n_trades;

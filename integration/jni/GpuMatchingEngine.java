@@ -82,7 +82,6 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     private static native int submit(long h, int slot, int n);
     private static native int poll(long h);
     private static native int complete(long h, int slot, long[] status);
-    private static native int rowsReady(long h, int slot, int want);
     private static native void forwarded(long h, int slot);
     private static native String statusText(int status);
     static native int checkpoint(long h, String path, long offset, long generation, long[] info);
@@ -233,9 +232,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         while (nReady > 0) {
             final int s = ready[0];
             final ByteBuffer r = rows[s];
-            int written = 0;                                            // native threads write the rows chunk by chunk
             for (int k = 0; k < readyRows[s]; k++) {
-                if (k == written) written = rowsReady(h, s, k + 1);    // (blocks until row k is written)
                 final int b = ROW_BYTES * k;
                 final Order o = new Order(r.getInt(b + 32), r.getLong(b), r.getLong(b + 8), r.getLong(b + 16),
                                           r.getInt(b + 36), r.getInt(b + 40));

@@ -13,16 +13,11 @@
  *   buffer(h, slot, column)   the slot's column 0..5 (action, oid, aid, sid, price, size) or 6 (rows)
  *   submit(h, slot, n)        kme_submit_epoch_host: H2D, kernels, D2H queued; returns at once
  *   poll(h)                   kme_poll: 1 when the oldest epoch in flight is done (punctuator)
- *   complete(h, slot, st)     kme_wait, then kme_expand_rows_async starts writing the MatchOut rows
- *                             into the slot's row buffer, in the reference's order: IN (KP:97), maker
- *                             / taker fill per trade (executeTrade, KP:265-274), OUT (KP:124); returns
- *                             the row count at once; st[0..3] = status, domain detail, error index,
- *                             records that took effect (kme_epoch_status).  The rows stay "ready"
- *                             (not yet forwarded) until forwarded(h, slot).
- *   rowsReady(h, slot, want)  kme_expand_rows_wait: blocks until the slot's first `want` rows are
- *                             written and returns how many are; the stream thread asks it at each
- *                             chunk boundary of its forward loop, so it reads every chunk of rows just
- *                             after the native threads wrote it
+ *   complete(h, slot, st)     kme_wait + kme_expand_rows_mt into the slot's row buffer, in the
+ *                             reference's order: IN (KP:97), maker / taker fill per trade
+ *                             (executeTrade, KP:265-274), OUT (KP:124); st[0..3] = status, domain
+ *                             detail, error index, records that took effect (kme_epoch_status).  The
+ *                             rows stay "ready" (not yet forwarded) until forwarded(h, slot).
  *   forwarded(h, slot)        Java has forwarded the slot's rows
  *   checkpoint(h, path, off, gen, info)
  *                             the commit point: kme_checkpoint_app of the engine
@@ -61,7 +56,6 @@ typedef struct jslot {
     kme_epoch_result res;          /* native host results, registered */
     uint32_t n;                    /* records of the epoch in flight (0 = none) */
     int64_t ready_rows;            /* rows completed and not yet forwarded (-1 = none) */
-    kme_expand_job* job;           /* the rows being written (complete -> forwarded / checkpoint), or NULL */
     uint64_t ready_seq;            /* completion order of the ready rows */
 } jslot;
 
@@ -115,8 +109,6 @@ static void free_handle(jkme* h) {
     }
     for (int s = 0; s < 2; ++s) {
         jslot* sl = &h->slot[s];
-        kme_expand_rows_free(sl->job);
-        sl->job = NULL;
         void* res[6] = {sl->res.out_action, sl->res.out_size, sl->res.out_prev, sl->res.out_flags, sl->res.trade_off,
                         sl->res.trades};
         for (int k = 0; k < NCOL; ++k) {
@@ -279,10 +271,7 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, 
     sl->n = 0;
     const uint32_t ne = s == KME_OK ? n : (st.n_effective < n ? st.n_effective : n);
     size_t rows = 0;
-    kme_expand_rows_free(sl->job);   /* (none: forwarded() or a checkpoint released it) */
-    sl->job = NULL;
-    const kme_status x = ne ? kme_expand_rows_async(&sl->in, ne, &sl->res, sl->rows, sl->rows_cap, &rows, 0, &sl->job)
-                            : KME_OK;
+    const kme_status x = ne ? kme_expand_rows_mt(&sl->in, ne, &sl->res, sl->rows, sl->rows_cap, &rows, 0) : KME_OK;
     jlong stv[4];
     stv[0] = (jlong)(s != KME_OK ? s : x);
     stv[1] = (jlong)(s != KME_OK ? st.detail : (x != KME_OK ? KME_D_CAP_TRADES : 0));
@@ -295,27 +284,11 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_complete(JNIEnv* env, jclass cls, 
     return (jint)rows;
 }
 
-/* static native int rowsReady(long h, int slot, int want): blocks until the slot's first `want` ready
- * rows are written (at most the slot's row count); returns how many are written. */
-JNIEXPORT jint JNICALL Java_GpuMatchingEngine_rowsReady(JNIEnv* env, jclass cls, jlong handle, jint slot, jint want) {
-    (void)env; (void)cls;
-    jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || slot < 0 || slot > 1 || h->slot[slot].ready_rows < 0) return 0;
-    jslot* sl = &h->slot[slot];
-    if (!sl->job) return (jint)sl->ready_rows;
-    size_t ready = 0;
-    if (kme_expand_rows_wait(sl->job, want > 0 ? (size_t)want : 0, &ready) != KME_OK) return 0;
-    return (jint)ready;
-}
-
 /* static native void forwarded(long h, int slot): the slot's ready rows have been forwarded. */
 JNIEXPORT void JNICALL Java_GpuMatchingEngine_forwarded(JNIEnv* env, jclass cls, jlong handle, jint slot) {
     (void)env; (void)cls;
     jkme* h = (jkme*)(intptr_t)handle;
-    if (!h || slot < 0 || slot > 1) return;
-    kme_expand_rows_free(h->slot[slot].job);
-    h->slot[slot].job = NULL;
-    h->slot[slot].ready_rows = -1;
+    if (h && slot >= 0 && slot <= 1) h->slot[slot].ready_rows = -1;
 }
 
 /* static native String statusText(int status) */
@@ -346,11 +319,6 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_checkpoint(JNIEnv* env, jclass cls
     if (!info || (*env)->GetArrayLength(env, info) < 2) return KME_E_INVALID;
     int order[2];
     const int nr = ready_order(h, order);
-    for (int k = 0; k < nr; ++k) {   /* every ready row written before it goes into the record */
-        jslot* sl = &h->slot[order[k]];
-        kme_expand_rows_free(sl->job);
-        sl->job = NULL;
-    }
     size_t bytes = sizeof(jrec_head);
     for (int k = 0; k < nr; ++k) bytes += sizeof(jrec_slot) + sizeof(kme_row) * (size_t)h->slot[order[k]].ready_rows;
     char* rec = (char*)malloc(bytes);

@@ -14,7 +14,6 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
-#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -112,113 +111,71 @@ kme_status kme_expand_rows(const kme_orders* in, uint32_t n, const kme_epoch_res
 
 }  // extern "C"
 
-// ------------------------------------------------------------------ row expansion jobs
-// An epoch's rows are expanded in chunks of records by host workers created once per process and
-// parked between jobs: starting threads per call cost ~0.5 ms per 65,536-record epoch (the drop-in's
-// default), most of its expand time.  Chunk c's rows start at 2 a + 2 (trade_off[a] - trade_off[0]),
-// a = its first record, so any worker can write any chunk; workers take chunks first to last, and a
-// consumer reads the complete prefix (kme_expand_rows_wait) -- or, for kme_expand_rows_mt, waits for
-// all.  One job uses the workers at a time; a job that finds them busy runs on threads of its own.
-struct kme_expand_job {
+namespace {
+// Workers kme_expand_rows_mt hands its record ranges to: created once (per process, on first use)
+// and parked on a condition variable between calls.  Starting threads per call cost ~0.5 ms per
+// 65,536-record epoch (the drop-in's default), most of its expand time.  One call at a time uses the
+// pool; a concurrent caller (another engine's completion) starts threads of its own as before.
+struct ExpandPool {
+    std::mutex use;                          // held by the call using the pool
+    std::mutex m;                            // everything below; tasks are picked under it
+    std::condition_variable wake, done;
+    std::vector<std::thread> th;
+    uint64_t gen = 0;                        // one generation per call
+    uint32_t ntask = 0, next = 0, nleft = 0;
     const kme_orders* in = nullptr;
     const kme_epoch_result* r = nullptr;
     kme_row* rows = nullptr;
-    uint32_t n = 0, ch = 1, nchunk = 0;
-    size_t total = 0;
-    std::atomic<uint32_t> next{0};           // chunks handed out
-    std::atomic<uint32_t> left{0};           // chunks not written yet
-    std::unique_ptr<std::atomic<uint8_t>[]> done;
-    uint32_t prefix = 0;                     // (consumer) chunks known complete, first to last
-    uint32_t workers = 0;                    // pool workers inside the job (under the pool lock)
-    bool pooled = false;
-    size_t row_start(uint32_t c) const {
-        if (c >= nchunk) return total;
-        const uint32_t a = c * ch;
-        return 2 * (size_t)a + 2 * (size_t)(r->trade_off[a] - r->trade_off[0]);
-    }
-    // takes and writes chunks until none is left to take; true when this call wrote the last one
-    bool work() {
-        bool last = false;
-        for (uint32_t c; (c = next.fetch_add(1)) < nchunk;) {
-            const uint32_t a = c * ch, b = std::min(n, a + ch);
-            expand_range(in, a, b, r, rows + row_start(c));
-            done[c].store(1, std::memory_order_release);
-            last |= left.fetch_sub(1, std::memory_order_acq_rel) == 1;
+    uint32_t n = 0;
+    // take the call's tasks until none is left (a task: its record range, read under the lock)
+    void drain() {
+        for (;;) {
+            uint32_t a, b;
+            const kme_orders* tin;
+            const kme_epoch_result* tr;
+            kme_row* tw;
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (next >= ntask) return;
+                const uint32_t t = next++;
+                a = (uint32_t)((uint64_t)n * t / ntask); b = (uint32_t)((uint64_t)n * (t + 1) / ntask);
+                tin = in; tr = r;
+                tw = rows + 2 * (size_t)a + 2 * (size_t)(r->trade_off[a] - r->trade_off[0]);
+            }
+            expand_range(tin, a, b, tr, tw);
+            std::lock_guard<std::mutex> g(m);
+            if (--nleft == 0) done.notify_all();
         }
-        return last;
     }
-};
-
-namespace {
-struct ExpandPool {
-    std::atomic<bool> busy{false};           // a job holds the workers
-    std::mutex m;
-    std::condition_variable wake, fin;
-    uint32_t nthreads = 0;
-    uint64_t gen = 0;
-    kme_expand_job* cur = nullptr;
     void worker() {
         uint64_t seen = 0;
         for (;;) {
-            kme_expand_job* j;
             {
                 std::unique_lock<std::mutex> g(m);
                 wake.wait(g, [&] { return gen != seen; });
                 seen = gen;
-                j = cur;
-                if (!j) continue;
-                ++j->workers;
             }
-            j->work();
-            std::lock_guard<std::mutex> g(m);
-            --j->workers;
-            fin.notify_all();
+            drain();
         }
     }
-    void start(kme_expand_job* j, uint32_t T) {
+    void run(const kme_orders* in_, uint32_t n_, const kme_epoch_result* r_, kme_row* rows_, uint32_t T) {
+        while (th.size() + 1 < T) { th.emplace_back([this] { worker(); }); th.back().detach(); }
         {
             std::lock_guard<std::mutex> g(m);
-            while (nthreads + 1 < T) { std::thread([this] { worker(); }).detach(); ++nthreads; }
-            cur = j;
+            in = in_; n = n_; r = r_; rows = rows_;
+            ntask = T; next = 0; nleft = T;
             ++gen;
         }
         wake.notify_all();
-    }
-    void finish(kme_expand_job* j) {
+        drain();
         std::unique_lock<std::mutex> g(m);
-        fin.wait(g, [&] { return j->left.load() == 0 && j->workers == 0; });
-        if (cur == j) cur = nullptr;
+        done.wait(g, [&] { return nleft == 0; });
+        ntask = 0;                           // (a late worker finds nothing to take)
     }
 };
 ExpandPool& expand_pool() {
     static ExpandPool* p = new ExpandPool;   // (never destroyed: its detached workers outlive static teardown)
     return *p;
-}
-uint32_t expand_threads(uint32_t n, uint32_t n_threads) {
-    uint32_t T = n_threads ? n_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    return std::min<uint32_t>(std::min<uint32_t>(T, 64), std::max<uint32_t>(1, n / 4096));   // >= 4,096 records each
-}
-// the job's chunks on threads of its own (the workers are busy): all written when this returns
-void run_unpooled(kme_expand_job* j, uint32_t T) {
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; ++t) th.emplace_back([j] { j->work(); });
-    j->work();
-    for (auto& x : th) x.join();
-}
-kme_status job_init(kme_expand_job* j, const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows,
-                    size_t cap, size_t* n_rows, uint32_t T, uint32_t chunk) {
-    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
-    j->total = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
-    *n_rows = j->total;
-    if (j->total > cap) return KME_E_CAPACITY;
-    j->in = in; j->r = r; j->rows = rows; j->n = n;
-    j->ch = std::max<uint32_t>(1, chunk);
-    j->nchunk = (n + j->ch - 1) / j->ch;
-    j->left.store(j->nchunk);
-    j->done.reset(new std::atomic<uint8_t>[j->nchunk > 0 ? j->nchunk : 1]);
-    for (uint32_t c = 0; c < j->nchunk; ++c) j->done[c].store(0, std::memory_order_relaxed);
-    (void)T;
-    return KME_OK;
 }
 }  // namespace
 
@@ -226,64 +183,29 @@ extern "C" {
 
 kme_status kme_expand_rows_mt(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
                               size_t* n_rows, uint32_t n_threads) {
-    const uint32_t T = expand_threads(n, n_threads);
-    kme_expand_job j;
-    const kme_status st = job_init(&j, in, n, r, rows, cap, n_rows, T, (n + 4 * T - 1) / (4 * T));
-    if (st != KME_OK) return st;
-    if (T <= 1) { j.work(); return KME_OK; }
+    if (!in || !r || !n_rows || (cap && !rows)) return KME_E_INVALID;
+    const size_t need = 2 * (size_t)n + 2 * (size_t)(r->trade_off[n] - r->trade_off[0]);
+    *n_rows = need;
+    if (need > cap) return KME_E_CAPACITY;
+    uint32_t T = n_threads ? n_threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    T = std::min<uint32_t>(std::min<uint32_t>(T, 64), std::max<uint32_t>(1, n / 4096));   // >= 4,096 records each
+    if (T <= 1) { expand_range(in, 0, n, r, rows); return KME_OK; }
     ExpandPool& pool = expand_pool();
-    bool idle = false;
-    if (!pool.busy.compare_exchange_strong(idle, true)) { run_unpooled(&j, T); return KME_OK; }
-    pool.start(&j, T);
-    j.work();
-    pool.finish(&j);
-    pool.busy.store(false);
-    return KME_OK;
-}
-
-kme_status kme_expand_rows_async(const kme_orders* in, uint32_t n, const kme_epoch_result* r, kme_row* rows, size_t cap,
-                                 size_t* n_rows, uint32_t n_threads, kme_expand_job** job) {
-    if (!job) return KME_E_INVALID;
-    *job = nullptr;
-    const uint32_t T = expand_threads(n, n_threads);
-    kme_expand_job* j = new kme_expand_job;
-    // chunks of ~16K records (~50K rows, ~2.4 MB): the consumer's next chunk is written shortly before
-    // it reads it, while the lines are still in the host's caches
-    const kme_status st = job_init(j, in, n, r, rows, cap, n_rows, T, 16384);
-    if (st != KME_OK) { delete j; return st; }
-    ExpandPool& pool = expand_pool();
-    bool idle = false;
-    if (T <= 1) j->work();
-    else if (pool.busy.compare_exchange_strong(idle, true)) { j->pooled = true; pool.start(j, T + 1); }   // (+1: the caller reads)
-    else run_unpooled(j, T);
-    *job = j;
-    return KME_OK;
-}
-
-kme_status kme_expand_rows_wait(kme_expand_job* j, size_t want, size_t* ready) {
-    if (!j || !ready) return KME_E_INVALID;
-    if (want > j->total) want = j->total;
-    for (uint32_t spins = 0;; ++spins) {
-        while (j->prefix < j->nchunk && j->done[j->prefix].load(std::memory_order_acquire)) ++j->prefix;
-        *ready = j->row_start(j->prefix);
-        if (*ready >= want) return KME_OK;
-        // the next chunk is not written yet: write one (any not taken) rather than wait idle
-        if (j->next.load(std::memory_order_relaxed) < j->nchunk) {
-            if (j->work() && j->pooled) { std::lock_guard<std::mutex> g(expand_pool().m); expand_pool().fin.notify_all(); }
-        } else if (spins > 64) {
-            std::this_thread::yield();
-        }
+    if (pool.use.try_lock()) {
+        pool.run(in, n, r, rows, T);
+        pool.use.unlock();
+        return KME_OK;
     }
-}
-
-void kme_expand_rows_free(kme_expand_job* j) {
-    if (!j) return;
-    if (j->pooled) {
-        ExpandPool& pool = expand_pool();
-        pool.finish(j);
-        pool.busy.store(false);
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (uint32_t t = 0; t < T; ++t) {
+        const uint32_t a = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T);
+        kme_row* w = rows + 2 * (size_t)a + 2 * (size_t)(r->trade_off[a] - r->trade_off[0]);
+        if (t + 1 == T) expand_range(in, a, b, r, w);
+        else th.emplace_back(expand_range, in, a, b, r, w);
     }
-    delete j;
+    for (auto& x : th) x.join();
+    return KME_OK;
 }
 
 kme_status kme_tape_json(const kme_orders* in, uint32_t n, const kme_epoch_result* r, char* buf, size_t cap, size_t* len) {

@@ -82,8 +82,7 @@ EXPORTS = [
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
-    "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_expand_rows_mt",
-    "kme_expand_rows_async", "kme_expand_rows_wait", "kme_expand_rows_free", "kme_build_id",
+    "kme_host_register", "kme_host_unregister", "kme_submit_epoch_host", "kme_poll", "kme_expand_rows", "kme_expand_rows_mt", "kme_build_id",
     "kme_rccl_load", "kme_rccl_last_error", "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
     "kme_credit_adjust", "kme_credit_rebalance",
     "kme_multi_create", "kme_multi_destroy", "kme_multi_submit_epoch_host", "kme_multi_poll", "kme_multi_wait",
@@ -162,10 +161,6 @@ def lib():
                                  C.POINTER(C.c_size_t)]),
         "kme_expand_rows_mt": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
                                     C.POINTER(C.c_size_t), u32]),
-        "kme_expand_rows_async": (st, [C.POINTER(kme_orders), u32, C.POINTER(kme_epoch_result), vp, C.c_size_t,
-                                       C.POINTER(C.c_size_t), u32, C.POINTER(vp)]),
-        "kme_expand_rows_wait": (st, [vp, C.c_size_t, C.POINTER(C.c_size_t)]),
-        "kme_expand_rows_free": (None, [vp]),
         "kme_build_id": (C.c_char_p, []),
         "kme_rccl_load": (st, [C.c_char_p]),
         "kme_rccl_last_error": (C.c_char_p, []),
@@ -658,39 +653,6 @@ def expand_rows(orders: Orders, res: EpochResult, n: int | None = None, threads:
         raise KmeError(rc, "kme_expand_rows")
     del keep
     return rows
-
-
-def expand_rows_async(orders: Orders, res: EpochResult, n: int | None = None, threads: int = 0, step: int = 1):
-    """kme_expand_rows_async + kme_expand_rows_wait + kme_expand_rows_free, consumed as the JNI glue's
-    forward loop consumes them: returns (rows, the ready counts seen), each row copied out only once
-    kme_expand_rows_wait said it was written (asking for `step` rows more each time)."""
-    L = lib()
-    n = len(orders) if n is None else n
-    s, keep = _soa(orders)
-    r = kme_epoch_result(_np_ptr(res.out_action), _np_ptr(res.out_size), _np_ptr(res.out_prev),
-                         _np_ptr(res.out_flags), _np_ptr(res.trade_off), _np_ptr(res.trades), len(res.trades))
-    need = C.c_size_t(0)
-    L.kme_expand_rows(C.byref(s), n, C.byref(r), None, 0, C.byref(need))
-    buf = np.zeros(need.value, ROW_DTYPE)
-    out = np.zeros(need.value, ROW_DTYPE)
-    job = C.c_void_p()
-    rc = L.kme_expand_rows_async(C.byref(s), n, C.byref(r), C.c_void_p(buf.ctypes.data), len(buf), C.byref(need),
-                                 threads, C.byref(job))
-    if rc:
-        raise KmeError(rc, "kme_expand_rows_async")
-    seen, got, ready = [], 0, C.c_size_t(0)
-    try:
-        while got < need.value:
-            rc = L.kme_expand_rows_wait(job, got + step, C.byref(ready))
-            if rc:
-                raise KmeError(rc, "kme_expand_rows_wait")
-            seen.append(ready.value)
-            out[got:ready.value] = buf[got:ready.value]
-            got = ready.value
-    finally:
-        L.kme_expand_rows_free(job)
-    del keep
-    return out, seen
 
 
 def tape_json_from(orders: Orders, res: EpochResult) -> str:

@@ -253,27 +253,3 @@ def test_expand_rows_pool_under_concurrent_calls(kme_mod):
     for t in th:
         t.join()
     assert not bad
-
-
-@pytest.mark.parametrize("n,threads", [(300_000, 0), (300_000, 16), (5_000, 0), (0, 0)])
-def test_expand_rows_async_prefix_is_final(kme_mod, n, threads):
-    """kme_expand_rows_async / _wait: every ready count is a row boundary the rows up to which are
-    already kme_expand_rows's, the counts only grow and end at the epoch's rows; free after the last."""
-    import numpy as np
-
-    from kme import workloads as W
-
-    rng = np.random.Generator(np.random.PCG64(23))
-    orders = W.uniform(max(n, 64), n_symbols=64, n_accounts=128, seed=23)
-    counts = np.where(rng.random(n) < 0.3, rng.integers(1, 5, n), 0).astype(np.uint32)
-    off = np.zeros(n + 1, np.uint32)
-    off[1:] = np.cumsum(counts)
-    res = kme_mod.new_result(max(n, 1), max(int(off[-1]), 1))
-    res.out_action[:n] = orders.action[:n]
-    res.out_size[:n] = rng.integers(0, 100, n)
-    res.trade_off[:n + 1] = off
-    res.trades["maker_oid"] = rng.integers(1, 1 << 40, len(res.trades))
-    want = kme_mod.expand_rows(orders, res, n=n)
-    got, seen = kme_mod.expand_rows_async(orders, res, n=n, threads=threads, step=5000)
-    assert got.tobytes() == want.tobytes()
-    assert seen == sorted(seen) and (not seen or seen[-1] == len(want))

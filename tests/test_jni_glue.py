@@ -22,8 +22,8 @@ from kme import workloads as W
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
 CHECK_LIB = os.path.join(ROOT, "integration", "jni", "libkme_jni_check.so")
-SYMBOLS = ["create", "destroy", "buffer", "submit", "poll", "complete", "rowsReady", "forwarded", "statusText",
-           "checkpoint", "restore"]
+SYMBOLS = ["create", "destroy", "buffer", "submit", "poll", "complete", "forwarded", "statusText", "checkpoint",
+           "restore"]
 ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
                       ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
 assert ROW_DTYPE.itemsize == 48
@@ -118,8 +118,6 @@ def _lib():
     lib.Java_GpuMatchingEngine_poll.restype = I
     lib.Java_GpuMatchingEngine_complete.argtypes = [P, P, L, I, P]
     lib.Java_GpuMatchingEngine_complete.restype = I
-    lib.Java_GpuMatchingEngine_rowsReady.argtypes = [P, P, L, I, I]
-    lib.Java_GpuMatchingEngine_rowsReady.restype = I
     lib.Java_GpuMatchingEngine_statusText.argtypes = [P, P, I]
     lib.Java_GpuMatchingEngine_statusText.restype = P
     return lib
@@ -183,20 +181,9 @@ class Proc:
         slot = self.pending.pop(0)
         m = self.lib.Java_GpuMatchingEngine_complete(self.j.env, None, self.h, slot, self.status)
         assert not self.j.thrown, self.j.thrown
-        _rows_ready(self.lib, self.j, self.h, slot, m)
         out = self.rows[slot][:m].copy(), self.j.objs[self.status].copy()
         self.lib.Java_GpuMatchingEngine_forwarded(self.j.env, None, self.h, slot)
         return out
-
-
-def _rows_ready(lib, j, h, slot, m):
-    """GpuMatchingEngine.forwardReady's loop: rows are read only up to what rowsReady() says is written
-    (asked again at each chunk boundary); the count only grows and reaches m."""
-    written = 0
-    while written < m:
-        got = lib.Java_GpuMatchingEngine_rowsReady(j.env, None, h, slot, written + 1)
-        assert written < got <= m, (written, got, m)
-        written = got
 
 
 def _as_tape(rows, rec_dtype):
@@ -380,7 +367,6 @@ class JavaProcessor:
     def forward_ready(self):
         while self.ready:
             s = self.ready.pop(0)
-            _rows_ready(self.lib, self.j, self.h, s, self.ready_rows[s])
             self.out.append(self.rows[s][:self.ready_rows[s]].copy())
             self.lib.Java_GpuMatchingEngine_forwarded(self.j.env, None, self.h, s)
             self.busy[s] = False
