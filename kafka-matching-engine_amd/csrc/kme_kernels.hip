@@ -3107,6 +3107,12 @@ struct GroupLane {
     }
 
     // ---------------- node slots (the block format of GroupWave::spill_blocks)
+    // A freed slot's node keeps live = 1 while the slot sits on this lane's stack: most are handed
+    // out again within the epoch (a rest rewrites the whole node), so the store of live = 0 -- a
+    // partial-line write to a random node -- is made only when the slot leaves the stack unused (in
+    // a spilled block, including the ones store_group spills at the end).  Meanwhile a node on the
+    // stack is dead to this lane's cancels (in_stack), the only readers of the group's nodes before
+    // the group's next epoch.
     // Stack entries [b, fsp) become one block: the last entry hosts the others' ids.
     KDEV void spill_block(int b) {
         const int host = fs[fsp - 1][lane];
@@ -3115,6 +3121,8 @@ struct GroupLane {
         w[0] = free_head; w[1] = cnt;
 #pragma unroll
         for (int k = 0; k < FBLK - 1; ++k) w[2 + k] = k < cnt ? fs[b + k][lane] : -1;
+#pragma unroll
+        for (int k = 0; k < FBLK - 1; ++k) if (k < cnt) S.pool[w[2 + k]].live = 0;
         w[14] = 0; w[15] = 0;                               // Node::live = 0
         KG int4* d = reinterpret_cast<KG int4*>(&S.pool[host]);
 #pragma unroll
@@ -3156,9 +3164,13 @@ struct GroupLane {
         return chunk_next++;
     }
     KDEV void free_slot(int32_t s) {
-        S.pool[s].live = 0;
         if (fsp == LFS) spill_block(LFS - FBLK);
         fs[fsp++][lane] = s;
+    }
+    KDEV bool in_stack(int32_t s) const {
+        bool hit = false;
+        for (int k = 0; k < fsp; ++k) hit |= fs[k][lane] == s;
+        return hit;
     }
 
     // ---------------- trades: one TradeTmp per trade.  Each lane reserves LANE_TCH slots at a time
@@ -3310,6 +3322,7 @@ struct GroupLane {
     KDEV bool cancel(const Rec& r, int32_t slot, int4 c0, int4 c1, int4 c2, int4 c3, int32_t vlev, int4 vl1) {
         if (slot < 0) return false;                          // orders.get(oid) == null
         if (!(c3.z != 0 && mk64(c0.x, c0.y) == r.oid && mk64(c0.z, c0.w) == r.aid)) return false;   // KP:291
+        if (in_stack(slot)) return false;                    // freed this epoch (filled or removed)
         if (!exists) { die(KME_E_DOMAIN, KME_D_NPE_BOOK); return false; }
         const int32_t action = c3.y, price = c3.x, size = c1.z, next = c1.w, prev = c2.z;
         const int64_t prev_oid = mk64(c2.x, c2.y);

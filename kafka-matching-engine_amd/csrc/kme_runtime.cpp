@@ -306,9 +306,18 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             // sort key aid << hb | hash(sid), hb = 8: a bucket holds ~one chain.  (Measured and not
             // kept: hb = 2 at 65,536 accounts, two radix passes instead of three -- the longer bucket
             // runs cost k_lchains and k_ldetect far more than the pass saves.  KME_LEDGER_HBITS: A/B.)
+            // Fewer hash bits where an epoch cannot give an account many ops: with more accounts than
+            // ops per epoch (the drop-in's 2^20 accounts, 65,536-record epochs) a bucket holds ~one
+            // chain at any hb, so hb shrinks until the key fits one pass fewer (28 -> 27 bits: three
+            // passes, not four); at C3 (~113 ops per account) hb stays 8.
             int abits = 0;
             while ((1ull << abits) < (uint64_t)cfg->max_accounts) ++abits;
-            int hb = 8;
+            const uint64_t per_acct = (nops + cfg->max_accounts - 1) / std::max<uint64_t>(1, cfg->max_accounts);
+            int hb_min = 1;
+            while (hb_min < 8 && (1ull << (hb_min - 1)) < per_acct) ++hb_min;
+            hb_min = std::max(2, hb_min);
+            const int passes = (abits + hb_min + RADIX_BITS - 1) / RADIX_BITS;
+            int hb = std::min(8, passes * RADIX_BITS - abits);
             if (const char* v = std::getenv("KME_LEDGER_HBITS")) hb = std::max(1, std::min(8, std::atoi(v)));
             S.lhbits = hb;
             S.lpasses = std::max(1, (abits + hb + RADIX_BITS - 1) / RADIX_BITS);
