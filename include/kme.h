@@ -370,7 +370,8 @@ kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t*
  * kme_credit_rebalance: state, all-gather over RCCL, adjust -- a collective every rank calls and
  * every rank completes: a rank that cannot re-split (an epoch in flight: KME_E_INVALID, a failed
  * engine: KME_E_FAILED) still takes part with a status word, and then no rank adjusts; that rank
- * returns its own status, the others KME_E_INVALID. */
+ * returns its own status, the others KME_E_INVALID.  All three have completed on the device when they
+ * return (dev_out may be read on any stream). */
 kme_status kme_credit_state(kme_engine* e, int64_t* dev_out);
 kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_shards, uint32_t my_shard);
 kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c);

@@ -1027,6 +1027,9 @@ kme_status kme_credit_state(kme_engine* e, int64_t* dev_out) {
     HIP_TRY(hipSetDevice(e->device));
     launch_credit_state(e->S, dev_out, e->stream);
     HIP_TRY(hipGetLastError());
+    // complete on return, like kme_credit_adjust: the caller reads dev_out on a stream of its own
+    // (a torch stream, a transport's), which nothing orders after the engine stream
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return KME_OK;
 }
 
@@ -1094,6 +1097,9 @@ kme_status credit_state_enqueue(kme_engine* e, int64_t* dev_out) {
     HIP_TRY(hipSetDevice(e->device));
     launch_credit_state(e->S, dev_out, e->stream);
     HIP_TRY(hipGetLastError());
+    // complete on return, like kme_credit_adjust: the caller reads dev_out on a stream of its own
+    // (a torch stream, a transport's), which nothing orders after the engine stream
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return KME_OK;
 }
 kme_status credit_adjust_enqueue(kme_engine* e, const int64_t* dev_all, uint32_t n, uint32_t me, size_t stride) {
