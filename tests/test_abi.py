@@ -253,3 +253,47 @@ def test_expand_rows_pool_under_concurrent_calls(kme_mod):
     for t in th:
         t.join()
     assert not bad
+
+
+@pytest.mark.parametrize("misalign", [0, 8])
+def test_expand_rows_streaming_and_unaligned_buffers_agree(kme_mod, misalign):
+    """The row writer streams 16-B stores into a 16-B aligned buffer and falls back to ordinary
+    stores otherwise: both give kme_expand_rows's rows byte for byte."""
+    import ctypes as C
+
+    import numpy as np
+
+    from kme import workloads as W
+
+    n = 20_000
+    rng = np.random.Generator(np.random.PCG64(31))
+    orders = W.uniform(n, n_symbols=64, n_accounts=128, seed=31)
+    counts = np.where(rng.random(n) < 0.4, rng.integers(1, 4, n), 0).astype(np.uint32)
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum(counts)
+    res = kme_mod.new_result(n, int(off[-1]))
+    res.out_action[:] = orders.action
+    res.out_size[:] = rng.integers(0, 100, n)
+    res.out_flags[:] = rng.integers(0, 2, n)
+    res.out_prev[:] = rng.integers(1, 1 << 40, n)
+    res.trade_off[:] = off
+    res.trades["maker_oid"] = rng.integers(1, 1 << 40, len(res.trades))
+    want = kme_mod.expand_rows(orders, res)
+    L = kme_mod.lib()
+    s, keep = kme_mod._soa(orders)
+    r = kme_mod.kme_epoch_result(kme_mod._np_ptr(res.out_action), kme_mod._np_ptr(res.out_size),
+                                 kme_mod._np_ptr(res.out_prev), kme_mod._np_ptr(res.out_flags),
+                                 kme_mod._np_ptr(res.trade_off), kme_mod._np_ptr(res.trades), len(res.trades))
+    raw = np.zeros(want.nbytes + 64, np.uint8)
+    base = (-raw.ctypes.data) % 16 + misalign            # 16-B aligned, or 8 B past it
+    need = C.c_size_t(0)
+    for threads in (1, 4):
+        raw[:] = 0
+        buf = C.c_void_p(raw.ctypes.data + base)
+        if threads == 1:
+            rc = L.kme_expand_rows(C.byref(s), n, C.byref(r), buf, len(want), C.byref(need))
+        else:
+            rc = L.kme_expand_rows_mt(C.byref(s), n, C.byref(r), buf, len(want), C.byref(need), threads)
+        assert rc == 0 and need.value == len(want)
+        assert raw[base:base + want.nbytes].tobytes() == want.tobytes()
+    del keep
