@@ -2792,14 +2792,13 @@ struct GroupWave {
 // all: k_match_lanes is not launched this epoch (its last launch found no light group), so the
 // light groups are k_match's too.
 // Four wavefronts per SIMD (<= 128 VGPRs; left to itself the compiler takes 134 and three): same-box
-// A/B against three, C2 / C5 / the N = 8 shard shape 1-10% faster (diagnostic builds: -DKME_MATCH_WAVES)
-#ifndef KME_MATCH_WAVES
-#define KME_MATCH_WAVES 4
-#endif
-#define KME_MATCH_ATTR __attribute__((amdgpu_waves_per_eu(KME_MATCH_WAVES)))
+// A/B against three, C2 / C5 / the N = 8 shard shape 1-10% faster.  WAVES = 5 (<= 96 VGPRs, 48 B of
+// spills) is the launch for many busy groups and few removes (the shard shapes: N = 8 +2.7% same-box);
+// cancel-heavy epochs (C5) lose up to 16% with it and two-wave epochs (C2) gain nothing, so they keep four.
 // TWO: two wavefronts per group (TwoLds): wave 0 below, wave 1 GroupWave::run_levels.
-template <bool TWO>
-__global__ void __launch_bounds__(TWO ? 128 : 64) KME_MATCH_ATTR k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
+template <bool TWO, int WAVES>
+__global__ void __launch_bounds__(TWO ? 128 : 64) __attribute__((amdgpu_waves_per_eu(WAVES)))
+k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
                                                                       int buf, int all, int dense) {
     __shared__ GroupLds lds;
     const DevState& S = *Sp;
@@ -3986,7 +3985,7 @@ __global__ void __launch_bounds__(256) k_glist_scatter(DevState S, const uint32_
     if (e > b && pos[g + 1] != pos[g]) S.glist[pos[g]] = g;   // (pos: the exclusive scan of the flags, in place)
 }
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, int two,
-                  int dense) {
+                  int dense, int five) {
     if (dense) {
         const uint32_t G = (uint32_t)S.G;
         hipLaunchKernelGGL(k_glist_flags, dim3(cdiv(G, 256)), dim3(256), 0, st, S, all);
@@ -3995,8 +3994,9 @@ void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_de
         launch_excl_scan(S.gflag, S.gflag, G + 1, S.gcount + 64, S.gcount, st);
         hipLaunchKernelGGL(k_glist_scatter, dim3(cdiv(G, 256)), dim3(256), 0, st, S, (const uint32_t*)S.gflag);
     }
-    if (two) hipLaunchKernelGGL(k_match<true>, dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
-    else hipLaunchKernelGGL(k_match<false>, dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
+    if (two) hipLaunchKernelGGL((k_match<true, 4>), dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
+    else if (five) hipLaunchKernelGGL((k_match<false, 5>), dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
+    else hipLaunchKernelGGL((k_match<false, 4>), dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

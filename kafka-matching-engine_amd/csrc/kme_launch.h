@@ -49,7 +49,8 @@ void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t
 // returns the buffer index (0/1) holding the sorted input permutation
 int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st);
 // two: two wavefronts per group (the pass one segment ahead of the level step; few busy groups)
-void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st, int all, int two, int dense);
+void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st, int all, int two, int dense,
+                  int five);
 // light groups (at most S.light_max records in the epoch), one lane each; independent of k_match
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st);
 void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st);

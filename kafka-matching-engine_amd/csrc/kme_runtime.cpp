@@ -544,7 +544,9 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         // busy groups sparse in the id space (a symbol shard of a larger universe: 8,277 of 65,537
         // ids at the N = 8 shard of C3): k_match's first blocks take them, from a compact list
         const bool dense = e->dense_grid && e->last_busy > 0 && (uint64_t)e->last_busy * 4 < (uint64_t)S.G;
-        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0);
+        // five wavefronts per SIMD for many busy groups and few removes (k_match's WAVES)
+        const bool five = !two && e->last_busy > e->two_max && !e->last_cancel_heavy;
+        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0, five ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);

@@ -198,3 +198,18 @@ def test_ledger_tables_grow_online_at_the_c3_accounts(kme_mod, oracle_mod, monke
     assert b.snapshot_ledger() == want_ledger
     assert b.snapshot_books() == want_books
     b.close()
+
+
+def test_drop_in_shape_accounts_far_outnumber_ops(kme_mod, oracle_mod, monkeypatch):
+    """The drop-in's shape: 2^20 accounts, 65,536-record epochs.  The stream's 2,048 accounts are
+    spread 300 ids apart (every gap between two accounts with ops is longer than k_lseg's 256, so
+    each goes to the gap list k_lseg_gaps fills, and so does the ~400K-id tail after the last one),
+    and with fewer ops than accounts the sort key takes 7 sid-hash bits for three radix passes
+    instead of four.  Tape, books and ledger against the oracle after every epoch."""
+    n_sym, n_used, E, stride = 1024, 2048, 1 << 16, 300
+    body = W.uniform(4 * E, n_symbols=n_sym, n_accounts=n_used, seed=2401)
+    setup = W.funded_setup(n_used, range(1, n_sym + 1))
+    body.aid[:] = body.aid * stride
+    setup.aid[:] = setup.aid * stride
+    stats, _ = _run(kme_mod, oracle_mod, setup, body, n_sym, 1 << 20, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    assert all(s == 0 for _, s in stats[1:]), stats
