@@ -3359,7 +3359,12 @@ struct GroupLane {
 // a resting order's own level, a cancel's target node or rest slot and its level; second: the
 // taker's first maker, a same-epoch cancel's node), so the round trips of a step are ~2 plus the
 // makers beyond the first, not the sum of every path's chain.
-__global__ void __launch_bounds__(64) k_match_lanes(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
+#ifdef KME_LANES_WAVES   // diagnostic builds: a VGPR cap for k_match_lanes (waves per SIMD)
+#define KME_LANES_ATTR __attribute__((amdgpu_waves_per_eu(KME_LANES_WAVES)))
+#else
+#define KME_LANES_ATTR
+#endif
+__global__ void __launch_bounds__(64) KME_LANES_ATTR k_match_lanes(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf) {
     __shared__ int32_t fs[LFS][64];
     const DevState& S = *Sp;
     const EpochIO& io = *iop;
