@@ -3069,6 +3069,15 @@ struct GroupLane {
     size_t tpos, tlim;            // this lane's reserved trade scratch [tpos, tlim) (LANE_TCH at a time)
     uint32_t tspare;              // a spare reservation (shard offset), valid if has_spare: requested
     bool has_spare;               //   with a record's first gather, so running out costs no round trip
+    // The last rest's stores, held back until the next record's gathers are issued (flush_rest): a
+    // load waits for every older memory operation of the wavefront (vmcnt is in order), so stores
+    // issued before the next record's loads would lengthen its first round trip.  The next record's
+    // gathers take the values from here where they read what the rest wrote.
+    bool pv = false;
+    int32_t p_slot = -1, p_nprev = -1;   // the new node; the old tail whose next becomes p_slot (or -1)
+    uint32_t p_otpos = 0;                // the oid-table entry that becomes p_slot
+    KG Level* p_lev = nullptr;           // the level line, whole
+    int4 p_node[4], p_l0, p_l1;
     LST(uint32_t nload = 0;)      // (stamps build) maker loads of the sweep beyond the first
 
     KDEV GroupLane(const DevState& s, const EpochIO& e, int32_t (*f)[64], int32_t gg)
@@ -3288,8 +3297,8 @@ struct GroupLane {
         int32_t nprev = -1;
         int64_t poid = 0;
         if (!check_bit(lo, hi, p)) {                         // new bucket (KP:209-211)
-            reinterpret_cast<KG int4*>(lv)[0] = make_int4(slot, slot, 0, 0);
-            reinterpret_cast<KG int4*>(lv)[1] = make_int4((int32_t)tsize, tsize < 0 ? -1 : 0, lo32(r.oid), hi32(r.oid));
+            p_l0 = make_int4(slot, slot, 0, 0);
+            p_l1 = make_int4((int32_t)tsize, tsize < 0 ? -1 : 0, lo32(r.oid), hi32(r.oid));
             set_bit(lo, hi, p);
             set_bm(s, lo, hi);
         } else {                                             // append at the tail (KP:213-219)
@@ -3297,23 +3306,40 @@ struct GroupLane {
             nprev = l0.y;
             poid = mk64(l1.z, l1.w);
             const int64_t q = mk64(l1.x, l1.y) + tsize;
-            S.pool[nprev].next = slot;
-            lv->tail = slot;
-            reinterpret_cast<KG int4*>(lv)[1] = make_int4(lo32(q), hi32(q), lo32(r.oid), hi32(r.oid));
+            p_l0 = make_int4(l0.x, slot, l0.z, l0.w);
+            p_l1 = make_int4(lo32(q), hi32(q), lo32(r.oid), hi32(r.oid));
             o.has_prev = true;
             o.prev = poid;
         }
-        KG int4* nd = reinterpret_cast<KG int4*>(&S.pool[slot]);
-        nd[0] = make_int4(lo32(r.oid), hi32(r.oid), lo32(r.aid), hi32(r.aid));
-        nd[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
-        nd[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
-        nd[3] = make_int4(p, r.action, 1, 0);
         // its oid-table entry (k_emap's pending one: r.tgt of a BUY/SELL is its position) becomes the
-        // rest slot here, one 4-B store -- no rest_slot store and no pass in k_unsort (k_match's
-        // groups store rest_slot, which k_unsort copies)
+        // rest slot, one 4-B store -- no rest_slot store and no pass in k_unsort (k_match's groups
+        // store rest_slot, which k_unsort copies)
         if (r.tgt > (int64_t)S.otab_mask) { die(KME_E_CAPACITY, KME_D_SENTINEL_OID); return; }   // (guard)
-        otab_final(S.otab, (int32_t)r.tgt, slot);
+        p_node[0] = make_int4(lo32(r.oid), hi32(r.oid), lo32(r.aid), hi32(r.aid));
+        p_node[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
+        p_node[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
+        p_node[3] = make_int4(p, r.action, 1, 0);
+        p_slot = slot; p_nprev = nprev; p_otpos = (uint32_t)r.tgt; p_lev = lv;
+        pv = true;                                           // (stored by flush_rest)
         o.rested = true;
+    }
+
+    KDEV void flush_rest() {
+        if (!pv) return;
+        pv = false;
+        KG int4* lvp = reinterpret_cast<KG int4*>(p_lev);
+        lvp[0] = p_l0;
+        lvp[1] = p_l1;
+        if (p_nprev >= 0) S.pool[p_nprev].next = p_slot;
+        KG int4* nd = reinterpret_cast<KG int4*>(&S.pool[p_slot]);
+        nd[0] = p_node[0]; nd[1] = p_node[1]; nd[2] = p_node[2]; nd[3] = p_node[3];
+        otab_final(S.otab, (int32_t)p_otpos, p_slot);
+    }
+    // a node the held-back rest wrote, as the next record's gather must see it (all four 16-B pieces)
+    KDEV void fwd_node(int32_t s, int4& c0, int4& c1, int4& c2, int4& c3) const {
+        if (!pv) return;
+        if (s == p_slot) { c0 = p_node[0]; c1 = p_node[1]; c2 = p_node[2]; c3 = p_node[3]; }
+        else if (s == p_nprev) c1.w = p_slot;               // the old tail: its next
     }
 
     // ---------------- removeOrder, KP:289-323 (victim node c0..c3; vl1: its level's qty words when
@@ -3449,14 +3475,23 @@ __global__ void __launch_bounds__(64) KME_LANES_ATTR k_match_lanes(const DevStat
                     vslot = (int32_t)r.tgt;
                     const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                     c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
+                    w.fwd_node(vslot, c0, c1, c2, c3);
                 } else if (r.tgt <= -2) {   // an order of this epoch (earlier in arrival order, so decided):
                     // the low word of its oid-table entry (position in the size word, k_route) -- its rest
                     // slot, or still pending if it did not rest
                     const uint32_t hv = (uint32_t)r.size;
-                    const uint32_t v = hv <= S.otab_mask ? reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)hv] : OT_DEAD;
+                    uint32_t v = hv <= S.otab_mask ? reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)hv] : OT_DEAD;
+                    if (w.pv && hv == w.p_otpos) v = (uint32_t)w.p_slot;   // (the held-back rest's entry)
                     if (hv > S.otab_mask) w.die(KME_E_DOMAIN, KME_D_SENTINEL_OID);   // (guard)
                     vslot = (v & OT_PENDING) ? -1 : (int32_t)v;
                     if ((uint32_t)vslot >= S.pool_cap && vslot >= 0) { w.die(KME_E_UNSUPPORTED, KME_D_SENTINEL_OID); vslot = -1; }   // (guard)
+                }
+            }
+            if (w.pv) {                                      // levels the held-back rest wrote
+                const KG int4* pl = reinterpret_cast<const KG int4*>(w.p_lev);
+                if (la == pl) { la0 = w.p_l0; la1 = w.p_l1; }
+                if (own_pre && reinterpret_cast<const KG int4*>(w.level(book_side(r.sid, is_buy), r.price)) == pl) {
+                    lo0 = w.p_l0; lo1 = w.p_l1;
                 }
             }
             if (order) w.request_spare();
@@ -3471,12 +3506,19 @@ __global__ void __launch_bounds__(64) KME_LANES_ATTR k_match_lanes(const DevStat
                 ms = la0.x;
                 lqty = mk64(la1.x, la1.y);
                 if (ms < 0) { w.die(KME_E_DOMAIN, KME_D_NPE_ORDER); tm = false; }
-                else { const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[ms]); m0 = nd[0]; m1 = nd[1]; }
+                else {
+                    const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[ms]);
+                    m0 = nd[0]; m1 = nd[1];
+                    int4 x2 = z, x3 = z;
+                    w.fwd_node(ms, m0, m1, x2, x3);
+                }
             }
             if (cxl && r.tgt <= -2 && vslot >= 0) {
                 const KG int4* nd = reinterpret_cast<const KG int4*>(&S.pool[vslot]);
                 c0 = nd[0]; c1 = nd[1]; c2 = nd[2]; c3 = nd[3];
+                w.fwd_node(vslot, c0, c1, c2, c3);
             }
+            w.flush_rest();                                  // (after both gathers are issued)
             if (w.dead) break;
             LST({ const unsigned long long t1 = lstamp(); lacc[2] += t1 - lt; lt = t1; })
             // ---- the record
@@ -3522,6 +3564,7 @@ __global__ void __launch_bounds__(64) KME_LANES_ATTR k_match_lanes(const DevStat
             n_cancel += (cxl && ok) ? 1u : 0u;
             LST({ const unsigned long long t1 = lstamp(); lacc[4] += t1 - lt; lt = t1; })
         }
+        w.flush_rest();
         if (pend && !KME_DIAG_NO_OUT) S.osort[pend_pos] = pend_a;
         LST(if (lane_id() == __ffsll((long long)__ballot(1)) - 1) for (int q = 0; q < 12; ++q) atomicAdd(&S.dbg[q], lacc[q]);)
         w.store_group();
