@@ -446,6 +446,7 @@ def main():
     tobs = [torch.full((rows, 4), -1, dtype=torch.int32, device=dev) for _ in range(2)]
     tob = tobs[0]
     tob_all = torch.zeros((world * rows, 4), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)   # torch's fills before the engine's (non-blocking) stream writes them
     # N > 1 on GPU ranks: the market data goes through the library's ABI entry (its own RCCL
     # communicator, kme_market_data_allgather on the engine stream); torch's RCCL all-gather only if
     # that communicator cannot be made, and in the gloo rehearsal
@@ -547,6 +548,7 @@ def main():
     # market data check (outside the timed region): this rank's rows of the full-range snapshot,
     # its own compact snapshot, and its block of the all-gathered one agree
     full = torch.zeros((max_sid + 1, 4), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
     eng.top_of_book(full.data_ptr())
     torch.cuda.synchronize(dev)
     md_local = bool((full[groups.long()] == tob[:len(sids)]).all().item()) and bool((tob[:len(sids), 0] >= 0).any().item())

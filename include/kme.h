@@ -189,7 +189,10 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out);
 /* MatchingEngine.close (KP:129): frees device memory. */
 kme_status kme_destroy(kme_engine* e);
 
-/* Use this HIP stream (hipStream_t) for all device work; NULL = the engine's own stream. */
+/* Use this HIP stream (hipStream_t) for all device work; NULL = the engine's own stream.  The own
+ * stream is non-blocking: nothing orders it after work the caller queued on another stream (torch's
+ * fill of an output tensor, say), so a device buffer handed to an entry below must be ready when
+ * the call is made -- synchronize first, or pass the caller's stream here. */
 kme_status kme_set_stream(kme_engine* e, void* hip_stream);
 
 /* MatchingEngine.process (KP:96-126) for n records, HOST buffers, synchronous.  In FUNDED mode the

@@ -45,16 +45,20 @@ def test_one_rank_communicator_market_data_and_rebalance(kme_mod):
     groups = torch.arange(1, n_sym + 1, dtype=torch.int32, device="cuda")
     rows = n_sym + 7                                  # padded rows: -1 / 0
     allv = torch.zeros((rows, 4), dtype=torch.int32, device="cuda")
-    comm.market_data_allgather(groups.data_ptr(), n_sym, rows, allv.data_ptr())
     own = torch.zeros((n_sym, 4), dtype=torch.int32, device="cuda")
+    # torch fills its tensors on its own stream, the engine writes them on the engine stream: nothing
+    # orders the two, so the fills must be done before the engine's kernels are queued
+    torch.cuda.synchronize()
+    comm.market_data_allgather(groups.data_ptr(), n_sym, rows, allv.data_ptr())
     eng.top_of_book_groups(groups.data_ptr(), n_sym, own.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(allv[:n_sym], own) and (own[:, 0] >= 0).any()
     assert (allv[n_sym:, :2] == -1).all() and (allv[n_sym:, 2:] == 0).all()
     before = torch.zeros(2 * n_acc, dtype=torch.int64, device="cuda")
+    after = torch.zeros(2 * n_acc, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()                          # (the fills before the engine writes, as above)
     eng.credit_state(before.data_ptr())
     comm.credit_rebalance()                           # one shard: its own bound back
-    after = torch.zeros(2 * n_acc, dtype=torch.int64, device="cuda")
     eng.credit_state(after.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(before, after) and (before[:n_acc] > 0).all()
@@ -86,6 +90,7 @@ def test_credit_resplit_keeps_every_epoch_parallel(kme_mod, oracle_mod, rebalanc
         cfg.credit_shards = NS
         engines.append(kme_mod.Engine(cfg))
     state = torch.zeros((NS, 2, n_acc), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()                          # (torch's fill before the engines write)
     chunks, refused = {}, None
     allin = W.Orders.concat([setup, body])
     bounds = [len(setup)] + [len(setup) + (k + 1) * NS * E for k in range(n_ep)]
@@ -112,6 +117,7 @@ def test_credit_resplit_keeps_every_epoch_parallel(kme_mod, oracle_mod, rebalanc
             torch.cuda.synchronize()
             # the re-split keeps the pooled bound of every account
             after = torch.zeros_like(state)
+            torch.cuda.synchronize()
             for k, eng in enumerate(engines):
                 eng.credit_state(after[k].data_ptr())
             torch.cuda.synchronize()
@@ -152,6 +158,7 @@ def test_rebalance_of_a_failed_engine_still_takes_part(kme_mod):
     assert kme_mod.STATUS[ke.value.status] == "FAILED"
     groups = torch.arange(1, n_sym + 1, dtype=torch.int32, device="cuda")
     allv = torch.zeros((n_sym, 4), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
     comm.market_data_allgather(groups.data_ptr(), n_sym, n_sym, allv.data_ptr())
     torch.cuda.synchronize()
     comm.close()
@@ -179,6 +186,7 @@ def test_credit_state_marks_absent_accounts(kme_mod):
                                                                   (W.TRANSFER, 0, 3, 0, 0, 1000)])]))
     engines[1].process(both)
     state = torch.zeros((2, 2, n_acc), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
     for k, e in enumerate(engines):
         e.credit_state(state[k].data_ptr())
     torch.cuda.synchronize()
@@ -188,6 +196,7 @@ def test_credit_state_marks_absent_accounts(kme_mod):
     for k, e in enumerate(engines):
         e.credit_adjust(state.data_ptr(), 2, k)
     after = torch.zeros_like(state)
+    torch.cuda.synchronize()
     for k, e in enumerate(engines):
         e.credit_state(after[k].data_ptr())
     torch.cuda.synchronize()

@@ -163,6 +163,7 @@ def test_top_of_book(kme_mod, oracle_mod):
     eng = _funded_engine(kme_mod, 9, accounts=64)
     eng.process(W.Orders.concat([setup, stream]))
     tob = torch.zeros((9, 4), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()                          # (torch's fill before the engine's stream writes)
     eng.top_of_book(tob.data_ptr())
     torch.cuda.synchronize()
     eng.wait()
