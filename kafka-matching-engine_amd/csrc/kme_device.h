@@ -148,6 +148,7 @@ enum Ctr : int {
                        // its quantity -- stay off)
     C_LREPAIRED,       // exact ledger: position chains the parallel pass replayed for value-key couplings
     C_LSERIAL,         // exact ledger: nonzero = the serial replay applied this epoch's ledger
+    C_GLIST,           // FUNDED, list mode: groups k_segments listed for k_match_list (glist)
     C_NCTR = 20
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
@@ -207,7 +208,8 @@ struct DevState {
     KG uint32_t* ghist;
     KG uint32_t* seg;
     KG uint32_t* gflag;               // per group: 1 = k_match takes it this epoch (then its scanned offset)
-    KG uint32_t* glist;               // those groups, in id order (k_match's dense grid); gcount[0] = how many
+    KG uint32_t* glist;               // those groups, in id order (k_match's dense grid); gcount[0] = how many.
+                                      // List mode: the groups k_segments found busy, C_GLIST of them, any order
     KG uint32_t* gcount;
     KG TradeTmp* ttmp;                // TSHARDS regions of tshard_cap, then the overflow region
     KG unsigned long long* tsh;       // TSHARDS x CTR_STRIDE words (TShardWord in each line)

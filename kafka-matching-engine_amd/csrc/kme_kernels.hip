@@ -646,25 +646,61 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
 constexpr int RADIX_DIGITS = 1 << RADIX_BITS;
 constexpr int RADIX_PER_T = RADIX_DIGITS / 256;   // digits per thread of a 256-thread block
 
-KDEV uint32_t radix_key(const RadixIO& R, int pass, int src, uint32_t k) {
-    if (pass == 0) { const int32_t g = R.key0[k]; return g < 0 ? R.none : (uint32_t)g; }
-    return R.keys[src][k];
-}
 KDEV uint32_t radix_n(const RadixIO& R) {
     if (!R.n_dev) return R.n;
     const uint32_t d = (uint32_t)*R.n_dev;
     return d < R.n ? d : R.n;
+}
+// A tile's keys (and values), RJ per thread at base + off + j * stride + lane-offset: every load is
+// issued before any is used (no branch between a load and the next one: an index past n reads
+// element 0 and is masked afterwards), so a thread has all of them in flight at once -- a load per
+// round behind its own wait made both kernels one memory round trip per round.
+template <int RJ, bool VALS>
+KDEV void radix_load(const RadixIO& R, int pass, int src, uint32_t n, uint32_t first, uint32_t stride, uint32_t* keys,
+                     uint32_t* vals) {
+    if (n == 0) {
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) { keys[j] = 0; vals[j] = 0; }
+        return;
+    }
+    // (selects, not an index into the argument's arrays: a dynamic index reads them through a vector
+    // load whose wait then lands before every later memory operation)
+    const KG uint32_t* kp = pass == 0 ? reinterpret_cast<const KG uint32_t*>(R.key0) : (src ? R.keys[1] : R.keys[0]);
+    const KG uint32_t* vp = pass == 0 ? R.val0 : (src ? R.vals[1] : R.vals[0]);
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const uint32_t k = first + j * stride;
+        keys[j] = kp[k < n ? k : 0];
+    }
+    if (VALS && vp) {
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) {
+            const uint32_t k = first + j * stride;
+            vals[j] = vp[k < n ? k : 0];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const uint32_t k = first + j * stride;
+        // pass 0: the group (int32), records without one into bucket `none`
+        if (pass == 0 && (int32_t)keys[j] < 0) keys[j] = R.none;
+        if (VALS && !vp) vals[j] = k;
+        if (k >= n) { keys[j] = 0; vals[j] = 0; }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_radix_hist(RadixIO R, int pass, int src) {
     __shared__ uint32_t h[RADIX_DIGITS];
     const int t = threadIdx.x;
     for (int q = 0; q < RADIX_PER_T; ++q) h[t + 256 * q] = 0;
-    __syncthreads();
     const uint32_t base = blockIdx.x * RADIX_TILE, n = radix_n(R);
-    for (int j = 0; j < RADIX_TILE / 256; ++j) {
-        const uint32_t k = base + j * 256 + t;
-        if (k < n) atomicAdd(&h[(radix_key(R, pass, src, k) >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1)], 1u);
+    constexpr int RJ = RADIX_TILE / 256;
+    uint32_t keys[RJ], unused[RJ];
+    radix_load<RJ, false>(R, pass, src, n, base + t, 256, keys, unused);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        if (base + j * 256 + t < n) atomicAdd(&h[(keys[j] >> (RADIX_BITS * pass)) & (RADIX_DIGITS - 1)], 1u);
     }
     __syncthreads();
     for (int q = 0; q < RADIX_PER_T; ++q) R.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
@@ -694,15 +730,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     constexpr int RJ = RADIX_TILE / 256;
     constexpr int WCH = RADIX_TILE / 4;          // elements per wavefront
     uint32_t keys[RJ], vals[RJ], wr[RJ];
-#pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-        const uint32_t k = base + w * WCH + j * 64 + lane;
-        keys[j] = 0; vals[j] = 0;
-        if (k < n) {
-            keys[j] = radix_key(R, pass, src, k);
-            vals[j] = pass == 0 ? (R.val0 ? R.val0[k] : k) : R.vals[src][k];
-        }
-    }
+    radix_load<RJ, true>(R, pass, src, n, base + w * WCH + lane, 64, keys, vals);
 #pragma unroll
     for (int q = 0; q < RADIX_DIGITS / 64; ++q) wh[w][lane + 64 * q] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -754,8 +782,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     __syncthreads();
     if (base >= n) return;
     const uint32_t cnt = n - base < (uint32_t)RADIX_TILE ? n - base : (uint32_t)RADIX_TILE;
-    KG uint32_t* okeys = R.keys[dst];
-    KG uint32_t* ovals = R.vals[dst];
+    KG uint32_t* okeys = dst ? R.keys[1] : R.keys[0];
+    KG uint32_t* ovals = dst ? R.vals[1] : R.vals[0];
     const bool last = pass == R.passes - 1 && R.rank;
     const bool pay = pass == R.passes - 1 && R.pay_src;
 #pragma unroll
@@ -767,13 +795,17 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
             okeys[pos] = key;
             ovals[pos] = val;
             if (last) R.rank[val] = (int32_t)pos;
-            if (pay) R.pay_dst[pos] = R.pay_src[val];   // a 16-B payload gathered into sorted order
+            // a 16-B payload gathered into sorted order, one element at a time: with all of a thread's
+            // gathers in flight at once the pass was slower (the exact ledger's op sort: 194 -> 259 us)
+            if (pay) R.pay_dst[pos] = R.pay_src[val];
         }
     }
 }
 
 // Group segment offsets from the sorted keys: seg[g] = first position with key >= g.
-__global__ void k_segments(DevState S, EpochIO io, int buf) {
+// list_min >= 0: the thread at a group's first record also lists the group when it has more than
+// list_min records (its record list_min places on is still the group's) -- k_match_list's work.
+__global__ void k_segments(DevState S, EpochIO io, int buf, int list_min) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = io.n;
     const uint32_t nseg = (uint32_t)S.G + 2;
@@ -786,6 +818,13 @@ __global__ void k_segments(DevState S, EpochIO io, int buf) {
     const int64_t prev = k == 0 ? -1 : (int64_t)keys[k - 1];
     const int64_t cur = k == n ? (int64_t)nseg - 1 : (int64_t)keys[k];
     for (int64_t g = prev + 1; g <= cur; ++g) S.seg[g] = k;
+    if (list_min >= 0 && k < n && cur != prev && cur < (int64_t)S.G) {
+        const uint32_t kl = k + (uint32_t)list_min;
+        if (kl < n && (int64_t)keys[kl] == cur) {
+            const unsigned long long x = atomicAdd(&S.ctr[ci(C_GLIST)], 1ull);
+            S.glist[x] = (uint32_t)cur;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ exclusive scan (DPP)
@@ -832,12 +871,29 @@ __global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x;
     const uint32_t tile = blockIdx.x, base = tile * LB_TILE;
+    // every load issued before any is used (clamped indices, masked afterwards): a conditional load
+    // per round made each round wait for its own
+    uint32_t x[LB_ITEMS];
+#pragma unroll
+    for (int j = 0; j < LB_ITEMS; ++j) {
+        const uint32_t k = base + j * 256 + t;
+        x[j] = L ? in[k < L ? k : L - 1] : 0u;
+    }
     uint32_t pre = 0;                                  // this thread's share of the tiles before this one
-    for (uint32_t q = t; q < tile; q += 256) pre += sums[q];
+    for (uint32_t q0 = 0; q0 < tile; q0 += 8 * 256) {
+        uint32_t y[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint32_t q = q0 + r * 256 + t;
+            y[r] = sums[q < tile ? q : 0];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pre += q0 + r * 256 + t < tile ? y[r] : 0u;
+    }
 #pragma unroll
     for (int j = 0; j < LB_ITEMS; ++j) {
         const uint32_t k = j * 256 + t;
-        buf[lb_pad(k)] = base + k < L ? in[base + k] : 0u;
+        buf[lb_pad(k)] = base + k < L ? x[j] : 0u;
     }
     uint32_t excl;
     (void)block_excl_scan_256(pre, wsum, excl);        // (its barriers also order the LDS stores above)
@@ -2796,14 +2852,11 @@ struct GroupWave {
 // spills) is the launch for many busy groups and few removes (the shard shapes: N = 8 +2.7% same-box);
 // cancel-heavy epochs (C5) lose up to 16% with it and two-wave epochs (C2) gain nothing, so they keep four.
 // TWO: two wavefronts per group (TwoLds): wave 0 below, wave 1 GroupWave::run_levels.
-template <bool TWO, int WAVES>
-__global__ void __launch_bounds__(TWO ? 128 : 64) __attribute__((amdgpu_waves_per_eu(WAVES)))
-k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
-                                                                      int buf, int all, int dense) {
-    __shared__ GroupLds lds;
+// One group's records (the body of k_match's block, and of each of k_match_list's iterations).
+template <bool TWO>
+KDEV __attribute__((always_inline)) void match_group(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf,
+                                                     int all, int32_t g, GroupLds& lds, TwoLds* tlsp) {
     const DevState& S = *Sp;
-    // dense: block k takes the k-th listed group (the busy ones first in the grid, the rest exit)
-    const int32_t g = dense ? (blockIdx.x < S.gcount[0] ? (int32_t)S.glist[blockIdx.x] : S.G) : (int32_t)blockIdx.x;
     if (g >= S.G) return;
     const uint32_t b = S.seg[g], e = S.seg[g + 1];
     if (b >= e || (!all && e - b <= (uint32_t)S.light_max)) return;   // empty, or a light group (k_match_lanes)
@@ -2814,7 +2867,7 @@ k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
     GroupWave w(S, lds, g);
     const int lane = lane_id();
     if constexpr (TWO) {
-        __shared__ TwoLds tls;
+        TwoLds& tls = *tlsp;
         w.tl = &tls;
         if (threadIdx.x >= 64) {                            // wave 1: the level steps
             uint32_t tpos = 0, tlim = 0;
@@ -3019,6 +3072,35 @@ k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
     if (lane == 0)
         for (int q = 0; q < ST_N; ++q) S.dbg[(size_t)g * KME_DBG_WORDS + q] += w.acc[q];
 #endif
+}
+
+template <bool TWO, int WAVES>
+__global__ void __launch_bounds__(TWO ? 128 : 64) __attribute__((amdgpu_waves_per_eu(WAVES)))
+k_match(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
+                                                                      int buf, int all, int dense) {
+    __shared__ GroupLds lds;
+    const DevState& S = *Sp;
+    // dense: block k takes the k-th listed group (the busy ones first in the grid, the rest exit)
+    const int32_t g = dense ? (blockIdx.x < S.gcount[0] ? (int32_t)S.glist[blockIdx.x] : S.G) : (int32_t)blockIdx.x;
+    if constexpr (TWO) {
+        __shared__ TwoLds tls;
+        match_group<true>(Sp, iop, buf, all, g, lds, &tls);
+    } else {
+        match_group<false>(Sp, iop, buf, all, g, lds, nullptr);
+    }
+}
+
+// List mode: the groups k_segments listed (C_GLIST of them; none at C3), a block per group in turn
+// over a grid far smaller than G.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
+k_match_list(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop, int buf, int all) {
+    __shared__ GroupLds lds;
+    const DevState& S = *Sp;
+    const uint32_t cnt = (uint32_t)S.ctr[ci(C_GLIST)];
+    for (uint32_t x = blockIdx.x; x < cnt; x += gridDim.x) {
+        match_group<false>(Sp, iop, buf, all, (int32_t)S.glist[x], lds, nullptr);
+        __syncthreads();   // (the next group's set-up rewrites the LDS state)
+    }
 }
 
 // ------------------------------------------------------------------ (2') FUNDED, light groups
@@ -3931,7 +4013,7 @@ __global__ void k_epoch_reset(DevState S) {
     const int k = threadIdx.x;
     if (k == C_ERR) S.ctr[ci(k)] = ~0ull;
     else if ((k >= C_TRADES && k <= C_TTMP) || k == C_ACCT_OPS || k == C_FALLBACK || k == C_BUSY || k == C_LIGHT ||
-             k == C_LREPAIRED || k == C_LSERIAL)
+             k == C_LREPAIRED || k == C_LSERIAL || k == C_GLIST)
         S.ctr[ci(k)] = 0ull;
 }
 
@@ -4001,7 +4083,7 @@ void launch_radix(const RadixIO& R, hipStream_t st) {
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st) {
     launch_scan2(in, out, L, sums, total, 0, st);
 }
-int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
+int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int list_min) {
     RadixIO R{};
     R.key0 = S.route_grp;
     R.val0 = nullptr;
@@ -4016,7 +4098,7 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st) {
     launch_radix(R, st);
     const int src = S.passes & 1;
     const uint32_t nthreads = (io.n + 1) > (uint32_t)S.G + 2 ? io.n + 1 : (uint32_t)S.G + 2;
-    hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src);
+    hipLaunchKernelGGL(k_segments, dim3(cdiv(nthreads, 256)), dim3(256), 0, st, S, io, src, list_min);
     return src;
 }
 // the groups k_match takes this epoch (non-empty; busy ones unless `all`), listed in id order
@@ -4045,6 +4127,9 @@ void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_de
     if (two) hipLaunchKernelGGL((k_match<true, 4>), dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
     else if (five) hipLaunchKernelGGL((k_match<false, 5>), dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
     else hipLaunchKernelGGL((k_match<false, 4>), dim3((uint32_t)S.G), dim3(64), 0, st, S_dev, io_dev, buf, all, dense);
+}
+void launch_match_list(const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st, int all, uint32_t blocks) {
+    hipLaunchKernelGGL(k_match_list, dim3(blocks), dim3(64), 0, st, S_dev, io_dev, buf, all);
 }
 void launch_match_lanes(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int buf, hipStream_t st) {
     hipLaunchKernelGGL(k_match_lanes, dim3(((uint32_t)S.G + LANE_GROUPS - 1) / LANE_GROUPS), dim3(64), 0, st, S_dev, io_dev, buf);

@@ -47,7 +47,12 @@ void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st);
 // returns the buffer index (0/1) holding the sorted input permutation
-int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st);
+// list_min >= 0: k_segments also lists the groups with more than list_min records (glist, C_GLIST)
+int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int list_min = -1);
+// k_match over the listed groups only (a grid of `blocks` looping over the list): for epochs that
+// are expected to have few or no busy groups among many (C3: a G-block k_match that finds nothing
+// costs ~16 us)
+void launch_match_list(const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st, int all, uint32_t blocks);
 // two: two wavefronts per group (the pass one segment ahead of the level step; few busy groups)
 void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_dev, int perm_buf, hipStream_t st, int all, int two, int dense,
                   int five);

@@ -51,6 +51,7 @@ struct kme_engine {
     // path a cancel-heavy stream takes often makes wave 0 wait
     uint64_t two_max = 4096;
     bool dense_grid = true;              // k_match's busy groups first in the grid (KME_DENSE_GRID=0: off, A/B)
+    bool match_list = true;              // k_match_list when no group was busy (KME_MATCH_LIST=0: off, A/B)
     bool last_cancel_heavy = false;
     uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
@@ -379,6 +380,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (const char* v = std::getenv("KME_TWO_DRAIN")) if (S.fast && std::atoi(v)) S.fast |= 2;   // diagnostics
     if (const char* v = std::getenv("KME_TWO_MAX")) e->two_max = (uint64_t)std::max(0, std::atoi(v));   // A/B diagnostics
     if (const char* v = std::getenv("KME_DENSE_GRID")) e->dense_grid = std::atoi(v) != 0;
+    if (const char* v = std::getenv("KME_MATCH_LIST")) e->match_list = std::atoi(v) != 0;
     if (funded) ALLOC(S.osort, (size_t)E + 64);   // + a dump slot per lane (k_match)
     if (funded) {
         ALLOC(S.rkeys[0], E); ALLOC(S.rkeys[1], E);
@@ -518,8 +520,13 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     launch_route(S, io, funded, st);
     phase_end(e, PH_ROUTE);
     if (funded) {
+        // list mode: with many groups and none busy in the last epoch (C3) k_segments lists the busy
+        // ones and k_match_list takes them over a small grid -- a G-block k_match finding nothing
+        // costs ~16 us of the epoch
+        const bool lanes_next = S.light_max > 0 && e->last_light != 0;
+        const bool list = e->match_list && lanes_next && e->last_busy == 0 && S.G >= 4096;
         phase_begin(e, PH_PART);
-        const int buf = launch_partition(S, io, st);
+        const int buf = launch_partition(S, io, st, list ? S.light_max : -1);
         phase_end(e, PH_PART);
         launch_acct_refresh(S, io, st);
         phase_begin(e, PH_MATCH);
@@ -528,7 +535,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         // ~30 us per epoch (measured), k_match then only finds empty work (~16 us at C3).
         // Likewise, when the last epoch had no light group (every group busy: the N = 8 shard shape,
         // C2, C5), k_match_lanes is not launched and k_match takes any light group itself.
-        const bool lanes = S.light_max > 0 && e->last_light != 0;
+        const bool lanes = lanes_next;
         const bool fork = lanes && e->last_busy != 0;
         if (fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, st));
@@ -546,7 +553,8 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         const bool dense = e->dense_grid && e->last_busy > 0 && (uint64_t)e->last_busy * 4 < (uint64_t)S.G;
         // five wavefronts per SIMD for many busy groups and few removes (k_match's WAVES)
         const bool five = !two && e->last_busy > e->two_max && !e->last_cancel_heavy;
-        launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0, five ? 1 : 0);
+        if (list) launch_match_list(e->d_S, e->d_io, buf, st, 0, 1024);
+        else launch_match(S, e->d_S, e->d_io, buf, st, lanes ? 0 : 1, two ? 1 : 0, dense ? 1 : 0, five ? 1 : 0);
         if (fork) HIP_TRY(hipStreamWaitEvent(st, e->ev_join, 0));
         phase_end(e, PH_MATCH);
         phase_begin(e, PH_COMPACT);

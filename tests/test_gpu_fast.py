@@ -165,3 +165,30 @@ def test_sweeps_over_thin_levels(kme_mod, oracle_mod, fast, seed):
     o.size = np.where(bs, np.where(big, rng.integers(4, 13, n), rng.integers(1, 4, n)), o.size).astype(np.int32)
     setup = W.funded_setup(n_acc, range(1, n_sym + 1))
     _run(kme_mod, oracle_mod, setup, o, n_sym, n_acc, fast)
+
+
+@pytest.mark.parametrize("list_mode", ["1", "0"])
+def test_busy_groups_after_an_all_light_epoch(kme_mod, oracle_mod, list_mode):
+    """List mode (k_segments lists the busy groups, k_match_list takes them over a small grid): with
+    8,192 symbols an all-light epoch (a few records per group) makes the next one run in list mode;
+    that epoch has four hot symbols (~3,000 records each), the one after runs k_match's full grid
+    again.  Alternating epochs, tape and books against the oracle (KME_MATCH_LIST=0: the full grid
+    throughout)."""
+    n_sym, n_acc, E = 8192, 512, 1 << 15
+    everyone = np.arange(1, n_sym + 1)
+    hot = np.concatenate([everyone, np.repeat(np.array([5, 77, 900, 4000]), 1200)])
+    parts = []
+    for k in range(5):
+        parts.append(W.uniform(E, n_symbols=n_sym, n_accounts=n_acc, seed=40 + k, oid_base=1 + k * E,
+                               symbols=hot if k % 2 else everyone))
+    stream = W.Orders.concat(parts)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1), transfers_per_account=4)
+    old = os.environ.get("KME_MATCH_LIST")
+    os.environ["KME_MATCH_LIST"] = list_mode
+    try:
+        _run(kme_mod, oracle_mod, setup, stream, n_sym, n_acc, True, epoch=E)
+    finally:
+        if old is None:
+            os.environ.pop("KME_MATCH_LIST")
+        else:
+            os.environ["KME_MATCH_LIST"] = old

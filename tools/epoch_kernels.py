@@ -1,11 +1,13 @@
 """Per-kernel time inside one epoch of a rocprofv3 kernel trace (the span between the last two k_emap
-launches, i.e. the last complete epoch): python3 tools/epoch_kernels.py <kernel_trace.csv> [n]"""
+launches, i.e. the last complete epoch): python3 tools/epoch_kernels.py <kernel_trace.csv> [n] [--seq]
+(--seq: also every launch of that epoch in order, with its start offset and duration)"""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+args = [a for a in sys.argv[2:] if a != "--seq"]
+top = int(args[0]) if args else 40
 by = collections.defaultdict(list)
 for r in rows:
     by[r["Kernel_Name"].split("(")[0]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
@@ -19,3 +21,7 @@ for k, v in by.items():
 for k, d in tot.most_common(top):
     print(f"{d / 1e3:9.1f} us  {k}")
 print(f"kernels {sum(tot.values()) / 1e3:.1f} us, epoch span {(t1 - t0) / 1e3:.1f} us")
+if "--seq" in sys.argv:
+    seq = sorted((s, d, k) for k, v in by.items() for s, d in v if t0 <= s < t1)
+    for s, d, k in seq:
+        print(f"  +{(s - t0) / 1e3:8.1f} us {d / 1e3:8.1f} us  {k}")

@@ -10,4 +10,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 rc=$?; echo "prof_rc=$rc"
 [ $rc -eq 0 ] || { tail -5 $OUT/bench.err; exit $rc; }
 f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
-python3 tools/epoch_kernels.py $f 40 | tee $OUT/epoch_kernels.txt
+python3 tools/epoch_kernels.py $f 40 --seq | tee $OUT/epoch_kernels.txt
