@@ -292,11 +292,17 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
     };
     if ((a == BUY || a == SELL) && out == a) {
         const int64_t aid = io.aid[i], sid = io.sid[i];
-        const int32_t price = io.price[i];
+        const int32_t price = io.price[i], size = io.size[i];
+        const uint32_t t1 = io.trade_off[i + 1];
         const uint32_t buy = a == BUY ? 1u : 0u;
-        put(aid, sid, i + 2 * t0, io.size[i], price, OP_CHECK | buy << 2);                          // KP:167-182
-        for (uint32_t q = t0; q < io.trade_off[i + 1]; ++q) {
-            const TradeRec tr = io.trades[q];
+        // each trade is loaded one step ahead of its ops' stores (a load behind this thread's stores
+        // waits for them: vmcnt counts both, in order)
+        TradeRec nx{};
+        if (t0 < t1) nx = io.trades[t0];
+        put(aid, sid, i + 2 * t0, size, price, OP_CHECK | buy << 2);                                // KP:167-182
+        for (uint32_t q = t0; q < t1; ++q) {
+            const TradeRec tr = nx;
+            if (q + 1 < t1) nx = io.trades[q + 1];
             put(tr.maid, tr.msid, i + 2 * q + 1, tr.size, 0, OP_FILL | (buy ^ 1u) << 2);             // KP:266-267
             put(aid, sid, i + 2 * q + 2, tr.size, jisub(price, tr.mprice), OP_FILL | buy << 2);      // KP:268-269
         }
@@ -772,7 +778,12 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
         const char* v = std::getenv("KME_LEDGER_GRID");
         return v ? (uint32_t)std::max(64, std::atoi(v)) : 32768u;
     }();
-    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), 8192), gl = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
+    // the grid of the grid-stride passes over the ops (KME_LEDGER_GRID_S: A/B runs)
+    static const uint32_t grid_s = [] {
+        const char* v = std::getenv("KME_LEDGER_GRID_S");
+        return v ? (uint32_t)std::max(64, std::atoi(v)) : 8192u;
+    }();
+    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), grid_s), gl = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
     hipLaunchKernelGGL(k_lchains, dim3(gl), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lr_rounds, dim3(1), dim3(1024), 0, st, S);
