@@ -371,22 +371,6 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     }
 }
 
-// With account records in the epoch (k_ledger_funded has applied them), a BUY/SELL's acct_ok is
-// decided again (k_emap read the accounts as they stood before the epoch).
-__global__ void __launch_bounds__(256) k_acct_refresh(DevState S, EpochIO io) {
-    if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
-        const int32_t a = io.action[i];
-        if (a != BUY && a != SELL) continue;
-        const int32_t g = S.route_grp[i];
-        if (g < 0) continue;
-        const int64_t aid = io.aid[i];
-        const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
-        KG int32_t* w0 = reinterpret_cast<KG int32_t*>(&S.prec[2 * (size_t)i]);
-        *w0 = (*w0 & ~(1 << 16)) | ((acct_ok ? 1 : 0) << 16);
-    }
-}
-
 // FUNDED account records in arrival order (one wavefront; skipped when the epoch has none).
 // createBalance KP:131-138; transfer KP:140-146 with the balance replaced by the reservation
 // bound: a debit is accepted only when it provably passes, otherwise KME_E_UNFUNDED.
@@ -560,8 +544,16 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     uint32_t vpos = 0;
     S.rest_slot[i] = (a == BUY || a == SELL) ? RS_PENDING : -1;
     io.n_trades[i] = 0;
-    if (funded && (a == BUY || a == SELL)) {   // routed by k_emap (acct_ok again: k_acct_refresh)
+    if (funded && (a == BUY || a == SELL)) {   // routed by k_emap
         if (S.fallback) S.cancel_tgt[i] = -1;
+        // with account records in the epoch (k_ledger_funded has applied them) acct_ok is decided
+        // again (k_emap read the accounts as they stood before the epoch); was a kernel of its own
+        if (S.ctr[ci(C_ACCT_OPS)] != 0 && S.route_grp[i] >= 0) {
+            const int64_t aid = io.aid[i];
+            const bool acct_ok = aid >= 0 && aid < S.A && S.acct_since[aid] < io.seq_base + (int64_t)i;
+            KG int32_t* w0 = reinterpret_cast<KG int32_t*>(&S.prec[2 * (size_t)i]);
+            *w0 = (*w0 & ~(1 << 16)) | ((acct_ok ? 1 : 0) << 16);
+        }
         return;
     }
     bool direct = false, ok = false, acct_ok = false;
@@ -4035,10 +4027,6 @@ void launch_epoch_reset(const DevState& S, hipStream_t st) {
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st) {
     const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
     hipLaunchKernelGGL(k_emap, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0, io_dev);
-}
-void launch_acct_refresh(const DevState& S, const EpochIO& io, hipStream_t st) {
-    const uint32_t nb = std::min<uint32_t>(cdiv(io.n > 0 ? io.n : 1, 256), STREAM_BLOCKS);
-    hipLaunchKernelGGL(k_acct_refresh, dim3(nb), dim3(256), 0, st, S, io);
 }
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_funded, dim3(1), dim3(64), 0, st, S, io);

@@ -42,7 +42,6 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
 // FUNDED pipeline
 void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);
-void launch_acct_refresh(const DevState& S, const EpochIO& io, hipStream_t st);  // acct_ok after account records
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st);

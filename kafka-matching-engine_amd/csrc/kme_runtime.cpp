@@ -528,7 +528,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         phase_begin(e, PH_PART);
         const int buf = launch_partition(S, io, st, list ? S.light_max : -1);
         phase_end(e, PH_PART);
-        launch_acct_refresh(S, io, st);
         phase_begin(e, PH_MATCH);
         // light groups one lane each, concurrently with k_match's busy ones (a second stream).  When
         // the last epoch had no busy group both go on the engine stream: the fork / join costs
