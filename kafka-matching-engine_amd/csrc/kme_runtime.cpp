@@ -72,6 +72,7 @@ struct kme_engine {
     uint32_t *d_ser_len = nullptr, *d_ser_off = nullptr, *d_ser_tmp = nullptr;
     unsigned long long* d_ser_total = nullptr;
     unsigned long long* h_ser_total = nullptr;
+    char* h_stage = nullptr;              // pinned bounce buffer of the snapshots' device reads (kStage bytes)
     std::vector<void*> allocs;
     int64_t seq_base = 0;
     // epochs in flight: submitted to the stream, not yet waited for (at most two; slot = submission
@@ -444,6 +445,7 @@ kme_status kme_destroy(kme_engine* e) {
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
     for (auto& evs : e->ev)
         for (auto& ev : evs) if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : e->ev_end) if (ev) (void)hipEventDestroy(ev);
@@ -1668,20 +1670,51 @@ static char* dup_string(const std::string& s, size_t* len) {
     return p;
 }
 
+// The snapshots' device reads: stream-ordered copies through the engine's pinned bounce buffer (no
+// pageable-destination copy on the null stream), each named in the error report.  A device fault
+// pending from earlier work is reported as such before any copy (round 5: a snapshot read of the
+// Balances once failed with an illegal-address error whose origin the plain copy could not tell).
+constexpr size_t kStage = 8ull << 20;
+static kme_status snap_begin(kme_engine* e, const char* what) {
+    HIP_TRY(hipSetDevice(e->device));
+    const hipError_t q = hipStreamSynchronize(e->stream);
+    const hipError_t d = q == hipSuccess ? hipDeviceSynchronize() : q;
+    if (d != hipSuccess) {
+        std::fprintf(stderr, "kme: %s: a device fault was pending before its reads: %s\n", what, hipGetErrorString(d));
+        return KME_E_HIP;
+    }
+    if (!e->h_stage) HIP_TRY(hipHostMalloc((void**)&e->h_stage, kStage, hipHostMallocDefault));
+    return KME_OK;
+}
+static kme_status snap_read(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    for (size_t off = 0; off < bytes; off += kStage) {
+        const size_t c = std::min(kStage, bytes - off);
+        hipError_t r = hipMemcpyAsync(e->h_stage, (const char*)src + off, c, hipMemcpyDeviceToHost, e->stream);
+        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+        if (r != hipSuccess) {
+            std::fprintf(stderr, "kme: snapshot read of %s (%zu bytes at %p + %zu) failed: %s\n", what, bytes, src, off,
+                         hipGetErrorString(r));
+            return KME_E_HIP;
+        }
+        std::memcpy((char*)dst + off, e->h_stage, c);
+    }
+    return KME_OK;
+}
+
 kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     if (!e || !text) return KME_E_INVALID;
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (kme_status r = snap_begin(e, "kme_snapshot_books")) return r;
     const uint32_t G = e->cfg.max_symbols;
     std::vector<GroupState> grp(G);
     std::vector<Level> lev((size_t)G * 2 * NLEV);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
-    HIP_TRY(hipMemcpy(ctr, e->S.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (kme_status r = snap_read(e, ctr, e->S.ctr, sizeof ctr, "counters")) return r;
     const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
     std::vector<Node> pool(nslots);
-    HIP_TRY(hipMemcpy(grp.data(), e->S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(lev.data(), e->S.lev, lev.size() * sizeof(Level), hipMemcpyDeviceToHost));
-    if (nslots) HIP_TRY(hipMemcpy(pool.data(), e->S.pool, nslots * sizeof(Node), hipMemcpyDeviceToHost));
+    if (kme_status r = snap_read(e, grp.data(), e->S.grp, G * sizeof(GroupState), "groups")) return r;
+    if (kme_status r = snap_read(e, lev.data(), e->S.lev, lev.size() * sizeof(Level), "levels")) return r;
+    if (nslots)
+        if (kme_status r = snap_read(e, pool.data(), e->S.pool, nslots * sizeof(Node), "pool")) return r;
 
     struct BookLine { int64_t key, msb, lsb; };
     struct BucketLine { int64_t ptr, first, last; };
@@ -1759,16 +1792,15 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
 kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
     if (!e || !text) return KME_E_INVALID;
     if (e->cfg.mode != KME_MODE_EXACT && !e->S.ledger_replay) return KME_E_UNSUPPORTED;
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (kme_status r = snap_begin(e, "kme_snapshot_ledger")) return r;
     const size_t lb = (size_t)e->S.bal_mask + 1, lp = (size_t)e->S.pos_mask + 1;
     std::vector<uint32_t> bst(lb);
     std::vector<int64_t> bk(lb), bv(lb);
     std::vector<PosEntry> pos(lp);
-    HIP_TRY(hipMemcpy(bst.data(), e->S.bal_state, lb * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(bk.data(), e->S.bal_key, lb * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(bv.data(), e->S.bal_val, lb * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(pos.data(), e->S.pos, lp * sizeof(PosEntry), hipMemcpyDeviceToHost));
+    if (kme_status r = snap_read(e, bst.data(), e->S.bal_state, lb * 4, "Balances states")) return r;
+    if (kme_status r = snap_read(e, bk.data(), e->S.bal_key, lb * 8, "Balances keys")) return r;
+    if (kme_status r = snap_read(e, bv.data(), e->S.bal_val, lb * 8, "Balances values")) return r;
+    if (kme_status r = snap_read(e, pos.data(), e->S.pos, lp * sizeof(PosEntry), "Positions")) return r;
     std::vector<std::pair<int64_t, int64_t>> bal;
     for (size_t h = 0; h < lb; ++h) if (bst[h] == 1) bal.push_back({bk[h], bv[h]});
     std::sort(bal.begin(), bal.end());
