@@ -144,6 +144,73 @@ static void dfree(kme_engine* e, void* p) {
     (void)hipFree(p);
 }
 
+// Host <-> device copies of the snapshot, checkpoint and restore paths: stream-ordered, through the
+// engine's pinned bounce buffer (kStage bytes, made on first use), never a pageable-host copy on the
+// null stream.  Each failure names what was being copied.  (Round 5: a snapshot's pageable read of
+// the Balances failed twice with an illegal-address error the plain copy could not attribute.)
+constexpr size_t kStage = 8ull << 20;
+static bool stage_ready(kme_engine* e) {
+    if (e->h_stage) return true;
+    if (hipHostMalloc((void**)&e->h_stage, kStage, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        e->h_stage = nullptr;
+        return false;
+    }
+    return true;
+}
+// src (device) -> dst (host); sink(chunk, bytes) instead of dst when given
+template <typename Sink>
+static bool staged_read(kme_engine* e, const void* src, size_t bytes, const char* what, Sink&& sink) {
+    if (!stage_ready(e)) return false;
+    for (size_t off = 0; off < bytes; off += kStage) {
+        const size_t c = std::min(kStage, bytes - off);
+        hipError_t r = hipMemcpyAsync(e->h_stage, (const char*)src + off, c, hipMemcpyDeviceToHost, e->stream);
+        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+        if (r != hipSuccess) {
+            std::fprintf(stderr, "kme: device read of %s (%zu bytes at %p + %zu) failed: %s\n", what, bytes, src, off,
+                         hipGetErrorString(r));
+            return false;
+        }
+        if (!sink(e->h_stage, c, off)) return false;
+    }
+    return true;
+}
+static bool staged_d2h(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    return staged_read(e, src, bytes, what, [&](const char* chunk, size_t c, size_t off) {
+        std::memcpy((char*)dst + off, chunk, c);
+        return true;
+    });
+}
+static bool staged_h2d(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    if (!stage_ready(e)) return false;
+    for (size_t off = 0; off < bytes; off += kStage) {
+        const size_t c = std::min(kStage, bytes - off);
+        std::memcpy(e->h_stage, (const char*)src + off, c);
+        hipError_t r = hipMemcpyAsync((char*)dst + off, e->h_stage, c, hipMemcpyHostToDevice, e->stream);
+        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);   // (the stage is reused next chunk)
+        if (r != hipSuccess) {
+            std::fprintf(stderr, "kme: device write of %s (%zu bytes at %p + %zu) failed: %s\n", what, bytes, dst, off,
+                         hipGetErrorString(r));
+            return false;
+        }
+    }
+    return true;
+}
+// The snapshots: a device fault pending from earlier work is reported as such before any read.
+static kme_status snap_begin(kme_engine* e, const char* what) {
+    HIP_TRY(hipSetDevice(e->device));
+    const hipError_t q = hipStreamSynchronize(e->stream);
+    const hipError_t d = q == hipSuccess ? hipDeviceSynchronize() : q;
+    if (d != hipSuccess) {
+        std::fprintf(stderr, "kme: %s: a device fault was pending before its reads: %s\n", what, hipGetErrorString(d));
+        return KME_E_HIP;
+    }
+    return stage_ready(e) ? KME_OK : KME_E_HIP;
+}
+static kme_status snap_read(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    return staged_d2h(e, dst, src, bytes, what) ? KME_OK : KME_E_HIP;
+}
+
 // ------------------------------------------------------------------ ledger table sizes
 // The most entries one epoch can add: Balances one per CREATE_BALANCE record (KP:131-138); Positions
 // one per ledger effect -- a record's checkBalance / postRemoveAdjustments, both fillOrder calls of
@@ -1157,17 +1224,10 @@ struct CkptHeader3 {
     uint64_t pool_used, n_levels, bal_live, pos_live, app_bytes;
     uint64_t _reserved[3];
 };
-constexpr size_t kChunk = 64ull << 20;   // device <-> host staging per copy
 
 // n bytes of device memory at `dev` into the writer, through a host staging buffer
-bool put_dev(kme::CkptWriter& w, const void* dev, size_t n, std::vector<char>& stage) {
-    for (size_t off = 0; off < n; off += kChunk) {
-        const size_t c = std::min(kChunk, n - off);
-        stage.resize(std::max(stage.size(), c));
-        if (hipMemcpy(stage.data(), (const char*)dev + off, c, hipMemcpyDeviceToHost) != hipSuccess) return false;
-        if (!w.write(stage.data(), c)) return false;
-    }
-    return true;
+bool put_dev(kme_engine* e, kme::CkptWriter& w, const void* dev, size_t n, const char* what) {
+    return staged_read(e, dev, n, what, [&](const char* chunk, size_t c, size_t) { return w.write(chunk, c); });
 }
 }  // namespace
 }  // extern "C"
@@ -1282,7 +1342,7 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
     // the compact stores on the device first: the set levels (counted from the group bitmaps) and
     // the live ledger entries (counted by k_ledger_live), into scratch of exactly that size
     std::vector<GroupState> grp(G);
-    HIP_TRY(hipMemcpy(grp.data(), S.grp, G * sizeof(GroupState), hipMemcpyDeviceToHost));
+    if (!staged_d2h(e, grp.data(), S.grp, G * sizeof(GroupState), "groups")) return KME_E_HIP;
     uint64_t nlev = 0;
     for (const GroupState& gs : grp)
         nlev += (uint64_t)(__builtin_popcountll(gs.bm0_lsb) + __builtin_popcountll(gs.bm0_msb) + __builtin_popcountll(gs.bm1_lsb) +
@@ -1312,21 +1372,20 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
     h.n_levels = cnt[0];
     h.bal_live = cnt[1];
     h.pos_live = cnt[2];
-    std::vector<char> stage;
     {
         kme::CkptWriter w(path);
         ok = ok && w.write(&h, sizeof h);
         ok = ok && w.write(grp.data(), G * sizeof(GroupState));
-        ok = ok && put_dev(w, d_lev, h.n_levels * sizeof(Level), stage);
-        ok = ok && put_dev(w, S.pool, h.pool_used * sizeof(Node), stage);
+        ok = ok && put_dev(e, w, d_lev, h.n_levels * sizeof(Level), "levels");
+        ok = ok && put_dev(e, w, S.pool, h.pool_used * sizeof(Node), "pool");
         if (funded) {
-            ok = ok && put_dev(w, S.acct_since, A * sizeof(int64_t), stage);
-            ok = ok && put_dev(w, S.acct_lb, A * sizeof(int64_t), stage);
-            ok = ok && put_dev(w, S.acct_demand, A * sizeof(int64_t), stage);
+            ok = ok && put_dev(e, w, S.acct_since, A * sizeof(int64_t), "accounts");
+            ok = ok && put_dev(e, w, S.acct_lb, A * sizeof(int64_t), "accounts");
+            ok = ok && put_dev(e, w, S.acct_demand, A * sizeof(int64_t), "accounts");
         }
         if (e->ledger) {
-            ok = ok && put_dev(w, d_bal, h.bal_live * 16, stage);
-            ok = ok && put_dev(w, d_pos, h.pos_live * 32, stage);
+            ok = ok && put_dev(e, w, d_bal, h.bal_live * 16, "Balances");
+            ok = ok && put_dev(e, w, d_pos, h.pos_live * 32, "Positions");
         }
         ok = ok && w.write(app, app_bytes);
         ok = ok && w.commit(app_bytes, nullptr);
@@ -1414,17 +1473,16 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     };
     hipStream_t st = e->stream;
     void *d_lev = nullptr, *d_bal = nullptr, *d_pos = nullptr;
-    bool dok = hipMemcpy(S.grp, grp.data(), grp.size(), hipMemcpyHostToDevice) == hipSuccess &&
+    bool dok = staged_h2d(e, S.grp, grp.data(), grp.size(), "groups") &&
                hipMemsetAsync(S.lev, 0, G * 2 * NLEV * sizeof(Level), st) == hipSuccess &&
                hipMalloc(&d_lev, std::max<size_t>(lev.size(), 16)) == hipSuccess &&
-               hipMemcpy(d_lev, lev.data(), lev.size(), hipMemcpyHostToDevice) == hipSuccess &&
-               (pool.empty() || hipMemcpy(S.pool, pool.data(), pool.size(), hipMemcpyHostToDevice) == hipSuccess);
+               staged_h2d(e, d_lev, lev.data(), lev.size(), "levels") &&
+               (pool.empty() || staged_h2d(e, S.pool, pool.data(), pool.size(), "pool"));
     if (dok) launch_rst_levels(S, (const Level*)d_lev, (uint32_t)h.n_levels, st);
     if (dok && funded) {
         const int64_t* a = reinterpret_cast<const int64_t*>(acct.data());
-        dok = hipMemcpy(S.acct_since, a, A * 8, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(S.acct_lb, a + A, A * 8, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(S.acct_demand, a + 2 * A, A * 8, hipMemcpyHostToDevice) == hipSuccess;
+        dok = staged_h2d(e, S.acct_since, a, A * 8, "accounts") && staged_h2d(e, S.acct_lb, a + A, A * 8, "accounts") &&
+              staged_h2d(e, S.acct_demand, a + 2 * A, A * 8, "accounts");
     }
     unsigned long long fail = 0;
     if (dok && e->ledger) {
@@ -1432,8 +1490,7 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
               hipMemsetAsync(S.pos, 0, ((size_t)S.pos_mask + 1) * sizeof(PosEntry), st) == hipSuccess &&
               hipMalloc(&d_bal, std::max<size_t>(bal.size(), 16)) == hipSuccess &&
               hipMalloc(&d_pos, std::max<size_t>(pos.size(), 16)) == hipSuccess &&
-              hipMemcpy(d_bal, bal.data(), bal.size(), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d_pos, pos.data(), pos.size(), hipMemcpyHostToDevice) == hipSuccess;
+              staged_h2d(e, d_bal, bal.data(), bal.size(), "Balances") && staged_h2d(e, d_pos, pos.data(), pos.size(), "Positions");
         if (dok) {
             launch_rst_ledger(S, d_bal, (uint32_t)h.bal_live, d_pos, (uint32_t)h.pos_live, e->d_maint, st);
             dok = hipMemcpyAsync(&fail, e->d_maint, sizeof fail, hipMemcpyDeviceToHost, st) == hipSuccess;
@@ -1668,37 +1725,6 @@ static char* dup_string(const std::string& s, size_t* len) {
     p[s.size()] = 0;
     if (len) *len = s.size();
     return p;
-}
-
-// The snapshots' device reads: stream-ordered copies through the engine's pinned bounce buffer (no
-// pageable-destination copy on the null stream), each named in the error report.  A device fault
-// pending from earlier work is reported as such before any copy (round 5: a snapshot read of the
-// Balances once failed with an illegal-address error whose origin the plain copy could not tell).
-constexpr size_t kStage = 8ull << 20;
-static kme_status snap_begin(kme_engine* e, const char* what) {
-    HIP_TRY(hipSetDevice(e->device));
-    const hipError_t q = hipStreamSynchronize(e->stream);
-    const hipError_t d = q == hipSuccess ? hipDeviceSynchronize() : q;
-    if (d != hipSuccess) {
-        std::fprintf(stderr, "kme: %s: a device fault was pending before its reads: %s\n", what, hipGetErrorString(d));
-        return KME_E_HIP;
-    }
-    if (!e->h_stage) HIP_TRY(hipHostMalloc((void**)&e->h_stage, kStage, hipHostMallocDefault));
-    return KME_OK;
-}
-static kme_status snap_read(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
-    for (size_t off = 0; off < bytes; off += kStage) {
-        const size_t c = std::min(kStage, bytes - off);
-        hipError_t r = hipMemcpyAsync(e->h_stage, (const char*)src + off, c, hipMemcpyDeviceToHost, e->stream);
-        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
-        if (r != hipSuccess) {
-            std::fprintf(stderr, "kme: snapshot read of %s (%zu bytes at %p + %zu) failed: %s\n", what, bytes, src, off,
-                         hipGetErrorString(r));
-            return KME_E_HIP;
-        }
-        std::memcpy((char*)dst + off, e->h_stage, c);
-    }
-    return KME_OK;
 }
 
 kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
