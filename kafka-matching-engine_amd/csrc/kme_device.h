@@ -219,6 +219,7 @@ struct DevState {
     int32_t lpar, lpasses, lhbits, _lpad2;
     uint32_t lr_cap, lx_cap, lc_cap, lrounds;
     uint64_t lvk_mask;
+    uint32_t lvk_tag, _lpad3;         // this epoch's tag in the value-key table (1..65535: no per-epoch clear)
     KG uint32_t* lcnt;                // per record: its ops, then their offset
     KG uint32_t* lscan;               // scan scratch
     KG uint32_t* lk0;                 // per op (arrival order): sort key aid << 8 | hash8(sid)

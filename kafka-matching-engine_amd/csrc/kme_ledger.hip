@@ -262,6 +262,10 @@ KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
 // maker's key) and taker fill, an accepted cancel's postRemoveAdjustments.
 __global__ void __launch_bounds__(256) k_lcount(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    // the epoch's counters and per-account deltas start at 0 (was three fills before this launch)
+    if (i < (uint32_t)(LC_N * CTR_STRIDE)) S.lctr[i] = 0;
+    if (i < (uint32_t)(LPOSC_LINES * CTR_STRIDE)) S.lposc[i] = 0;
+    for (int64_t a = i; a < S.A; a += (int64_t)gridDim.x * blockDim.x) S.ldelta[a] = 0;
     if (i >= io.n) return;
     uint32_t c = 0;
     if (!lskip(S)) {
@@ -572,20 +576,36 @@ __global__ void __launch_bounds__(1024) k_lr_rounds(DevState S) {
 // different keys sends the epoch to the serial replay).
 namespace {
 KDEV uint64_t vkey_hash(int64_t k0, int64_t k1) { return mix64((uint64_t)k0 * 0xc2b2ae3d27d4eb4full ^ mix64((uint64_t)k1 + 1)) | 1ull; }
+// The table is not cleared between epochs: an entry's hash word carries the epoch's tag in its low 16
+// bits (S.lvk_tag, 1..65535; the host clears the table when the tag wraps) and its max word the tag
+// above the arrival number (vk_last), so an entry of an earlier epoch reads as empty and loses every
+// atomicMax.
+KDEV uint64_t vk_word(const DevState& S, uint64_t h) { return (h & ~0xFFFFull) | (uint64_t)S.lvk_tag; }
+KDEV bool vk_live(const DevState& S, unsigned long long cur) { return cur != 0 && (cur & 0xFFFFull) == S.lvk_tag; }
+KDEV unsigned long long vk_last(const DevState& S, uint32_t es) {
+    return ((unsigned long long)S.lvk_tag << 40) | ((unsigned long long)es + 1);
+}
 // The slot of key hash h (insert: claimed when absent), or -1.  A position value is a small pair, so
 // a few keys take most value writes of an epoch: the probe reads before it claims (no atomic on a
 // hot key's line unless the slot is empty).
 KDEV int64_t vk_slot(const DevState& S, uint64_t h, bool insert, bool* inserted = nullptr) {
+    const uint64_t hx = vk_word(S, h);
     uint64_t p = h & S.lvk_mask;
     for (uint32_t probes = 0; probes < 4096; ++probes) {
         KG unsigned long long* e = reinterpret_cast<KG unsigned long long*>(&S.lvk[p]);
         unsigned long long cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == 0 && insert) {
-            cur = atomicCAS(e, 0ull, (unsigned long long)h);
-            if (cur == 0 && inserted) *inserted = true;
+        if (!vk_live(S, cur)) {
+            if (!insert) return -1;
+            const unsigned long long prev = atomicCAS(e, cur, (unsigned long long)hx);
+            if (prev == cur) {
+                if (inserted) *inserted = true;
+                return (int64_t)p;
+            }
+            cur = prev;                                  // another writer's claim of this epoch
+            if (!vk_live(S, cur)) continue;              // (cannot happen: only claims change a word; the
+                                                         // probe cap bounds the retries regardless)
         }
-        if (cur == h || (insert && cur == 0)) return (int64_t)p;
-        if (cur == 0) return -1;
+        if (cur == hx) return (int64_t)p;
         p = (p + 1) & S.lvk_mask;
     }
     return -1;
@@ -615,7 +635,7 @@ __global__ void __launch_bounds__(256) k_lvw_classify(DevState S) {
         const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), true, &ins);
         if (v < 0) { lfallback(S); return; }
         if (ins) { S.lvk[v].z = (unsigned long long)w.x; S.lvk[v].w = (unsigned long long)w.y; }   // the key, by its inserter
-        vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[v]) + 1, (unsigned long long)es + 1);
+        vk_max(reinterpret_cast<KG unsigned long long*>(&S.lvk[v]) + 1, vk_last(S, es));
     }
 }
 // Every writer's key against the one its hash slot holds: two keys with one hash send the epoch to
@@ -668,7 +688,7 @@ __global__ void __launch_bounds__(256) k_lcommit(DevState S) {
         if (!(meta & 3u) || S.lvw_tgt[p] >= 0) continue;
         const long4 w = S.lvw[p];
         const int64_t v = vk_slot(S, vkey_hash(w.x, w.y), false);
-        if (v < 0 || S.lvk[v].y != (unsigned long long)S.lsrt[p].es + 1) continue;
+        if (v < 0 || S.lvk[v].y != vk_last(S, S.lsrt[p].es)) continue;
         int32_t free;
         uint32_t fst;
         const int32_t h = pos_lookup_free(S, w.x, w.y, free, fst);
@@ -745,13 +765,15 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     const uint32_t n = io.n;
     auto cdiv = [](uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); };
     const uint64_t nops = (uint64_t)n + 2ull * max_trades;    // (ops: at most one per arrival number)
-    (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
-    (void)hipMemsetAsync(S.lposc, 0, sizeof(unsigned long long) * LPOSC_LINES * CTR_STRIDE, st);
-    // (lvw_meta and lxmark of the epoch's ops are cleared by k_lgen: the ops fill [0, count) exactly)
-    (void)hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * (size_t)S.A, st);
-    (void)hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st);
-    if (n == 0) return;
-    hipLaunchKernelGGL(k_lcount, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
+    // (lvw_meta and lxmark of the epoch's ops are cleared by k_lgen: the ops fill [0, count) exactly;
+    // the value-key table by its tag, S.lvk_tag; the counters and deltas by k_lcount)
+    if (n == 0) {
+        (void)hipMemsetAsync(S.lctr, 0, sizeof(unsigned long long) * LC_N * CTR_STRIDE, st);
+        (void)hipMemsetAsync(S.lposc, 0, sizeof(unsigned long long) * LPOSC_LINES * CTR_STRIDE, st);
+        return;
+    }
+    static_assert(LC_N * CTR_STRIDE <= 256 && LPOSC_LINES * CTR_STRIDE <= 1024, "k_lcount's first threads clear them");
+    hipLaunchKernelGGL(k_lcount, dim3(std::max<uint32_t>(cdiv(n, 256), 4)), dim3(256), 0, st, S, io);
     // offsets (in place) and the op count (LC_OPS, low word)
     launch_excl_scan(S.lcnt, S.lcnt, n, S.lscan, reinterpret_cast<uint32_t*>(S.lctr + ci(LC_OPS)), st);
     hipLaunchKernelGGL(k_lgen, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);

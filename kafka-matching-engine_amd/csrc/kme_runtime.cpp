@@ -52,6 +52,7 @@ struct kme_engine {
     uint64_t two_max = 4096;
     bool dense_grid = true;              // k_match's busy groups first in the grid (KME_DENSE_GRID=0: off, A/B)
     bool match_list = true;              // k_match_list when no group was busy (KME_MATCH_LIST=0: off, A/B)
+    uint32_t lvk_next_tag = 1;           // the exact ledger's next value-key table tag (DevState::lvk_tag)
     bool last_cancel_heavy = false;
     uint64_t last_light = 1;             // k_match_lanes wavefronts with a group in the last epoch (C_LIGHT)
     hipStream_t stream = nullptr;
@@ -411,6 +412,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lgap, (size_t)cfg->max_accounts / 256 + 4);
             ALLOC(S.ldelta, cfg->max_accounts);
             ALLOC(S.lvk, vk);
+            HIP_TRY(hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * vk, e->stream));   // (tags from 1 on)
             ALLOC(S.lx, S.lx_cap); ALLOC(S.lxn, S.lx_cap);
             ALLOC(S.lxmark, nops);
             ALLOC(S.lrun, S.lr_cap);
@@ -636,7 +638,15 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         }
         if (S.ledger_replay) {
             phase_begin(e, PH_REPLAY);
-            if (S.lpar) launch_ledger_parallel(S, io, e->cfg.max_trades, st);
+            if (S.lpar) {
+                // the value-key table's tag for this epoch; the table is cleared when the tag wraps
+                if (e->lvk_next_tag > 0xFFFFu) {
+                    HIP_TRY(hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * ((size_t)S.lvk_mask + 1), st));
+                    e->lvk_next_tag = 1;
+                }
+                e->S.lvk_tag = e->lvk_next_tag++;
+                launch_ledger_parallel(S, io, e->cfg.max_trades, st);
+            }
             launch_ledger_replay(e->d_S, e->d_io, st);   // (works only when the parallel pass fell back)
             phase_end(e, PH_REPLAY);
         }
