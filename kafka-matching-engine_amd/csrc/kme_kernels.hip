@@ -681,12 +681,13 @@ KDEV void radix_load(const RadixIO& R, int pass, int src, uint32_t n, uint32_t f
     }
 }
 
+template <int TILE>
 __global__ void __launch_bounds__(256) k_radix_hist(RadixIO R, int pass, int src) {
     __shared__ uint32_t h[RADIX_DIGITS];
     const int t = threadIdx.x;
     for (int q = 0; q < RADIX_PER_T; ++q) h[t + 256 * q] = 0;
-    const uint32_t base = blockIdx.x * RADIX_TILE, n = radix_n(R);
-    constexpr int RJ = RADIX_TILE / 256;
+    const uint32_t base = blockIdx.x * TILE, n = radix_n(R);
+    constexpr int RJ = TILE / 256;
     uint32_t keys[RJ], unused[RJ];
     radix_load<RJ, false>(R, pass, src, n, base + t, 256, keys, unused);
     __syncthreads();
@@ -707,20 +708,21 @@ KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
 // round, lane) and counts its digits in its own LDS row round by round (match-any over the digit
 // bits; the first lane of each digit adds the run), so the only block barriers are the few
 // between the counting, the per-digit offsets and the placement.
+template <int TILE>
 __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int src) {
     static_assert(RADIX_DIGITS == 512, "two digits per thread");
-    static_assert(RADIX_TILE % 256 == 0, "whole rounds");
+    static_assert(TILE % 256 == 0, "whole rounds");
     __shared__ uint32_t wh[4][RADIX_DIGITS];     // wavefront w's count of digit d, then its first local slot
     __shared__ uint32_t gdelta[RADIX_DIGITS];    // digit d's global offset minus its local start
-    __shared__ uint32_t lkey[RADIX_TILE], lval[RADIX_TILE];
+    __shared__ uint32_t lkey[TILE], lval[TILE];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t base = blockIdx.x * RADIX_TILE, n = radix_n(R);
+    const uint32_t base = blockIdx.x * TILE, n = radix_n(R);
     const int dst = src ^ 1;
     const int shift = RADIX_BITS * pass;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    constexpr int RJ = RADIX_TILE / 256;
-    constexpr int WCH = RADIX_TILE / 4;          // elements per wavefront
+    constexpr int RJ = TILE / 256;
+    constexpr int WCH = TILE / 4;                // elements per wavefront
     uint32_t keys[RJ], vals[RJ], wr[RJ];
     radix_load<RJ, true>(R, pass, src, n, base + w * WCH + lane, 64, keys, vals);
 #pragma unroll
@@ -773,7 +775,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     }
     __syncthreads();
     if (base >= n) return;
-    const uint32_t cnt = n - base < (uint32_t)RADIX_TILE ? n - base : (uint32_t)RADIX_TILE;
+    const uint32_t cnt = n - base < (uint32_t)TILE ? n - base : (uint32_t)TILE;
     KG uint32_t* okeys = dst ? R.keys[1] : R.keys[0];
     KG uint32_t* ovals = dst ? R.vals[1] : R.vals[0];
     const bool last = pass == R.passes - 1 && R.rank;
@@ -4056,17 +4058,22 @@ static void launch_scan2(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t
 }
 // Stable LSD radix sort of (key, value) pairs, R.passes digit passes; the result is in keys / vals
 // [R.passes & 1].
-void launch_radix(const RadixIO& R, hipStream_t st) {
-    const uint32_t ntiles = cdiv(R.n > 0 ? R.n : 1, RADIX_TILE);
+template <int TILE>
+static void radix_passes(const RadixIO& R, hipStream_t st) {
+    const uint32_t ntiles = cdiv(R.n > 0 ? R.n : 1, TILE);
     int src = 0;
     for (int pass = 0; pass < R.passes; ++pass) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(256), 0, st, R, pass, src);
+        hipLaunchKernelGGL(k_radix_hist<TILE>, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
         const uint32_t L = RADIX_DIGITS * ntiles;
         launch_scan2(R.ghist, R.ghist, L, R.ghist + L, nullptr, 0, st);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(256), 0, st, R, pass, src);
+        hipLaunchKernelGGL(k_radix_scatter<TILE>, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         src ^= 1;
     }
+}
+void launch_radix(const RadixIO& R, hipStream_t st) {
+    if (R.small || R.n <= RADIX_SMALL_N) radix_passes<RADIX_TILE_SMALL>(R, st);
+    else radix_passes<RADIX_TILE>(R, st);
 }
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st) {
     launch_scan2(in, out, L, sums, total, 0, st);

@@ -12,6 +12,10 @@ namespace kme {
 // inputs per partition tile (256 threads x 32): each digit's run of a tile ~16 keys (64 B) at 512
 // digits; 4,096 left 32-B runs (same-box A/B: partition 0.128 -> 0.119 ms at C3, 74 KB of LDS)
 constexpr int RADIX_TILE = KME_RADIX_TILE;
+// small sorts (at most RADIX_SMALL_N keys: the drop-in's 65,536-record epochs) take 2,048-key tiles --
+// 32 blocks instead of 8 per pass; buffers sized per tile are sized for these
+constexpr int RADIX_TILE_SMALL = 2048;
+constexpr uint32_t RADIX_SMALL_N = 1u << 18;
 constexpr int RADIX_BITS = 9;        // digit width of the partition passes
 constexpr int POOL_CHUNK = 64;       // node slots a group takes from the global bump at a time
 constexpr int kDefaultLightMax = 128;  // DevState::light_max default (KME_LIGHT_MAX overrides)
@@ -34,6 +38,7 @@ struct RadixIO {
     uint32_t n;
     const KG unsigned long long* n_dev;
     int passes;
+    int small;                       // 2,048-key tiles (a small sort; n may be a capacity far above it)
 };
 void launch_radix(const RadixIO& R, hipStream_t st);
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st);

@@ -398,7 +398,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             if (const char* v = std::getenv("KME_LEDGER_ROUNDS")) S.lrounds = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
             const uint64_t vk = pow2_at_least(std::min<uint64_t>(2 * nops, 1ull << 22));
             S.lvk_mask = vk - 1;
-            const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE - 1) / RADIX_TILE);
+            const uint64_t lh = (uint64_t)(1 << RADIX_BITS) * ((nops + RADIX_TILE_SMALL - 1) / RADIX_TILE_SMALL);
             ALLOC(S.lcnt, E);
             ALLOC(S.lscan, E / 4096 + 64);
             ALLOC(S.lk0, nops);
@@ -458,7 +458,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
         ALLOC(S.ttmp, ttmp_total);
         ALLOC(S.tsh, (size_t)TSHARDS * CTR_STRIDE);
     }
-    const uint64_t ntiles = (E + RADIX_TILE - 1) / RADIX_TILE;
+    const uint64_t ntiles = (E + RADIX_TILE_SMALL - 1) / RADIX_TILE_SMALL;
     ALLOC(S.ghist, (size_t)(1 << RADIX_BITS) * ntiles + 2 * (E / 2048 + 16) + 4096);
     ALLOC(S.seg, (size_t)G + 2);
     ALLOC(S.gflag, (size_t)G + 1); ALLOC(S.glist, (size_t)G + 1); ALLOC(S.gcount, 64 + (size_t)G / 4096 + 64);
