@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define KME_ABI_VERSION 6
+#define KME_ABI_VERSION 7
 
 /* Order.action codes (KP:65-75). */
 enum kme_action {
@@ -59,15 +59,22 @@ enum kme_domain {
     KME_D_NPE_BOOK = 6,      /* book missing for a resting order (KP:294) */
     KME_D_PRICE = 7,         /* a resting price outside 0..126 aliases buckets across symbols (KP:379-416) */
     KME_D_DUP_OID = 8,       /* BUY/SELL reuses the oid of a live order (KP:221 would corrupt lists) */
-    KME_D_FUNDED_RANGE = 9,  /* FUNDED mode: BUY/SELL price outside 0..100 or size < 0 */
-    KME_D_SENTINEL_OID = 10, /* reserved (no longer raised: the oid tables have no sentinel oids) */
+    KME_D_FUNDED_RANGE = 9,  /* FUNDED mode without KME_FLAG_SERIAL_FALLBACK: BUY/SELL price outside
+                                0..100 or size < 0 (with the flag such an epoch runs serially) */
+    KME_D_SENTINEL_OID = 10, /* reserved (no longer raised) */
     KME_D_CAP_POOL = 11, KME_D_CAP_OIDTAB = 12, KME_D_CAP_TRADES = 13, KME_D_CAP_SYMBOL = 14,
     KME_D_CAP_ACCOUNT = 15, KME_D_CAP_LEDGER = 16, KME_D_CAP_EPOCH = 17,
-    KME_D_UNPROVEN = 18      /* KME_E_UNFUNDED of the epoch as a whole: the funded proof failed, so
+    KME_D_UNPROVEN = 18,     /* KME_E_UNFUNDED of the epoch as a whole: the funded proof failed, so
                                 none of its records took effect (error_index -1, n_effective 0),
                                 whatever other fault the epoch holds further on -- except a fault of
                                 record 0 itself, which is reported instead (the reference throws
                                 there whatever the ledger holds; nothing takes effect either way) */
+    KME_D_SID_RANGE = 19,    /* ADD_SYMBOL of sid = Long.MIN_VALUE or |sid| >= 2^55: the bucket pointer
+                                (sid << 8) | price (KP:379-381) then aliases other books' buckets */
+    KME_D_GUARD_OTPOS = 20,  /* internal consistency check (k_match_lanes): an oid-table position
+                                outside the table; never expected (a bug report, not an input fault) */
+    KME_D_GUARD_SLOT = 21    /* internal consistency check (k_match_lanes): a node slot outside the
+                                pool; never expected */
 };
 
 /* Engine modes.
@@ -99,6 +106,15 @@ enum kme_mode { KME_MODE_EXACT = 0, KME_MODE_FUNDED = 1 };
  *   which the funded bounds restart from the exact balances.  kme_epoch_status.serial_fallback
  *   tells which epochs took that path. */
 #define KME_FLAG_SERIAL_FALLBACK 2u
+/* With KME_FLAG_SERIAL_FALLBACK the FUNDED engine takes every record the reference takes: besides an
+ *   unprovable epoch, an epoch runs serially when it holds a BUY/SELL priced outside 0..100 or of
+ *   negative size, a record of an account id outside [0, max_accounts), a record on a sparse symbol
+ *   (|sid| >= max_symbols, kme_config.max_sparse_symbols) or on a symbol whose book holds such an order
+ *   (a level above 100, a negative size) -- the parallel matchers keep prices 0..100 and sizes >= 0.
+ * KME_FLAG_REFUSE_SERIAL (FUNDED, without SERIAL_FALLBACK; kme_multi sets it on its shards when it can
+ *   consolidate): such an epoch is refused as unproven (KME_E_UNFUNDED / KME_D_UNPROVEN, nothing of it
+ *   takes effect) instead of faulting, so that the caller can hand it to an engine that takes it. */
+#define KME_FLAG_REFUSE_SERIAL 4u
 
 typedef struct kme_config {
     uint32_t abi_version;      /* KME_ABI_VERSION */
@@ -123,7 +139,13 @@ typedef struct kme_config {
                                   (k_match_lanes), a busier one by a whole wavefront (k_match); both
                                   run concurrently.  0 = engine default (128), < 0 = wavefronts only.
                                   Results are identical either way. */
+    uint32_t max_sparse_symbols; /* symbols with |sid| >= max_symbols the stores hold (KP:184-191 takes any
+                                  long): 0 = the default, 4,096 for EXACT mode and FUNDED with
+                                  KME_FLAG_SERIAL_FALLBACK, none otherwise; KME_SPARSE_NONE = none.
+                                  Only the serial engine handles them (max_symbols + sparse <= 2^24). */
+    uint32_t _reserved;
 } kme_config;
+#define KME_SPARSE_NONE 0xFFFFFFFFu
 
 /* One epoch of input records, structure-of-arrays (Order fields KP:451-456).  The reference's
  * optional next/prev input fields must be null and are not carried. */
@@ -326,7 +348,8 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len);
 kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len);
 void kme_free(void* p);
 
-/* Top-of-book market data per symbol group g (device buffer of max_symbols entries, async):
+/* Top-of-book market data per symbol group g (device buffer of max_symbols entries, async; the sparse
+ * symbols of kme_config.max_sparse_symbols are not part of it):
  * {best bid price, best ask price, bid qty, ask qty} as int32 (-1 / 0 when a side is empty).
  * Bid = highest price in book +g, ask = lowest price in book -g (book 0 is shared). */
 typedef struct kme_tob { int32_t bid_px, ask_px, bid_qty, ask_qty; } kme_tob;

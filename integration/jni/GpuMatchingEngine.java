@@ -44,9 +44,13 @@
 //
 // Faults: the records before a fault took effect and are forwarded (as the reference's per-record
 // commit would have, KP:97, 124-125); then the processor fails like the reference's stream thread.
-// The default flags (EXACT_LEDGER | SERIAL_FALLBACK) give the reference's result for any stream, so
-// KME_E_UNFUNDED cannot occur; in a configuration without SERIAL_FALLBACK it is fatal here too (its
-// records were not processed, and a processor cannot hand records back to Kafka).
+// The default flags (EXACT_LEDGER | SERIAL_FALLBACK) give the reference's result for every record it
+// takes -- any price and size, any account id, any symbol id below 2^55 (sparse ones up to the
+// configured 4,096), the epochs the parallel path cannot prove or stage running on the serial engine
+// (include/kme.h) -- so KME_E_UNFUNDED cannot occur; the faults left are the reference's own (its NPEs,
+// a removeAllOrders that never returns) and capacities.  In a configuration without SERIAL_FALLBACK
+// KME_E_UNFUNDED is fatal here too (its records were not processed, and a processor cannot hand
+// records back to Kafka).
 import java.io.File;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;

@@ -64,7 +64,8 @@ struct alignas(64) GroupState {
     uint64_t bm0_lsb, bm0_msb;     // book +g  (KP:391-404 layout: lsb = prices 0..62, msb = 63..126)
     uint64_t bm1_lsb, bm1_msb;     // book -g
     int32_t exists, free_head, chunk_next, chunk_end;
-    int32_t _pad[4];
+    int32_t nneg;                  // resting orders of negative size (only the serial engine rests them)
+    int32_t _pad[3];
 };
 static_assert(sizeof(GroupState) == 64, "GroupState");
 
@@ -149,7 +150,9 @@ enum Ctr : int {
     C_LREPAIRED,       // exact ledger: position chains the parallel pass replayed for value-key couplings
     C_LSERIAL,         // exact ledger: nonzero = the serial replay applied this epoch's ledger
     C_GLIST,           // FUNDED, list mode: groups k_segments listed for k_match_list (glist)
-    C_NCTR = 20
+    C_ODD,             // persistent: nonzero once the serial engine made a book the FUNDED matchers cannot
+                       // take (a level above price 100, a negative-size order: GroupState::nneg)
+    C_NCTR = 21
 };
 constexpr int CTR_STRIDE = 16;                 // u64 words per counter line
 constexpr int ci(int k) { return k * CTR_STRIDE; }
@@ -244,6 +247,14 @@ struct DevState {
     KG uint32_t* lchg;                // the value writes a repair round changed
     KG unsigned long long* lctr;      // LC_N x CTR_STRIDE words
     KG unsigned long long* lposc;     // 64 x CTR_STRIDE words: positions k_linsert created (k_lbalances folds them)
+    // Sparse symbols: the reference takes any long sid (KP:184-191, 201).  Groups G .. G + Gs - 1 of the
+    // stores above hold symbols with |sid| >= G, named by gsid (open addressing on |sid|, slot k =
+    // group G + k, 0 = free).  Only the serial engine (k_serial) touches them: a FUNDED epoch with a
+    // record on one runs serially (KME_FLAG_SERIAL_FALLBACK).
+    int32_t Gs;
+    int32_t refuse;                   // KME_FLAG_REFUSE_SERIAL: what needs the serial engine is refused
+                                      // as an unproven epoch instead (kme_multi's shards)
+    KG int64_t* gsid;
 };
 
 struct EpochIO {

@@ -100,4 +100,7 @@ struct CkptReader {
 // fsync of the directory that holds `path` (a rename is durable only then)
 bool sync_dir_of(const std::string& path);
 
+// tests only (kme_runtime.cpp): env KME_TEST_FAIL == what
+bool test_hook_fail(const char* what);
+
 }  // namespace kme

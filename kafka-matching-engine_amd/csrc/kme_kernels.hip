@@ -125,6 +125,19 @@ KDEV int32_t group_of(int64_t sid, int32_t G) {
     int64_t a = sid < 0 ? -sid : sid;
     return a < (int64_t)G ? (int32_t)a : -1;
 }
+// A record only the serial engine takes (a BUY/SELL priced outside 0..100 or of negative size, an
+// account id outside [0, A), a sparse symbol, a book holding such an order): with
+// KME_FLAG_SERIAL_FALLBACK the epoch runs serially (k_serial, as an unprovable one); with
+// KME_FLAG_REFUSE_SERIAL it is refused as unproven -- nothing of it takes effect, KME_E_UNFUNDED at
+// index 0 (kme_multi then hands the stream to its consolidated engine).
+KDEV bool serial_capable(const DevState& S) { return S.fallback || S.refuse; }
+KDEV void need_serial(const DevState& S) {
+    if (S.fallback) { if (!S.ctr[ci(C_FALLBACK)]) atomicOr(&S.ctr[ci(C_FALLBACK)], 1ull); }
+    else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_UNPROVEN, 0);
+}
+// a cancel of an order of this epoch on a symbol the parallel path cannot name (a sparse one): its
+// group is resolved by k_serial (route_grp; the target stays in cancel_tgt)
+constexpr int32_t GRP_RESOLVE = -3;
 
 // ------------------------------------------------------------------ DPP wavefront scans
 // Inclusive scan over 64 lanes: row_shr 1,2,4,8 inside each 16-lane row, then row_bcast:15 and
@@ -296,7 +309,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
     for (uint32_t i = t0; i < io.n; i += gridDim.x * blockDim.x) {
         const int32_t a = io.action[i];
         n_orders += (a == BUY || a == SELL || a == CANCEL) ? 1u : 0u;
-        if ((a == BUY || a == SELL) && io.size[i] == 0 && !S.ctr[ci(C_SIZE0)]) atomicOr(&S.ctr[ci(C_SIZE0)], 1ull);
+        if ((a == BUY || a == SELL) && io.size[i] <= 0 && !S.ctr[ci(C_SIZE0)]) atomicOr(&S.ctr[ci(C_SIZE0)], 1ull);
         if (a == BUY || a == SELL) {
             // the order's oid-table entry (pending until k_table); on the way, the duplicate-oid
             // guard: another BUY/SELL of this epoch, or a live resting order, with this oid
@@ -305,10 +318,24 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
             const uint32_t fp = oid_fp(oid);
             const unsigned long long ent = hentry(fp, OT_PENDING | i);
             uint32_t h = (uint32_t)mix64((uint64_t)oid) & S.otab_mask;
-            bool placed = false;
+            bool placed = false, adopted = false;
+            uint32_t pos = OT_DEAD;
             for (uint32_t probes = 0; KME_DIAG_EMAP_NOCAS < 2 && probes <= (KME_DIAG_EMAP_NOCAS ? 0u : S.otab_mask); ++probes) {
-                const unsigned long long prev = atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent);
-                if (prev == 0) { S.epos[i] = h; placed = true; break; }
+                // (after adopting an entry: plain loads, the rest of the probe only looks for duplicates)
+                const unsigned long long prev = adopted ? (unsigned long long)S.otab[h] : atomicCAS((unsigned long long*)&S.otab[h], 0ull, ent);
+                if (prev == 0) {
+                    if (!adopted) { pos = h; placed = true; }
+                    break;
+                }
+                if (prev == ent && !adopted) {
+                    // an earlier epoch's pending entry of record i with this fingerprint (an order of
+                    // that epoch that did not rest, the same oid again at the same index): it becomes
+                    // this order's entry.  A second one further on would be the one k_route's cancel
+                    // probe finds after the first -- k_match_lanes then read a never-finalised entry.
+                    pos = h; placed = adopted = true;
+                    h = (h + 1) & S.otab_mask;
+                    continue;
+                }
                 const uint32_t v = (uint32_t)prev;
                 if ((uint32_t)(prev >> 32) == fp && v != OT_DEAD) {
                     if (v & OT_PENDING) {   // (an earlier epoch's entry counts only as a fact of this
@@ -327,13 +354,20 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                 }
                 h = (h + 1) & S.otab_mask;
             }
-            if (placed) ++n_ins;
-            else S.epos[i] = OT_DEAD;
+            S.epos[i] = pos;
+            if (placed && !adopted) ++n_ins;
             if (funded) {
                 const int32_t price = io.price[i], size = io.size[i];
                 const int64_t aid = io.aid[i];
-                if (price < 0 || price > 100 || size < 0) raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
-                else if (aid >= 0 && aid < S.A && !KME_DIAG_EMAP_NONEED) {   // the account's reservation need
+                const bool aid_in = aid >= 0 && aid < S.A;
+                // outside the parallel path's domain: prices 0..100, sizes >= 0 (the proof's risk
+                // bound, KP:172-176; the matchers' level staging), dense account and symbol ids
+                const bool range_bad = price < 0 || price > 100 || size < 0;
+                if (S.fallback && (!aid_in || (S.Gs > 0 && group_of(io.sid[i], S.G) < 0))) need_serial(S);
+                if (range_bad) {
+                    if (serial_capable(S)) need_serial(S);
+                    else raise_thread(S.ctr, KME_E_DOMAIN, KME_D_FUNDED_RANGE, i);
+                } else if (aid_in && !KME_DIAG_EMAP_NONEED) {   // the account's reservation need
                     const int64_t risk = (a == BUY) ? (int64_t)size * price : (int64_t)size * (100 - price);
                     atomicAdd((unsigned long long*)&S.acct_need[aid], (unsigned long long)risk);
                 }
@@ -353,7 +387,7 @@ __global__ void __launch_bounds__(256) k_emap(DevState S, EpochIO io, int funded
                     KG int4* p = &S.prec[2 * (size_t)i];
                     if (!KME_DIAG_EMAP_NOPREC) {
                         p[0] = make_int4(w0, size, (int32_t)(uint32_t)oid, (int32_t)((uint64_t)oid >> 32));
-                        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), placed ? (int32_t)h : -1, 0);
+                        p[1] = make_int4((int32_t)(uint32_t)aid, (int32_t)((uint64_t)aid >> 32), placed ? (int32_t)pos : -1, 0);
                     }
                 }
             }
@@ -392,6 +426,8 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
             const int64_t seq = io.seq_base + j;
             bool ok = false;
             if (aid < 0 || aid >= S.A) {
+                // (an account outside the dense range lives in the exact Balances only: k_serial)
+                if (S.fallback || (S.refuse && act == CREATE_BALANCE)) { need_serial(S); return; }
                 if (act == CREATE_BALANCE) { raise_wave(S.ctr, KME_E_CAPACITY, KME_D_CAP_ACCOUNT, j); return; }
             } else if (act == CREATE_BALANCE) {
                 if (!(S.acct_since[aid] < seq)) {
@@ -562,10 +598,21 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     case REMOVE_SYMBOL:
     case PAYOUT: {
         grp = group_of(io.sid[i], S.G);
-        if (grp < 0) {
-            if (a == ADD_SYMBOL) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_SYMBOL, i);
-            else if (a == REMOVE_SYMBOL) { direct = true; ok = true; }      // removeSymbol of an absent symbol
-            else if (funded) raise_thread(S.ctr, KME_E_UNSUPPORTED, KME_D_NONE, i);
+        // a sparse symbol (|sid| >= G) may exist in the serial engine's stores (S.Gs > 0)
+        const bool sparse = grp < 0 && S.Gs > 0 && (!funded || S.fallback);
+        if (funded && a == PAYOUT && serial_capable(S)) {
+            need_serial(S);                                                 // the positions ledger (KP:148-165)
+        } else if (grp < 0) {
+            if (a == ADD_SYMBOL) {
+                if (sparse) { if (funded) need_serial(S); }                 // (EXACT: k_serial names it)
+                else if (funded && S.refuse) need_serial(S);
+                else raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_SYMBOL, i);
+            } else if (a == REMOVE_SYMBOL) {
+                if (sparse) { if (funded) need_serial(S); }
+                else { direct = true; ok = true; }                          // removeSymbol of an absent symbol
+            } else if (funded) {
+                raise_thread(S.ctr, KME_E_UNSUPPORTED, KME_D_NONE, i);
+            }
         }
         break;
     }
@@ -596,13 +643,23 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
                 grp = gj; tgt = t;
                 const int side = (sj != 0 && ((sj < 0) != (io.action[j] != BUY))) ? 1 : 0;   // book_side
                 vlev = (pj & 0xFF) | (side << 8) | (1 << 9);
+            } else if (S.Gs > 0 && (!funded || S.fallback)) {
+                grp = GRP_RESOLVE; tgt = t;                                 // (order j made the epoch serial)
             }
         } else if (t >= 0) {
             grp = nd.group; tgt = t;
             const int side = (nd.sid != 0 && ((nd.sid < 0) != (nd.action != BUY))) ? 1 : 0;
             vlev = (nd.price & 0xFF) | (side << 8) | (1 << 9);
+            if (grp >= S.G) {                                               // an order on a sparse symbol:
+                grp = GRP_RESOLVE;                                          // k_serial names its group
+                if (funded) need_serial(S);
+            }
         }
-        if (grp < 0) { direct = true; ok = false; }                         // orders.get == null (KP:290-291)
+        if (funded && S.fallback && grp != -1) {
+            const int64_t caid = io.aid[i];
+            if (caid < 0 || caid >= S.A) need_serial(S);                    // an account of the exact ledger only
+        }
+        if (grp == -1) { direct = true; ok = false; }                       // orders.get == null (KP:290-291)
         break;
     }
     case CREATE_BALANCE:
@@ -616,7 +673,7 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
     if (!funded || S.fallback) S.cancel_tgt[i] = tgt;   // k_serial's cancel target
     if (!funded) return;
     if (direct) write_out(io, i, a, ok, io.size[i], false, 0);
-    if (grp >= 0) {   // the record as k_match reads it (PRec)
+    if (grp >= 0 && grp < S.G) {   // the record as k_match reads it (PRec)
         const int64_t oid = io.oid[i], aid = io.aid[i];
         // word 6: a cancel's target (a same-epoch order j: -(j + 2)); a FUNDED BUY/SELL's packed record
         // is k_emap's, with its own entry's position there.  Word 1 of a cancel of a same-epoch order:
@@ -812,6 +869,12 @@ __global__ void k_segments(DevState S, EpochIO io, int buf, int list_min) {
     const int64_t prev = k == 0 ? -1 : (int64_t)keys[k - 1];
     const int64_t cur = k == n ? (int64_t)nseg - 1 : (int64_t)keys[k];
     for (int64_t g = prev + 1; g <= cur; ++g) S.seg[g] = k;
+    // a group whose book only the serial engine can take (a level above 100, a negative size) makes the
+    // epoch serial -- checked once k_serial ever made such a book (C_ODD)
+    if (k < n && cur != prev && cur < (int64_t)S.G && S.ctr[ci(C_ODD)] != 0) {
+        const GroupState& gs = S.grp[cur];
+        if (gs.nneg > 0 || (gs.bm0_msb >> 38) != 0 || (gs.bm1_msb >> 38) != 0) need_serial(S);
+    }
     if (list_min >= 0 && k < n && cur != prev && cur < (int64_t)S.G) {
         const uint32_t kl = k + (uint32_t)list_min;
         if (kl < n && (int64_t)keys[kl] == cur) {
@@ -1005,6 +1068,15 @@ struct Core {
         free_head = -1; chunk_next = chunk_end = 0; glev = nullptr;
         tnext = 0; dead = false;
     }
+    // A book the FUNDED matchers cannot take (they stage prices 0..100 and assume sizes >= 0): a level
+    // above 100 (msb bits 38.., KP:391-404) or an order of negative size (GroupState::nneg counts them,
+    // kept here on the rare paths that change one).  k_segments sends an epoch on such a group to this
+    // engine; C_ODD (sticky) says one was ever made, so that check runs only from then on.
+    KDEV void note_odd() { S.ctr[ci(C_ODD)] = 1; }
+    KDEV void nneg_add(int32_t d) {
+        S.grp[g].nneg += d;   // (one wavefront: a plain read-modify-write)
+        if (d > 0) note_odd();
+    }
 
     KDEV void die(int status, int detail, int64_t idx) { raise_wave(S.ctr, status, detail, idx); dead = true; }
 
@@ -1024,6 +1096,31 @@ struct Core {
             G.bm0_lsb = b0l; G.bm0_msb = b0m; G.bm1_lsb = b1l; G.bm1_msb = b1m;
             G.free_head = free_head; G.chunk_next = chunk_next; G.chunk_end = chunk_end;
         }
+    }
+    // The group of a record's symbol (books +sid / -sid, KP:184-191, 201): |sid| < G is group |sid|; a
+    // sparse symbol (|sid| >= G) has the gsid slot its first ADD_SYMBOL took (create), group G + slot;
+    // -1 = no group (the books are absent).  Long.MIN_VALUE and |sid| >= 2^55 are refused at ADD_SYMBOL:
+    // their bucket pointers (sid << 8) | price alias other books' buckets (KP:379-381).
+    KDEV int32_t symbol_group(int64_t sid, bool create, int64_t idx) {
+        if (sid == INT64_MIN) { if (create) die(KME_E_DOMAIN, KME_D_SID_RANGE, idx); return -1; }
+        const int64_t a = sid < 0 ? -sid : sid;
+        if (a < (int64_t)S.G) return (int32_t)a;
+        if (S.Gs <= 0) { if (create) die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, idx); return -1; }
+        if (create && a >= (1ll << 55)) { die(KME_E_DOMAIN, KME_D_SID_RANGE, idx); return -1; }
+        const uint32_t mask = (uint32_t)S.Gs - 1;
+        uint32_t h = (uint32_t)mix64((uint64_t)a) & mask;
+        for (uint32_t p = 0; p <= mask; ++p) {
+            const int64_t k = S.gsid[h];
+            if (k == a) return S.G + (int32_t)h;
+            if (k == 0) {
+                if (!create) return -1;
+                S.gsid[h] = a;
+                return S.G + (int32_t)h;
+            }
+            h = (h + 1) & mask;
+        }
+        if (create) die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, idx);
+        return -1;
     }
     KDEV uint64_t bl(int side) const { return side ? b1l : b0l; }
     KDEV uint64_t bm(int side) const { return side ? b1m : b0m; }
@@ -1282,11 +1379,13 @@ struct Core {
                 trade(i, ntr, m, t, ts, is_buy);
                 if (dead) return false;
                 S.pool[ms].size = msize;
+                if ((msize | m.size) < 0) nneg_add((msize < 0 ? 1 : 0) - (m.size < 0 ? 1 : 0));
                 if (head_moved) { L->head = ms; S.pool[ms].prev = -1; }
                 L->qty = lqty;
                 return t.size == 0;
             }
             // maker consumed: orders.delete (KP:243)
+            if (m.size < 0) nneg_add(-1);
             int32_t nms;
             bool same_level = m.next >= 0;
             if (same_level) {
@@ -1354,6 +1453,8 @@ struct Core {
         nd->size = t.size; nd->next = -1; nd->prev = nprev; nd->group = g;
         nd->price = p; nd->action = t.action; nd->live = 1; nd->_pad = 0;
         S.rest_slot[i] = slot;
+        if (t.size < 0) nneg_add(1);
+        if (p > 100) note_odd();
     }
 
     // ---------------- removeOrder, KP:289-323
@@ -1389,6 +1490,7 @@ struct Core {
         }
         L->qty -= o.size;
         free_slot(slot);
+        if (o.size < 0) nneg_add(-1);
         post_remove_adjustments(o, i);
         return !dead;
     }
@@ -3390,7 +3492,13 @@ struct GroupLane {
         // its oid-table entry (k_emap's pending one: r.tgt of a BUY/SELL is its position) becomes the
         // rest slot, one 4-B store -- no rest_slot store and no pass in k_unsort (k_match's groups
         // store rest_slot, which k_unsort copies)
-        if (r.tgt > (int64_t)S.otab_mask) { die(KME_E_CAPACITY, KME_D_SENTINEL_OID); return; }   // (guard)
+        // (consistency check: a BUY/SELL's own entry position from k_emap, never outside the table)
+        if (r.tgt > (int64_t)S.otab_mask) {
+            printf("kme guard: k_match_lanes rest i=%u tgt=%lld size=%d otab_mask=%u g=%d\n", r.i, (long long)r.tgt, r.size,
+                   S.otab_mask, g);
+            die(KME_E_CAPACITY, KME_D_GUARD_OTPOS);
+            return;
+        }
         p_node[0] = make_int4(lo32(r.oid), hi32(r.oid), lo32(r.aid), hi32(r.aid));
         p_node[1] = make_int4(lo32(r.sid), hi32(r.sid), tsize, -1);
         p_node[2] = make_int4(lo32(poid), hi32(poid), nprev, g);
@@ -3558,9 +3666,14 @@ __global__ void __launch_bounds__(64) KME_LANES_ATTR k_match_lanes(const DevStat
                     const uint32_t hv = (uint32_t)r.size;
                     uint32_t v = hv <= S.otab_mask ? reinterpret_cast<const KG uint32_t*>(S.otab)[2 * (size_t)hv] : OT_DEAD;
                     if (w.pv && hv == w.p_otpos) v = (uint32_t)w.p_slot;   // (the held-back rest's entry)
-                    if (hv > S.otab_mask) w.die(KME_E_DOMAIN, KME_D_SENTINEL_OID);   // (guard)
                     vslot = (v & OT_PENDING) ? -1 : (int32_t)v;
-                    if ((uint32_t)vslot >= S.pool_cap && vslot >= 0) { w.die(KME_E_UNSUPPORTED, KME_D_SENTINEL_OID); vslot = -1; }   // (guard)
+                    // (consistency checks: k_route's entry position, the entry's slot)
+                    if (hv > S.otab_mask || (vslot >= 0 && (uint32_t)vslot >= S.pool_cap)) {
+                        printf("kme guard: k_match_lanes cancel i=%u tgt=%lld pos=%u entry=%u otab_mask=%u pool_cap=%u g=%d\n", r.i,
+                               (long long)r.tgt, hv, v, S.otab_mask, S.pool_cap, g);
+                        w.die(KME_E_CAPACITY, hv > S.otab_mask ? KME_D_GUARD_OTPOS : KME_D_GUARD_SLOT);
+                        vslot = -1;
+                    }
                 }
             }
             if (w.pv) {                                      // levels the held-back rest wrote
@@ -3689,8 +3802,20 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
             const uint32_t i = r.i;
             const int32_t a = r.action;
             int32_t grp = -1;
-            if (a == CANCEL) grp = rl32(bgrp, j);
-            else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) grp = group_of(r.sid, S.G);
+            if (a == CANCEL) {
+                grp = rl32(bgrp, j);
+                if (grp == GRP_RESOLVE) {   // an order on a sparse symbol (k_route): the node's group, or
+                    if (r.tgt >= 0) {       // the symbol's of the same-epoch order it names
+                        const Node nd = c.ld_node((int32_t)r.tgt);
+                        grp = nd.live && nd.oid == r.oid && nd.group >= 0 && nd.group < S.G + S.Gs ? nd.group : -1;
+                    } else {
+                        grp = c.symbol_group(io.sid[(uint32_t)(-(r.tgt + 2))], false, i);
+                    }
+                }
+            } else if (a == ADD_SYMBOL || a == REMOVE_SYMBOL || a == PAYOUT || a == BUY || a == SELL) {
+                grp = c.symbol_group(r.sid, a == ADD_SYMBOL, i);
+            }
+            if (c.dead) break;
             if (grp >= 0) {
                 if (grp != c.g) { c.store_group(); c.load_group(grp); }
                 const Out o = c.process(r);
@@ -3710,7 +3835,7 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
             switch (a) {
             case CREATE_BALANCE: ok = c.create_balance(r.aid, i); break;
             case TRANSFER: ok = c.transfer(r.aid, r.size); break;
-            case ADD_SYMBOL: c.die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, i); break;
+            case ADD_SYMBOL: c.die(KME_E_CAPACITY, KME_D_CAP_SYMBOL, i); break;   // (symbol_group died first)
             case REMOVE_SYMBOL: ok = true; break;           // absent symbol: removeSymbol returns true
             case PAYOUT: c.payout_settle(r.sid, r.size, i); break;
             default: break;                                 // BUY/SELL on absent book, unknown cancel, unknown action
@@ -3991,12 +4116,13 @@ __global__ void k_tob_groups(DevState S, const uint32_t* groups, uint32_t n, uin
 
 __global__ void k_init_state(DevState S) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < (uint32_t)S.G) {
+    if (k < (uint32_t)(S.G + S.Gs)) {   // the dense groups and the sparse ones
         GroupState gs;
         __builtin_memset(&gs, 0, sizeof gs);
         gs.free_head = -1;
         S.grp[k] = gs;
     }
+    if (k < (uint32_t)S.Gs) S.gsid[k] = 0;
     if (k < (uint32_t)S.A && S.acct_since) S.acct_since[k] = INT64_MAX;
     if (k == 0) S.ctr[ci(C_ERR)] = ~0ull;   // no epoch yet: nothing faulted (a fresh engine can be checkpointed)
 }
@@ -4181,7 +4307,7 @@ void launch_export_trades(const TradeRec* src, const uint32_t* count, uint32_t c
                        reinterpret_cast<int4*>(dst_mapped));
 }
 void launch_init_state(const DevState& S, hipStream_t st) {
-    const uint32_t n = (uint32_t)(S.G > S.A ? S.G : S.A);
+    const uint32_t n = (uint32_t)std::max<int64_t>((int64_t)S.G + S.Gs, S.A);
     hipLaunchKernelGGL(k_init_state, dim3(cdiv(n > 0 ? n : 1, 256)), dim3(256), 0, st, S);
 }
 

@@ -286,6 +286,10 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
     uint32_t o = S.lcnt[i];
     const uint32_t t0 = io.trade_off[i];
     auto put = [&](int64_t aid, int64_t sid, uint32_t es, int32_t size, int32_t price, uint32_t flags) {
+        // an account outside [0, A) (a maker that rested in a serial epoch, KME_FLAG_SERIAL_FALLBACK) is
+        // in the exact Balances only: the serial replay takes the epoch's ledger (the op stays, keyed in
+        // range, for the passes that still run before they see the fallback)
+        if (aid < 0 || aid >= S.A) { lfallback(S); aid = 0; }
         // one 16-B store: sid, arrival number, size, price term | flags << 16 (LOp's layout)
         reinterpret_cast<KG uint4*>(S.lrec)[o] =
             make_uint4((uint32_t)(int32_t)sid, es, (uint32_t)size, (uint32_t)(uint16_t)(int16_t)price | flags << 16);

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) k_pos_rehash(DevState N, const PosEntry* 
 // _pad[0].  Order is irrelevant (restore scatters by index).
 __global__ void __launch_bounds__(256) k_ckpt_levels(DevState S, Level* out, unsigned long long* cnt) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t total = (uint64_t)S.G * 2 * NLEV;
+    const uint64_t total = (uint64_t)(S.G + S.Gs) * 2 * NLEV;   // dense and sparse groups
     bool set = false;
     uint32_t g = 0, side = 0, p = 0;
     if (t < total) {
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) k_ckpt_levels(DevState S, Level* out, uns
     const uint32_t k = wave_reserve(cnt, set);
     if (set) {
         Level L = S.lev[t];
-        L._pad[0] = (int32_t)t;   // (t < G * 256 <= 2^32)
+        L._pad[0] = (int32_t)(uint32_t)t;   // (t < (G + Gs) * 256 <= 2^32)
         L._pad[1] = 0;
         out[k] = L;
     }
@@ -177,7 +177,7 @@ void launch_ledger_rehash(const DevState& N, const DevState& O, unsigned long lo
 }
 void launch_ckpt_levels(const DevState& S, Level* out, unsigned long long* cnt, hipStream_t st) {
     (void)hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st);
-    hipLaunchKernelGGL(k_ckpt_levels, dim3(mcdiv((uint64_t)S.G * 2 * NLEV, 256)), dim3(256), 0, st, S, out, cnt);
+    hipLaunchKernelGGL(k_ckpt_levels, dim3(mcdiv((uint64_t)(S.G + S.Gs) * 2 * NLEV, 256)), dim3(256), 0, st, S, out, cnt);
 }
 void launch_rst_levels(const DevState& S, const Level* in, uint32_t n, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_rst_levels, dim3(mcdiv(n, 256)), dim3(256), 0, st, S, in, n);

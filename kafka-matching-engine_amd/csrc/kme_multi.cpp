@@ -150,7 +150,9 @@ kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* de
     m->n = n;
     if (n > 1 && cfg->flags == both) {
         m->can_consolidate = true;
-        m->cfg.flags = 0;
+        // the shards refuse what only a serial engine takes (a record outside the funded domain, a sparse
+        // symbol) as unproven, so that it consolidates too instead of faulting
+        m->cfg.flags = KME_FLAG_REFUSE_SERIAL;
         m->cons_cfg = *cfg;
         m->cons_cfg.credit_shards = 1;
         m->cons_cfg.device = devices[0];

@@ -39,6 +39,15 @@ uint64_t pow2_at_least(uint64_t x) {
 
 }  // namespace
 
+namespace kme {
+// Tests only: env KME_TEST_FAIL names a failure path to take where the product path cannot otherwise
+// be driven into it (an allocation that fails).
+bool test_hook_fail(const char* what) {
+    const char* v = std::getenv("KME_TEST_FAIL");
+    return v && std::strcmp(v, what) == 0;
+}
+}  // namespace kme
+
 struct kme_engine {
     kme_config cfg{};
     int device = 0;
@@ -277,6 +286,13 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     if (!cfg || !out) return KME_E_INVALID;
     if (cfg->abi_version != KME_ABI_VERSION) return KME_E_INVALID;
     if (cfg->mode != KME_MODE_EXACT && cfg->mode != KME_MODE_FUNDED) return KME_E_INVALID;
+    // sparse symbols (|sid| >= max_symbols, KP:184-191 takes any long): serial engine only, so by default
+    // where a serial engine runs (EXACT; FUNDED with the serial fallback)
+    uint64_t Gs = 0;
+    if (cfg->max_sparse_symbols == KME_SPARSE_NONE) Gs = 0;
+    else if (cfg->max_sparse_symbols) Gs = pow2_at_least(cfg->max_sparse_symbols);
+    else if (cfg->mode == KME_MODE_EXACT || (cfg->flags & KME_FLAG_SERIAL_FALLBACK)) Gs = 4096;
+    if (cfg->max_symbols + Gs > (1ull << 24)) return KME_E_INVALID;
     if (cfg->max_symbols == 0 || cfg->max_symbols > (1u << 24) || cfg->max_epoch == 0 ||
         cfg->max_epoch > (1u << 30) || cfg->max_resting == 0 || cfg->max_resting >= (1ull << 31) ||
         cfg->max_trades == 0)
@@ -284,10 +300,13 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     // FUNDED: the oid table (a power of two >= 2 (pool + epoch) entries) stays within 2^30 entries,
     // so an entry's position rides in a packed record's signed 32-bit word (k_route, otab_final)
     if (cfg->mode == KME_MODE_FUNDED && (cfg->max_accounts == 0 || cfg->max_accounts > (1u << 28) ||
-                                         cfg->max_resting + (uint64_t)(cfg->max_symbols + 1) * POOL_CHUNK +
+                                         cfg->max_resting + (uint64_t)(cfg->max_symbols + 1 + Gs) * POOL_CHUNK +
                                                  cfg->max_epoch > (1ull << 29)))
         return KME_E_INVALID;
-    if ((cfg->flags & ~(KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK)) != 0 ||
+    if ((cfg->flags & KME_FLAG_REFUSE_SERIAL) &&
+        (cfg->mode != KME_MODE_FUNDED || (cfg->flags & (KME_FLAG_SERIAL_FALLBACK | KME_FLAG_EXACT_LEDGER))))
+        return KME_E_INVALID;   // (a shard of kme_multi: refuses what it cannot prove, takes nothing serially)
+    if ((cfg->flags & ~(KME_FLAG_EXACT_LEDGER | KME_FLAG_SERIAL_FALLBACK | KME_FLAG_REFUSE_SERIAL)) != 0 ||
         ((cfg->flags & KME_FLAG_EXACT_LEDGER) && cfg->credit_shards > 1) ||   // a shard sees part of the ledger only
         ((cfg->flags & KME_FLAG_SERIAL_FALLBACK) && !(cfg->flags & KME_FLAG_EXACT_LEDGER)))   // needs the exact ledger
         return KME_E_INVALID;
@@ -311,9 +330,12 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     const uint32_t E = cfg->max_epoch;
     // node pool: max_resting plus the slots a symbol group can hold back in its bump chunk
     // (k_match takes POOL_CHUNK slots at a time), so that max_resting resting orders always fit
-    const uint64_t P = cfg->max_resting + (funded ? (uint64_t)(G + 1) * POOL_CHUNK : 0);
+    // (a sparse symbol's group holds back a chunk too)
+    const uint64_t P = cfg->max_resting + (funded ? (uint64_t)(G + 1) * POOL_CHUNK : 0) + Gs * POOL_CHUNK;
     DevState& S = e->S;
     S.G = (int32_t)G;
+    S.Gs = (int32_t)Gs;
+    S.refuse = (cfg->flags & KME_FLAG_REFUSE_SERIAL) ? 1 : 0;
     S.mode = (int32_t)cfg->mode;
     S.A = funded ? (int32_t)cfg->max_accounts : 0;
     {
@@ -345,8 +367,9 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     S.ttmp_cap = (uint32_t)ttmp_ov;
     S.tshard_cap = (uint32_t)tshard_cap;
 
-    ALLOC(S.grp, G);
-    ALLOC(S.lev, (size_t)G * 2 * NLEV);
+    ALLOC(S.grp, G + Gs);
+    ALLOC(S.lev, (size_t)(G + Gs) * 2 * NLEV);
+    if (Gs) ALLOC(S.gsid, Gs);
     ALLOC(S.pool, P);
     ALLOC(S.otab, e->otab_cap);
     const bool exact_ledger = !funded || (cfg->flags & KME_FLAG_EXACT_LEDGER);
@@ -720,21 +743,30 @@ static kme_status ledger_reserve(kme_engine* e, uint64_t bal_used, uint64_t pos_
         tryalloc((void**)&N.pos, np * sizeof(PosEntry));
         N.pos_mask = (uint32_t)(np - 1);
     }
-    if (!alloc_ok) {   // out of HBM: free what was taken, keep the old tables
+    auto free_new = [&] {
         if (nb) { (void)hipFree(N.bal_state); (void)hipFree(N.bal_key); (void)hipFree(N.bal_val); }
         if (np) (void)hipFree(N.pos);
+    };
+    if (!alloc_ok) {   // out of HBM: free what was taken, keep the old tables
+        free_new();
         std::fprintf(stderr, "kme: ledger tables cannot grow (HBM): %llu / %llu slots kept\n", (unsigned long long)bs,
                      (unsigned long long)ps);
         return KME_OK;
     }
-    if (nb) HIP_TRY(hipMemsetAsync(N.bal_state, 0, nb * sizeof(uint32_t), e->stream));
-    if (np) HIP_TRY(hipMemsetAsync(N.pos, 0, np * sizeof(PosEntry), e->stream));
-    launch_ledger_rehash(N, S, e->d_maint + 2, e->stream);
-    HIP_TRY(hipGetLastError());
-    unsigned long long fail[2];
-    HIP_TRY(hipMemcpyAsync(fail, e->d_maint + 2, sizeof fail, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    if (fail[0] || fail[1]) return KME_E_CAPACITY;   // (cannot happen: the new tables are at most half full)
+    // (until the swap below a failure frees the new tables and leaves the old ones in place)
+    unsigned long long fail[2] = {0, 0};
+    bool rok = (!nb || hipMemsetAsync(N.bal_state, 0, nb * sizeof(uint32_t), e->stream) == hipSuccess) &&
+               (!np || hipMemsetAsync(N.pos, 0, np * sizeof(PosEntry), e->stream) == hipSuccess);
+    if (rok) launch_ledger_rehash(N, S, e->d_maint + 2, e->stream);
+    rok = rok && hipGetLastError() == hipSuccess &&
+          hipMemcpyAsync(fail, e->d_maint + 2, sizeof fail, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+          hipStreamSynchronize(e->stream) == hipSuccess;
+    if (!rok) {
+        (void)hipGetLastError();
+        free_new();
+        return KME_E_HIP;
+    }
+    if (fail[0] || fail[1]) { free_new(); return KME_E_CAPACITY; }   // (cannot happen: the new tables are at most half full)
     for (auto& a : e->allocs) {   // the new tables take the old ones' places in the allocation list
         if (nb && a == (void*)S.bal_state) a = N.bal_state;
         else if (nb && a == (void*)S.bal_key) a = N.bal_key;
@@ -1219,25 +1251,50 @@ extern "C" {
 const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
-// Format 3: header, then the stores in their compact form -- group states, the set price levels
-// (kme_maint.hip), the used prefix of the node pool, the FUNDED reservation ledger, the live Balances
-// and Positions entries -- then the application record, then the trailer (size of that record and
-// the digest of everything before it; kme_internal.h).  The oid table is not stored: a restore
-// rebuilds it from the resting orders (an entry of an order that no longer rests is only ever a stale
-// fact), and the ledger tables are rebuilt at the size their live entries need.
+// Format 4: header, then the stores in their compact form -- group states (the dense groups, then the
+// sparse ones), the set price levels (kme_maint.hip), the used prefix of the node pool, the FUNDED
+// reservation ledger, the live Balances and Positions entries, the sparse symbols' ids -- then the
+// application record, then the trailer (size of that record and the digest of everything before it;
+// kme_internal.h).  The oid table is not stored: a restore rebuilds it from the resting orders (an
+// entry of an order that no longer rests is only ever a stale fact), and the ledger
+// tables are rebuilt at the size their live entries need.
+// Format 3 (ABI 6, no sparse symbols) is still read: the same stores without the sparse groups and
+// ids, under a header whose kme_config lacks max_sparse_symbols; they restore as empty.
 namespace {
 constexpr char kCkptMagic3[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '3'};
+constexpr char kCkptMagic4[8] = {'K', 'M', 'E', 'C', 'K', 'P', 'T', '4'};
+struct kme_config_v6 {   // kme_config of ABI 6 (format-3 headers)
+    uint32_t abi_version, mode, max_symbols, max_accounts, max_epoch, max_trades;
+    uint64_t max_resting, ledger_capacity;
+    int32_t device;
+    uint32_t credit_shards, flags;
+    int32_t light_max;
+};
+static_assert(sizeof(kme_config_v6) == 56, "ABI-6 kme_config");
 struct CkptHeader3 {
     char magic[8];
-    kme_config cfg;
+    kme_config_v6 cfg;
     int64_t seq_base;
     uint64_t pool_used, n_levels, bal_live, pos_live, app_bytes;
     uint64_t _reserved[3];
 };
+struct CkptHeader4 {
+    char magic[8];
+    kme_config cfg;
+    int64_t seq_base;
+    uint64_t pool_used, n_levels, bal_live, pos_live, app_bytes;
+    uint64_t n_sparse;                 // sparse groups (their GroupStates and ids are in the file)
+    uint64_t _reserved[3];
+};
 
-// n bytes of device memory at `dev` into the writer, through a host staging buffer
-bool put_dev(kme_engine* e, kme::CkptWriter& w, const void* dev, size_t n, const char* what) {
-    return staged_read(e, dev, n, what, [&](const char* chunk, size_t c, size_t) { return w.write(chunk, c); });
+// n bytes of device memory at `dev` into the writer, through a host staging buffer; *file_fail is set
+// when the write failed (else a false return is the device's)
+bool put_dev(kme_engine* e, kme::CkptWriter& w, const void* dev, size_t n, const char* what, bool* file_fail) {
+    return staged_read(e, dev, n, what, [&](const char* chunk, size_t c, size_t) {
+        const bool ok = w.write(chunk, c);
+        if (!ok) *file_fail = true;
+        return ok;
+    });
 }
 }  // namespace
 }  // extern "C"
@@ -1341,18 +1398,19 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
     // the last epoch faulted: its state is not a checkpoint (an epoch refused with KME_E_UNFUNDED
     // changed nothing: the engine's state is the one before it)
     if (ctr[ci(C_ERR)] != ~0ull && (ctr[ci(C_ERR)] & 0xFF) != KME_E_UNFUNDED) return KME_E_FAILED;
-    const size_t G = e->cfg.max_symbols, A = e->cfg.max_accounts;
+    const size_t G = e->cfg.max_symbols, Gs = (size_t)S.Gs, A = e->cfg.max_accounts;
     const bool funded = e->cfg.mode == KME_MODE_FUNDED;
-    CkptHeader3 h{};
-    std::memcpy(h.magic, kCkptMagic3, sizeof h.magic);
+    CkptHeader4 h{};
+    std::memcpy(h.magic, kCkptMagic4, sizeof h.magic);
     h.cfg = e->cfg;
     h.seq_base = e->seq_base;
     h.pool_used = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], S.pool_cap);
     h.app_bytes = app_bytes;
+    h.n_sparse = Gs;
     // the compact stores on the device first: the set levels (counted from the group bitmaps) and
     // the live ledger entries (counted by k_ledger_live), into scratch of exactly that size
-    std::vector<GroupState> grp(G);
-    if (!staged_d2h(e, grp.data(), S.grp, G * sizeof(GroupState), "groups")) return KME_E_HIP;
+    std::vector<GroupState> grp(G + Gs);
+    if (!staged_d2h(e, grp.data(), S.grp, (G + Gs) * sizeof(GroupState), "groups")) return KME_E_HIP;
     uint64_t nlev = 0;
     for (const GroupState& gs : grp)
         nlev += (uint64_t)(__builtin_popcountll(gs.bm0_lsb) + __builtin_popcountll(gs.bm0_msb) + __builtin_popcountll(gs.bm1_lsb) +
@@ -1364,11 +1422,15 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
         HIP_TRY(hipMemcpyAsync(live, e->d_maint, sizeof live, hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
+    // what went wrong, if anything: scratch allocation (KME_E_CAPACITY), the device (KME_E_HIP), or
+    // the file (KME_E_INVALID)
+    kme_status why = KME_OK;
     Level* d_lev = nullptr;
     void *d_bal = nullptr, *d_pos = nullptr;
     bool ok = hipMalloc((void**)&d_lev, std::max<uint64_t>(nlev, 1) * sizeof(Level)) == hipSuccess &&
               hipMalloc(&d_bal, std::max<uint64_t>(live[0], 1) * 16) == hipSuccess &&
               hipMalloc(&d_pos, std::max<uint64_t>(live[1], 1) * 32) == hipSuccess;
+    if (!ok) why = KME_E_CAPACITY;
     if (ok) {
         launch_ckpt_levels(S, d_lev, e->d_maint, e->stream);
         if (e->ledger) launch_ckpt_ledger(S, d_bal, d_pos, e->d_maint + 1, e->stream);
@@ -1377,33 +1439,42 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
              hipStreamSynchronize(e->stream) == hipSuccess;
         if (!e->ledger) cnt[1] = cnt[2] = 0;
         ok = ok && cnt[0] == nlev && cnt[1] == live[0] && cnt[2] == live[1];
+        if (!ok) why = KME_E_HIP;
     }
     (void)hipGetLastError();
     h.n_levels = cnt[0];
     h.bal_live = cnt[1];
     h.pos_live = cnt[2];
-    {
+    if (ok) {
         kme::CkptWriter w(path);
-        ok = ok && w.write(&h, sizeof h);
-        ok = ok && w.write(grp.data(), G * sizeof(GroupState));
-        ok = ok && put_dev(e, w, d_lev, h.n_levels * sizeof(Level), "levels");
-        ok = ok && put_dev(e, w, S.pool, h.pool_used * sizeof(Node), "pool");
+        bool file_fail = false;
+        auto put = [&](const void* dev, size_t n, const char* what) {
+            if (ok && !put_dev(e, w, dev, n, what, &file_fail)) { ok = false; why = file_fail ? KME_E_INVALID : KME_E_HIP; }
+        };
+        auto write = [&](const void* p, size_t n) {
+            if (ok && !w.write(p, n)) { ok = false; why = KME_E_INVALID; }
+        };
+        write(&h, sizeof h);
+        write(grp.data(), (G + Gs) * sizeof(GroupState));
+        put(d_lev, h.n_levels * sizeof(Level), "levels");
+        put(S.pool, h.pool_used * sizeof(Node), "pool");
         if (funded) {
-            ok = ok && put_dev(e, w, S.acct_since, A * sizeof(int64_t), "accounts");
-            ok = ok && put_dev(e, w, S.acct_lb, A * sizeof(int64_t), "accounts");
-            ok = ok && put_dev(e, w, S.acct_demand, A * sizeof(int64_t), "accounts");
+            put(S.acct_since, A * sizeof(int64_t), "accounts");
+            put(S.acct_lb, A * sizeof(int64_t), "accounts");
+            put(S.acct_demand, A * sizeof(int64_t), "accounts");
         }
         if (e->ledger) {
-            ok = ok && put_dev(e, w, d_bal, h.bal_live * 16, "Balances");
-            ok = ok && put_dev(e, w, d_pos, h.pos_live * 32, "Positions");
+            put(d_bal, h.bal_live * 16, "Balances");
+            put(d_pos, h.pos_live * 32, "Positions");
         }
-        ok = ok && w.write(app, app_bytes);
-        ok = ok && w.commit(app_bytes, nullptr);
+        if (Gs) put(S.gsid, Gs * sizeof(int64_t), "sparse symbols");
+        write(app, app_bytes);
+        if (ok && !w.commit(app_bytes, nullptr)) { ok = false; why = KME_E_INVALID; }
     }
     (void)hipFree(d_lev);
     if (d_bal) (void)hipFree(d_bal);
     if (d_pos) (void)hipFree(d_pos);
-    return ok ? KME_OK : KME_E_INVALID;
+    return ok ? KME_OK : why;
 }
 
 kme_status kme_checkpoint(kme_engine* e, const char* path) { return kme_checkpoint_app(e, path, nullptr, 0); }
@@ -1415,34 +1486,58 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     if (app_bytes) *app_bytes = 0;
     HIP_TRY(hipSetDevice(e->device));
     kme::CkptReader r(path);
-    CkptHeader3 h{};
-    bool ok = r.read(&h, sizeof h) && std::memcmp(h.magic, kCkptMagic3, sizeof h.magic) == 0;
+    // the header: format 4, or format 3 (an ABI-6 kme_config, no sparse symbols)
+    CkptHeader4 h{};
+    char magic[8];
+    bool ok = r.read(magic, sizeof magic);
+    const bool v3 = ok && std::memcmp(magic, kCkptMagic3, sizeof magic) == 0;
+    if (ok && v3) {
+        CkptHeader3 h3{};
+        std::memcpy(h3.magic, magic, sizeof magic);
+        ok = r.read(reinterpret_cast<char*>(&h3) + sizeof magic, sizeof h3 - sizeof magic);
+        std::memcpy(h.magic, magic, sizeof magic);
+        h.cfg = e->cfg;   // (the fields a format-3 file has are compared below)
+        h.cfg.abi_version = e->cfg.abi_version;
+        h.cfg.mode = h3.cfg.mode; h.cfg.max_symbols = h3.cfg.max_symbols; h.cfg.max_accounts = h3.cfg.max_accounts;
+        h.cfg.max_resting = h3.cfg.max_resting; h.cfg.max_epoch = h3.cfg.max_epoch;
+        h.cfg.credit_shards = h3.cfg.credit_shards; h.cfg.flags = h3.cfg.flags;
+        ok = ok && h3.cfg.abi_version == 6;
+        h.seq_base = h3.seq_base; h.pool_used = h3.pool_used; h.n_levels = h3.n_levels;
+        h.bal_live = h3.bal_live; h.pos_live = h3.pos_live; h.app_bytes = h3.app_bytes;
+        h.n_sparse = 0;
+    } else if (ok) {
+        std::memcpy(h.magic, magic, sizeof magic);
+        ok = std::memcmp(magic, kCkptMagic4, sizeof magic) == 0 &&
+             r.read(reinterpret_cast<char*>(&h) + sizeof magic, sizeof h - sizeof magic) &&
+             h.cfg.max_sparse_symbols == e->cfg.max_sparse_symbols && h.n_sparse == (uint64_t)e->S.Gs;
+    }
     // the same store geometry (device, stream, timing and the ledger tables' initial size may differ)
+    const size_t G = e->cfg.max_symbols, Gs = (size_t)e->S.Gs, A = e->cfg.max_accounts;
     ok = ok && h.cfg.abi_version == e->cfg.abi_version && h.cfg.mode == e->cfg.mode &&
          h.cfg.max_symbols == e->cfg.max_symbols && h.cfg.max_accounts == e->cfg.max_accounts &&
          h.cfg.max_resting == e->cfg.max_resting && h.cfg.max_epoch == e->cfg.max_epoch &&
          h.cfg.credit_shards == e->cfg.credit_shards && h.cfg.flags == e->cfg.flags &&
-         h.pool_used <= e->S.pool_cap && h.n_levels <= (uint64_t)e->cfg.max_symbols * 2 * NLEV &&
+         h.pool_used <= e->S.pool_cap && h.n_levels <= (uint64_t)(G + h.n_sparse) * 2 * NLEV &&
          h.app_bytes < (1ull << 40) && h.bal_live < (1ull << 31) && h.pos_live < (1ull << 31) &&
          (e->ledger || (h.bal_live == 0 && h.pos_live == 0));
     if (ok && app_bytes) *app_bytes = (size_t)h.app_bytes;
     if (ok && (h.app_bytes > app_cap || (h.app_bytes && !app))) return KME_E_CAPACITY;   // nothing else read
     // the whole file is read and its digest checked before anything reaches the device: a mismatched,
     // truncated or corrupted checkpoint leaves the engine untouched
-    const size_t G = e->cfg.max_symbols, A = e->cfg.max_accounts;
     const bool funded = e->cfg.mode == KME_MODE_FUNDED;
-    std::vector<char> grp, lev, pool, acct, bal, pos, rec;
+    std::vector<char> grp, lev, pool, acct, bal, pos, gsid, rec;
     auto take = [&](std::vector<char>& v, uint64_t n) {
         if (!ok) return;
         v.resize(n);
         ok = r.read(v.data(), n);
     };
-    take(grp, G * sizeof(GroupState));
+    take(grp, (G + h.n_sparse) * sizeof(GroupState));
     take(lev, h.n_levels * sizeof(Level));
     take(pool, h.pool_used * sizeof(Node));
     if (funded) take(acct, 3 * A * sizeof(int64_t));
     take(bal, h.bal_live * 16);
     take(pos, h.pos_live * 32);
+    take(gsid, h.n_sparse * sizeof(int64_t));
     take(rec, h.app_bytes);
     kme::CkptTrailer t{};
     ok = ok && r.verify(&t) && t.app_bytes == h.app_bytes;
@@ -1450,29 +1545,51 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
         if (app_bytes) *app_bytes = 0;
         return KME_E_INVALID;
     }
-    // ledger tables large enough for the live entries and two epochs (a fresh engine's may be smaller)
+    // a format-3 file has no sparse groups: they restore empty
+    if (h.n_sparse < Gs) {
+        grp.resize((G + Gs) * sizeof(GroupState), 0);
+        for (size_t g = G + h.n_sparse; g < G + Gs; ++g) reinterpret_cast<GroupState*>(grp.data())[g].free_head = -1;
+        gsid.resize(Gs * sizeof(int64_t), 0);
+    }
+    // the groups whose book only the serial engine takes (C_ODD, k_segments' check)
+    uint64_t odd = 0;
+    for (size_t g = 0; g < G; ++g) {
+        const GroupState& gs = reinterpret_cast<const GroupState*>(grp.data())[g];
+        odd += (gs.nneg > 0 || (gs.bm0_msb >> 38) != 0 || (gs.bm1_msb >> 38) != 0) ? 1 : 0;
+    }
+    // ledger tables large enough for the live entries and two epochs (a fresh engine's may be
+    // smaller): every replacement is allocated before any old table is freed, so a failed allocation
+    // leaves the engine untouched (KME_E_CAPACITY)
     DevState& S = e->S;
+    uint32_t* nbst = nullptr;
+    int64_t *nbk = nullptr, *nbv = nullptr;
+    PosEntry* npos = nullptr;
+    uint64_t nb = 0, np = 0;
     if (e->ledger) {
-        const uint64_t nb = ledger_slots(h.bal_live, bal_bound(e->cfg), 2), np = ledger_slots(h.pos_live, pos_bound(e->cfg), 2);
+        nb = ledger_slots(h.bal_live, bal_bound(e->cfg), 2);
+        np = ledger_slots(h.pos_live, pos_bound(e->cfg), 2);
         if (nb > (1ull << 31) || np > (1ull << 31)) return KME_E_CAPACITY;
-        if (nb > (uint64_t)S.bal_mask + 1) {
-            uint32_t* st = nullptr; int64_t *k = nullptr, *v = nullptr;
-            if (hipMalloc((void**)&st, nb * 4) != hipSuccess || hipMalloc((void**)&k, nb * 8) != hipSuccess ||
-                hipMalloc((void**)&v, nb * 8) != hipSuccess) {
-                (void)hipGetLastError(); (void)hipFree(st); (void)hipFree(k); (void)hipFree(v);
-                return KME_E_CAPACITY;
-            }
+        bool aok = true;
+        if (nb > (uint64_t)S.bal_mask + 1)
+            aok = hipMalloc((void**)&nbst, nb * 4) == hipSuccess && hipMalloc((void**)&nbk, nb * 8) == hipSuccess &&
+                  hipMalloc((void**)&nbv, nb * 8) == hipSuccess;
+        if (aok && np > (uint64_t)S.pos_mask + 1) aok = hipMalloc((void**)&npos, np * sizeof(PosEntry)) == hipSuccess;
+        if (kme::test_hook_fail("restore_alloc")) aok = false;   // (tests: the failed-allocation path)
+        if (!aok) {
+            (void)hipGetLastError();
+            (void)hipFree(nbst); (void)hipFree(nbk); (void)hipFree(nbv); (void)hipFree(npos);
+            return KME_E_CAPACITY;
+        }
+        if (nbst) {
             dfree(e, S.bal_state); dfree(e, S.bal_key); dfree(e, S.bal_val);
-            e->allocs.push_back(st); e->allocs.push_back(k); e->allocs.push_back(v);
-            S.bal_state = st; S.bal_key = k; S.bal_val = v;
+            e->allocs.push_back(nbst); e->allocs.push_back(nbk); e->allocs.push_back(nbv);
+            S.bal_state = nbst; S.bal_key = nbk; S.bal_val = nbv;
             S.bal_mask = (uint32_t)(nb - 1);
         }
-        if (np > (uint64_t)S.pos_mask + 1) {
-            PosEntry* p = nullptr;
-            if (hipMalloc((void**)&p, np * sizeof(PosEntry)) != hipSuccess) { (void)hipGetLastError(); return KME_E_CAPACITY; }
+        if (npos) {
             dfree(e, S.pos);
-            e->allocs.push_back(p);
-            S.pos = p;
+            e->allocs.push_back(npos);
+            S.pos = npos;
             S.pos_mask = (uint32_t)(np - 1);
         }
     }
@@ -1484,10 +1601,11 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     hipStream_t st = e->stream;
     void *d_lev = nullptr, *d_bal = nullptr, *d_pos = nullptr;
     bool dok = staged_h2d(e, S.grp, grp.data(), grp.size(), "groups") &&
-               hipMemsetAsync(S.lev, 0, G * 2 * NLEV * sizeof(Level), st) == hipSuccess &&
+               hipMemsetAsync(S.lev, 0, (G + Gs) * 2 * NLEV * sizeof(Level), st) == hipSuccess &&
                hipMalloc(&d_lev, std::max<size_t>(lev.size(), 16)) == hipSuccess &&
                staged_h2d(e, d_lev, lev.data(), lev.size(), "levels") &&
-               (pool.empty() || staged_h2d(e, S.pool, pool.data(), pool.size(), "pool"));
+               (pool.empty() || staged_h2d(e, S.pool, pool.data(), pool.size(), "pool")) &&
+               (Gs == 0 || staged_h2d(e, S.gsid, gsid.data(), gsid.size(), "sparse symbols"));
     if (dok) launch_rst_levels(S, (const Level*)d_lev, (uint32_t)h.n_levels, st);
     if (dok && funded) {
         const int64_t* a = reinterpret_cast<const int64_t*>(acct.data());
@@ -1512,6 +1630,9 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     if (d_lev) (void)hipFree(d_lev);
     if (d_bal) (void)hipFree(d_bal);
     if (d_pos) (void)hipFree(d_pos);
+    // the device copy of the engine state (the tables above may have moved) before anything can fail
+    // later: a dead engine's kernels never run, a live one's read the state it holds
+    if (hipMemcpy(e->d_S, &e->S, sizeof(DevState), hipMemcpyHostToDevice) != hipSuccess) return dead(KME_E_HIP);
     if (!dok) return dead(KME_E_HIP);
     if (fail) return dead(KME_E_CAPACITY);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
@@ -1520,16 +1641,15 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
     ctr[ci(C_POOL_BUMP)] = h.pool_used;
     ctr[ci(C_BAL_USED)] = h.bal_live;
     ctr[ci(C_POS_USED)] = h.pos_live;
+    ctr[ci(C_ODD)] = odd ? 1 : 0;
     ctr[ci(C_ERR)] = ~0ull;
-    {   // a restored book may hold size-0 makers: then the fast segments stay off (C_SIZE0)
+    {   // a restored book may hold size-0 (or negative) makers: then the fast segments stay off (C_SIZE0)
         const Node* nodes = reinterpret_cast<const Node*>(pool.data());
         ctr[ci(C_SIZE0)] = 0;
         for (uint64_t k = 0; k < h.pool_used; ++k)
-            if (nodes[k].live && nodes[k].size == 0) { ctr[ci(C_SIZE0)] = 1; break; }
+            if (nodes[k].live && nodes[k].size <= 0) { ctr[ci(C_SIZE0)] = 1; break; }
     }
-    if (hipMemcpy(S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(e->d_S, &e->S, sizeof(DevState), hipMemcpyHostToDevice) != hipSuccess)
-        return dead(KME_E_HIP);
+    if (hipMemcpy(S.ctr, ctr, sizeof ctr, hipMemcpyHostToDevice) != hipSuccess) return dead(KME_E_HIP);
     e->seq_base = h.seq_base;
     if (!rec.empty()) std::memcpy(app, rec.data(), rec.size());
     return KME_OK;
@@ -1740,9 +1860,11 @@ static char* dup_string(const std::string& s, size_t* len) {
 kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     if (!e || !text) return KME_E_INVALID;
     if (kme_status r = snap_begin(e, "kme_snapshot_books")) return r;
-    const uint32_t G = e->cfg.max_symbols;
+    const uint32_t G = e->cfg.max_symbols + (uint32_t)e->S.Gs;   // the dense groups, then the sparse ones
+    const uint32_t Gd = e->cfg.max_symbols;
     std::vector<GroupState> grp(G);
     std::vector<Level> lev((size_t)G * 2 * NLEV);
+    std::vector<int64_t> gsid((size_t)e->S.Gs);
     unsigned long long ctr[C_NCTR * CTR_STRIDE];
     if (kme_status r = snap_read(e, ctr, e->S.ctr, sizeof ctr, "counters")) return r;
     const uint64_t nslots = std::min<uint64_t>(ctr[ci(C_POOL_BUMP)], e->S.pool_cap);
@@ -1751,6 +1873,8 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     if (kme_status r = snap_read(e, lev.data(), e->S.lev, lev.size() * sizeof(Level), "levels")) return r;
     if (nslots)
         if (kme_status r = snap_read(e, pool.data(), e->S.pool, nslots * sizeof(Node), "pool")) return r;
+    if (!gsid.empty())
+        if (kme_status r = snap_read(e, gsid.data(), e->S.gsid, gsid.size() * sizeof(int64_t), "sparse symbols")) return r;
 
     struct BookLine { int64_t key, msb, lsb; };
     struct BucketLine { int64_t ptr, first, last; };
@@ -1761,8 +1885,10 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
     for (uint32_t g = 0; g < G; ++g) {
         const GroupState& gs = grp[g];
         if (!gs.exists) continue;
+        const int64_t asid = g < Gd ? (int64_t)g : gsid[g - Gd];   // |sid| of the group's books
+        if (g >= Gd && asid == 0) { problems.push_back("X sparse group without a symbol"); continue; }
         for (int side = 0; side < (g == 0 ? 1 : 2); ++side) {
-            const int64_t key = side ? -(int64_t)g : (int64_t)g;
+            const int64_t key = side ? -asid : asid;
             const uint64_t l = side ? gs.bm1_lsb : gs.bm0_lsb, m = side ? gs.bm1_msb : gs.bm0_msb;
             books.push_back({key, (int64_t)m, (int64_t)l});
             for (int p = 0; p <= 126; ++p) {

@@ -26,9 +26,12 @@ MODE_EXACT, MODE_FUNDED = 0, 1
 KME_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "CAPACITY", 3: "DOMAIN", 4: "UNFUNDED", 5: "UNSUPPORTED", 6: "HIP",
           7: "FAILED"}
-ABI_VERSION = 6
+ABI_VERSION = 7
 FLAG_EXACT_LEDGER = 1
-FLAG_SERIAL_FALLBACK = 2   # FUNDED: an epoch whose funded proof fails runs serially (needs FLAG_EXACT_LEDGER)
+FLAG_SERIAL_FALLBACK = 2   # FUNDED: an epoch whose funded proof fails (or that holds a record outside the
+                           # parallel path's domain) runs serially (needs FLAG_EXACT_LEDGER)
+FLAG_REFUSE_SERIAL = 4     # FUNDED: such an epoch is refused as unproven instead (kme_multi's shards)
+SPARSE_NONE = 0xFFFFFFFF   # kme_config.max_sparse_symbols: no sparse symbols
 
 TRADE_DTYPE = np.dtype([("maker_oid", "<i8"), ("maker_aid", "<i8"), ("maker_sid", "<i8"),
                         ("maker_price", "<i4"), ("size", "<i4")])
@@ -40,7 +43,11 @@ class kme_config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("mode", C.c_uint32), ("max_symbols", C.c_uint32),
                 ("max_accounts", C.c_uint32), ("max_epoch", C.c_uint32), ("max_trades", C.c_uint32),
                 ("max_resting", C.c_uint64), ("ledger_capacity", C.c_uint64), ("device", C.c_int32),
-                ("credit_shards", C.c_uint32), ("flags", C.c_uint32), ("light_max", C.c_int32)]
+                ("credit_shards", C.c_uint32), ("flags", C.c_uint32), ("light_max", C.c_int32),
+                ("max_sparse_symbols", C.c_uint32), ("_reserved", C.c_uint32)]
+
+
+assert C.sizeof(kme_config) == 64
 
 
 class kme_orders(C.Structure):
@@ -247,10 +254,10 @@ class EpochResult:
 
 def default_config(mode: int, max_symbols: int, max_epoch: int, max_resting: int, max_trades: int | None = None,
                    max_accounts: int = 0, ledger_capacity: int = 1 << 16, device: int = 0,
-                   flags: int = 0, light_max: int = 0) -> kme_config:
+                   flags: int = 0, light_max: int = 0, max_sparse_symbols: int = 0) -> kme_config:
     return kme_config(ABI_VERSION, mode, max_symbols, max_accounts, max_epoch,
                       max_trades if max_trades is not None else max(4 * max_epoch, 1 << 16),
-                      max_resting, ledger_capacity, device, 0, flags, light_max)
+                      max_resting, ledger_capacity, device, 0, flags, light_max, max_sparse_symbols, 0)
 
 
 class Engine:
