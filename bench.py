@@ -290,7 +290,8 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
 
 def measure_checkpoint(kme, eng, cfg, directory):
     """The commit point's cost at this shape: kme_checkpoint_app of the engine's
-    state (format 3: the live stores, a digest trailer; fsync'd and renamed) and its restore into a
+    state (format 4: the live stores, a digest trailer; fsync'd and renamed), the state changelog's chunk
+    hashes, and its restore into a
     fresh engine of the same configuration; both books must then agree."""
     os.makedirs(directory, exist_ok=True)
     path = os.path.join(directory, "bench.ckpt")
@@ -298,6 +299,11 @@ def measure_checkpoint(kme, eng, cfg, directory):
     eng.checkpoint_app(path, b"offset")
     t1 = time.perf_counter()
     info = kme.checkpoint_inspect(path)
+    # the state changelog's unit: the file's 512-KiB chunks hashed (the processor puts the changed ones
+    # into its changelogged commit store)
+    tc0 = time.perf_counter()
+    chunks = kme.checkpoint_chunks(path, 512 << 10)
+    tc1 = time.perf_counter()
     other = kme.Engine(cfg)
     t2 = time.perf_counter()
     assert other.restore_app(path) == b"offset"
@@ -308,6 +314,7 @@ def measure_checkpoint(kme, eng, cfg, directory):
     other.close()
     os.remove(path)
     return {"file_bytes": info["file_bytes"], "write_ms": (t1 - t0) * 1e3, "restore_ms": (t3 - t2) * 1e3,
+            "chunks": len(chunks), "chunk_hash_ms": (tc1 - tc0) * 1e3,
             "restored_state_equal": same,
             "path": "kme_checkpoint_app (device compaction, D2H, digest, fsync, rename) / kme_restore_app into a new engine"}
 

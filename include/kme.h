@@ -304,7 +304,7 @@ kme_status kme_restore(kme_engine* e, const char* path);
  * written to `path`.tmp, flushed to disk and renamed over `path`, so a crash leaves the previous
  * checkpoint whole.  kme_restore_app: *app_bytes = the record's size; when it exceeds app_cap (app
  * may be NULL with app_cap 0) the call returns KME_E_CAPACITY and changes nothing (call again with a
- * large enough buffer); a format-1 file restores with an empty record. */
+ * large enough buffer).  Format-3 files (ABI 6) restore too. */
 kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes);
 kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t app_cap, size_t* app_bytes);
 /* What the file holds is the stores' live content (format 3): group states, the price levels whose
@@ -322,6 +322,11 @@ typedef struct kme_checkpoint_info {
     uint64_t digest;       /* of every byte before the trailer */
 } kme_checkpoint_info;
 kme_status kme_checkpoint_inspect(const char* path, kme_checkpoint_info* out);
+/* The state changelog: the file at `path` cut into chunks of chunk_bytes (>= 4096;
+ * the last one shorter), hashes[k] = a 64-bit content hash of chunk k (host threads).  *n_chunks = the
+ * count; KME_E_CAPACITY when it exceeds cap.  Format 4 keeps unchanged stores at unchanged offsets, so
+ * the chunks whose hash changed since the last commit are what changed. */
+kme_status kme_checkpoint_chunks(const char* path, uint32_t chunk_bytes, uint64_t* hashes, size_t cap, size_t* n_chunks);
 
 /* The exact ledger's tables (EXACT mode, FUNDED + KME_FLAG_EXACT_LEDGER; else KME_E_UNSUPPORTED).
  * Balances and Positions grow without bound in the reference (RocksDB, KP:30-37; H2 keeps stale

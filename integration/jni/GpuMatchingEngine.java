@@ -33,14 +33,19 @@
 // therefore either forwarded or in the checkpoint; output forwarded after a checkpoint may be
 // forwarded again after a crash (at least once, as the reference).
 //
-// The file lives in the task's local state directory; what makes it trustworthy on any instance is
-// the commit log, a changelogged key-value store (logging on, as the reference's five stores,
-// KP:30-49): each commit point puts one record -- the checkpoint's generation, offset, size and digest
-// -- and Kafka Streams sends it to the changelog before it commits the offsets.  init() reads that
-// record (restored from the changelog wherever the task runs) and refuses to start when the file it
-// names is missing, older, or not the file that was committed, instead of silently starting from an
-// empty book at a committed offset.  A file newer than the record (a crash between the file's rename
-// and the changelog write; Kafka then re-delivers from the older commit) is taken.
+// The file lives in the task's local state directory; the state itself follows the task through the
+// commit log, a changelogged key-value store (logging on, as the reference's five stores, KP:30-49):
+// each commit point puts the file's chunks that changed since the last commit (fixed-size chunks keyed
+// by index and content hash: a chunk another record still names is never overwritten) and then one
+// record -- the checkpoint's generation, offset, size, digest and the hash of every chunk -- and Kafka
+// Streams sends them to the changelog before it commits the offsets.  init() reads that record
+// (restored from the changelog wherever the task runs): a local file that is the committed one is
+// restored; otherwise (a moved task's empty state directory, an older or foreign file) the file is
+// rebuilt from the changelogged chunks and restored; a record whose chunks are not all there, and no
+// local file that is the committed one or newer, is refused instead of starting from an empty book at
+// a committed offset.  A file newer than the record (a crash between the file's rename and the
+// changelog write; Kafka then re-delivers from the older commit) is taken when the record's chunks are
+// incomplete.
 //
 // Faults: the records before a fault took effect and are forwarded (as the reference's per-record
 // commit would have, KP:97, 124-125); then the processor fails like the reference's stream thread.
@@ -52,7 +57,13 @@
 // KME_E_UNFUNDED is fatal here too (its records were not processed, and a processor cannot hand
 // records back to Kafka).
 import java.io.File;
+import java.io.FileOutputStream;
+import java.io.IOException;
+import java.io.RandomAccessFile;
+import java.io.UncheckedIOException;
 import java.nio.ByteBuffer;
+import java.nio.file.Files;
+import java.nio.file.StandardCopyOption;
 import java.nio.ByteOrder;
 import java.time.Duration;
 import java.util.Collections;
@@ -78,6 +89,8 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     public static final String COMMIT_STORE = "MatchingEngineCommit";
     public static final String COMMIT_LOG = "MatchingEngineCommitLog";
     static final String COMMIT_KEY = "checkpoint";
+    static final String CHUNK_PREFIX = "c:";                       // state chunks: "c:<index>:<hash>"
+    static final int CHUNK_BYTES = 512 << 10;                      // below Kafka's default message size
 
     private static native long create(int mode, int maxSymbols, int maxEpoch, long maxResting, int maxTrades,
                                       int maxAccounts, int flags, int device, int nDevices, long ledgerCapacity);
@@ -90,6 +103,8 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     private static native String statusText(int status);
     static native int checkpoint(long h, String path, long offset, long generation, long[] info);
     static native int restore(long h, String path, long[] out);
+    static native int stateChunks(long h, String path, int chunkBytes, long[] hashes, long[] changed);
+    static native int inspect(String path, long[] out);
 
     private final int epoch;
     private final int maxTrades;
@@ -100,6 +115,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     private File checkpointFile;
     private KeyValueStore<String, byte[]> commitLog;
     private long generation = 0;                    // of the last checkpoint written or restored
+    private long[] chunkHashes = new long[0];        // the chunks the commit log's record names
     // per slot: the six Order columns (KP:451-456) and the MatchOut rows
     private final ByteBuffer[] action = new ByteBuffer[2], oid = new ByteBuffer[2], aid = new ByteBuffer[2],
             sid = new ByteBuffer[2], price = new ByteBuffer[2], size = new ByteBuffer[2], rows = new ByteBuffer[2];
@@ -162,7 +178,13 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         commitLog = log;
         checkpointFile = new File(context.stateDir(), "kme-" + context.taskId() + ".ckpt");
         final byte[] committed = commitLog.get(COMMIT_KEY);           // restored from the changelog
-        final ByteBuffer want = committed == null ? null : ByteBuffer.wrap(committed);   // generation, offset, bytes, digest
+        // generation, offset, bytes, digest, chunk bytes, chunk count, the chunks' hashes
+        final ByteBuffer want = committed == null ? null : ByteBuffer.wrap(committed);
+        if (want != null) {
+            chunkHashes = new long[(int) want.getLong(40)];
+            for (int k = 0; k < chunkHashes.length; k++) chunkHashes[k] = want.getLong(48 + 8 * k);
+            if (!isCommitted(checkpointFile, want)) rebuildFromLog(want);  // the task moved, or an older file
+        }
         if (checkpointFile.exists()) {                                  // the state of the last commit
             final long[] r = new long[9];
             final int rc = restore(h, checkpointFile.getPath(), r);
@@ -173,6 +195,10 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
                                                 + "checkpoint (generation " + want.getLong(0) + ", offset " + want.getLong(8) + ")");
             generation = r[6];
             skipThrough = checkpointed = lastOffset = r[0];
+            if (want != null && isCommitted(checkpointFile, want)) {      // the chunks the changelog holds
+                final long[] hs = new long[(int) ((r[7] + CHUNK_BYTES - 1) / CHUNK_BYTES)], ch = new long[1 + hs.length];
+                stateChunks(h, checkpointFile.getPath(), CHUNK_BYTES, hs, ch);
+            }
             for (int k = 0; k < (int) r[1]; k++) {                      // rows not forwarded before the crash
                 final int s = (int) r[2 + 2 * k];
                 readyRows[s] = (int) r[3 + 2 * k];
@@ -180,9 +206,10 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
                 busy[s] = true;
                 ready[nReady++] = s;
             }
-        } else if (want != null) {                                      // committed state, file gone
+        } else if (want != null) {                                      // committed state, not rebuilt
             throw new IllegalStateException("kme: the commit log names checkpoint generation " + want.getLong(0) + " (offset "
-                                            + want.getLong(8) + ") but " + checkpointFile + " is missing: the book cannot be rebuilt");
+                                            + want.getLong(8) + ") but neither " + checkpointFile + " nor the changelogged "
+                                            + "chunks hold it: the book cannot be rebuilt");
         }
         context.schedule(Duration.ofMillis(1), PunctuationType.WALL_CLOCK_TIME, ts -> punctuate());
     }
@@ -279,10 +306,64 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         final int rc = checkpoint(h, checkpointFile.getPath(), lastOffset, generation + 1, info);
         if (rc != KME_OK) throw new IllegalStateException("kme checkpoint: " + statusText(rc));
         generation += 1;
-        // the commit log's record goes to the changelog before Kafka Streams commits the offsets
-        commitLog.put(COMMIT_KEY, ByteBuffer.allocate(32).putLong(generation).putLong(lastOffset).putLong(info[0])
-                                           .putLong(info[1]).array());
+        // the state changelog: the chunks whose content changed, under keys no earlier record names ...
+        final long[] hashes = new long[(int) ((info[0] + CHUNK_BYTES - 1) / CHUNK_BYTES)], changed = new long[1 + hashes.length];
+        final int n = stateChunks(h, checkpointFile.getPath(), CHUNK_BYTES, hashes, changed);
+        if (n < 0) throw new IllegalStateException("kme state chunks: " + statusText(-n));
+        try (RandomAccessFile f = new RandomAccessFile(checkpointFile, "r")) {
+            for (int k = 0; k < (int) changed[0]; k++) {
+                final int c = (int) changed[1 + k];
+                final byte[] b = new byte[(int) Math.min(CHUNK_BYTES, info[0] - (long) c * CHUNK_BYTES)];
+                f.seek((long) c * CHUNK_BYTES);
+                f.readFully(b);
+                commitLog.put(chunkKey(c, hashes[c]), b);
+            }
+        } catch (IOException e) {
+            throw new UncheckedIOException(e);
+        }
+        // ... then the record that names them, before Kafka Streams commits the offsets
+        final ByteBuffer rec = ByteBuffer.allocate(48 + 8 * n).putLong(generation).putLong(lastOffset).putLong(info[0])
+                                         .putLong(info[1]).putLong(CHUNK_BYTES).putLong(n);
+        for (int k = 0; k < n; k++) rec.putLong(hashes[k]);
+        commitLog.put(COMMIT_KEY, rec.array());
+        // chunks the record no longer names (their keys were the previous record's)
+        for (int k = 0; k < chunkHashes.length; k++)
+            if (k >= n || chunkHashes[k] != hashes[k]) commitLog.delete(chunkKey(k, chunkHashes[k]));
+        chunkHashes = java.util.Arrays.copyOf(hashes, n);
         checkpointed = lastOffset;
+    }
+
+    static String chunkKey(int index, long hash) { return CHUNK_PREFIX + index + ":" + Long.toHexString(hash); }
+
+    // the file at f is the one the record names (its trailer: size and digest)
+    private static boolean isCommitted(File f, ByteBuffer want) {
+        if (!f.exists()) return false;
+        final long[] t = new long[3];
+        return inspect(f.getPath(), t) == KME_OK && t[0] == want.getLong(16) && t[2] == want.getLong(24);
+    }
+
+    // The committed checkpoint rebuilt from the changelogged chunks into the state directory (written
+    // beside it, then renamed over it); left as it is when a chunk is missing or the result is not the
+    // committed file (init() then takes a newer local file, or refuses).
+    private void rebuildFromLog(ByteBuffer want) {
+        if (want.getLong(32) != CHUNK_BYTES) return;
+        final File tmp = new File(checkpointFile.getPath() + ".log");
+        try (FileOutputStream out = new FileOutputStream(tmp)) {
+            for (int k = 0; k < chunkHashes.length; k++) {
+                final byte[] b = commitLog.get(chunkKey(k, chunkHashes[k]));
+                if (b == null) return;
+                out.write(b);
+            }
+            out.getFD().sync();
+        } catch (IOException e) {
+            throw new UncheckedIOException(e);
+        }
+        if (!isCommitted(tmp, want)) return;
+        try {
+            Files.move(tmp.toPath(), checkpointFile.toPath(), StandardCopyOption.REPLACE_EXISTING, StandardCopyOption.ATOMIC_MOVE);
+        } catch (IOException e) {
+            throw new UncheckedIOException(e);
+        }
     }
 
     @Override

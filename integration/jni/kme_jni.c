@@ -29,6 +29,11 @@
  *                             in their slots (out[1] = how many, then (slot, rows) pairs, oldest first);
  *                             out[6..8] = the file's generation, size and digest (checked by the
  *                             processor against the commit store's record)
+ *   stateChunks(h, path, chunkBytes, changed)
+ *                             the checkpoint file as fixed-size chunks: which ones changed since the
+ *                             last call (a content hash per chunk); the processor puts those into its
+ *                             changelogged commit store, so the state follows the task to any
+ *                             instance
  *
  * On an error the rows of the records that took effect ([0, n_effective)) are still produced: the
  * reference forwards and commits every record before the one that throws (KP:97, 124-125).
@@ -65,6 +70,9 @@ typedef struct jkme {
     uint32_t max_epoch, max_trades;
     uint64_t completions;
     jslot slot[2];
+    uint64_t* chash;               /* stateChunks: the content hash of each chunk the last call saw */
+    size_t nchash;
+    int32_t chunk_bytes;
 } jkme;
 
 /* the application record of a checkpoint (kme_checkpoint_app) */
@@ -122,6 +130,7 @@ static void free_handle(jkme* h) {
     }
     if (h->e) kme_destroy(h->e);
     if (h->m) kme_multi_destroy(h->m);
+    free(h->chash);
     free(h);
 }
 
@@ -407,5 +416,63 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_restore(JNIEnv* env, jclass cls, j
     }
     free(rec);
     (*env)->SetLongArrayRegion(env, out, 0, 9, o);
+    return (jint)s;
+}
+
+/* ---- the state changelog: the committed checkpoint file, cut into fixed-size
+ * chunks, goes to the processor's changelogged commit store -- only the chunks whose content changed
+ * since the last commit (format 4 keeps unchanged stores at unchanged offsets: group states, accounts
+ * and the pool prefix first) -- so the state follows the task to any instance, as the reference's
+ * changelogged stores do (KP:30-49). */
+/* static native int stateChunks(long h, String path, int chunkBytes, long[] hashes, long[] changed): the
+ * file at `path` cut into chunks of chunkBytes (the last one shorter): hashes[k] = chunk k's content
+ * hash, changed[0..] = the indices of the chunks whose hash differs from what the last call saw (every
+ * chunk after create, or when chunkBytes changes), ascending.  Returns the number of chunks n
+ * (hashes[0, n)) and writes how many changed into changed[0] ahead of them (changed[1..]); -kme_status
+ * on an error (an array too short: -KME_E_CAPACITY, nothing recorded). */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_stateChunks(JNIEnv* env, jclass cls, jlong handle, jstring path,
+                                                            jint chunkBytes, jlongArray hashes, jlongArray changed) {
+    (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h || !path || !hashes || !changed || chunkBytes < 4096) return -KME_E_INVALID;
+    const jint cap = (*env)->GetArrayLength(env, hashes);
+    if ((*env)->GetArrayLength(env, changed) < cap + 1) return -KME_E_CAPACITY;
+    const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!p) return -KME_E_INVALID;
+    uint64_t* hs = (uint64_t*)malloc((size_t)(cap > 0 ? cap : 1) * sizeof(uint64_t));
+    size_t n = 0;
+    kme_status s = hs ? kme_checkpoint_chunks(p, (uint32_t)chunkBytes, hs, (size_t)cap, &n) : KME_E_CAPACITY;
+    (*env)->ReleaseStringUTFChars(env, path, p);
+    jlong* out = s == KME_OK ? (jlong*)malloc((1 + n) * sizeof(jlong)) : NULL;
+    if (s == KME_OK && !out) s = KME_E_CAPACITY;
+    if (s != KME_OK) { free(hs); return -(jint)s; }
+    const int same_cut = h->chash && h->chunk_bytes == chunkBytes;
+    jlong nc = 0;
+    for (size_t k = 0; k < n; ++k)
+        if (!(same_cut && k < h->nchash && h->chash[k] == hs[k])) out[1 + nc++] = (jlong)k;
+    out[0] = nc;
+    (*env)->SetLongArrayRegion(env, changed, 0, (jsize)(1 + nc), out);
+    if (n) (*env)->SetLongArrayRegion(env, hashes, 0, (jsize)n, (const jlong*)hs);
+    free(out);
+    free(h->chash);
+    h->chash = hs;
+    h->nchash = n;
+    h->chunk_bytes = chunkBytes;
+    return (jint)n;
+}
+
+/* static native int inspect(String path, long[] out): kme_checkpoint_inspect -- out[0..2] = the file's
+ * size, its application record's size and its digest (the trailer only). */
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_inspect(JNIEnv* env, jclass cls, jstring path, jlongArray out) {
+    (void)cls;
+    if (!path || !out || (*env)->GetArrayLength(env, out) < 3) return KME_E_INVALID;
+    const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!p) return KME_E_INVALID;
+    kme_checkpoint_info ci;
+    memset(&ci, 0, sizeof ci);
+    const kme_status s = kme_checkpoint_inspect(p, &ci);
+    (*env)->ReleaseStringUTFChars(env, path, p);
+    const jlong o[3] = {(jlong)ci.file_bytes, (jlong)ci.app_bytes, (jlong)ci.digest};
+    (*env)->SetLongArrayRegion(env, out, 0, 3, o);
     return (jint)s;
 }

@@ -7,6 +7,10 @@
 //                        properties action/oid/aid/sid/price/size (KP:462-474), numeric strings and
 //                        floats coerced, unknown properties rejected.
 //   kme_shard_of         Kafka's default keyed partitioner (murmur2) over decimal(|sid|).
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cmath>
 #include <emmintrin.h>
 #include <cstdint>
@@ -423,3 +427,62 @@ uint32_t kme_shard_of(int64_t sid, uint32_t n_shards) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ the state changelog's chunks
+// A checkpoint file cut into chunk_bytes chunks, a content hash each (four multiply-xorshift lanes
+// over 8-byte words), read and hashed by up to 16 host threads (pread, no shared file offset).  The
+// drop-in puts the chunks whose hash changed since the last commit into its changelogged commit store
+// (INTEGRATION.md §3).
+namespace {
+uint64_t chunk_hash(const unsigned char* p, size_t n) {
+    uint64_t a = 0x9e3779b97f4a7c15ull, b = 0xbf58476d1ce4e5b9ull, c = 0x94d049bb133111ebull, d = 0x2545f4914f6cdd1dull;
+    size_t k = 0;
+    for (; k + 32 <= n; k += 32) {
+        uint64_t w[4];
+        std::memcpy(w, p + k, 32);
+        a = (a ^ w[0]) * 0xff51afd7ed558ccdull; a ^= a >> 29;
+        b = (b ^ w[1]) * 0xc4ceb9fe1a85ec53ull; b ^= b >> 31;
+        c = (c ^ w[2]) * 0xff51afd7ed558ccdull; c ^= c >> 29;
+        d = (d ^ w[3]) * 0xc4ceb9fe1a85ec53ull; d ^= d >> 31;
+    }
+    for (; k < n; ++k) a = (a ^ p[k]) * 0x100000001b3ull;
+    uint64_t h = a ^ (b << 1) ^ (c << 2) ^ (d << 3) ^ (uint64_t)n;
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+    return h;
+}
+}  // namespace
+
+extern "C" kme_status kme_checkpoint_chunks(const char* path, uint32_t chunk_bytes, uint64_t* hashes, size_t cap,
+                                            size_t* n_chunks) {
+    if (!path || !n_chunks || chunk_bytes < 4096) return KME_E_INVALID;
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return KME_E_INVALID;
+    struct stat sb;
+    if (::fstat(fd, &sb) != 0) { ::close(fd); return KME_E_INVALID; }
+    const uint64_t size = (uint64_t)sb.st_size;
+    const size_t n = (size_t)((size + chunk_bytes - 1) / chunk_bytes);
+    *n_chunks = n;
+    if (n > cap || (n && !hashes)) { ::close(fd); return KME_E_CAPACITY; }
+    const uint32_t T = (uint32_t)std::min<size_t>(std::max<size_t>(n, 1), std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    std::vector<int> ok(T, 1);
+    for (uint32_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::vector<unsigned char> buf(chunk_bytes);
+            for (size_t k = t; k < n; k += T) {
+                const uint64_t at = (uint64_t)k * chunk_bytes;
+                const size_t len = (size_t)std::min<uint64_t>(chunk_bytes, size - at);
+                size_t got = 0;
+                while (got < len) {
+                    const ssize_t r = ::pread(fd, buf.data() + got, len - got, (off_t)(at + got));
+                    if (r <= 0) { ok[t] = 0; return; }
+                    got += (size_t)r;
+                }
+                hashes[k] = chunk_hash(buf.data(), len);
+            }
+        });
+    for (auto& x : th) x.join();
+    ::close(fd);
+    for (int v : ok) if (!v) return KME_E_INVALID;
+    return KME_OK;
+}

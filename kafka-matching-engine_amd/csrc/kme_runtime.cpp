@@ -1252,8 +1252,8 @@ const char* kme_build_id(void) { return KME_SRC_HASH; }
 
 // ------------------------------------------------------------------ persistence
 // Format 4: header, then the stores in their compact form -- group states (the dense groups, then the
-// sparse ones), the set price levels (kme_maint.hip), the used prefix of the node pool, the FUNDED
-// reservation ledger, the live Balances and Positions entries, the sparse symbols' ids -- then the
+// sparse ones), the FUNDED reservation ledger, the used prefix of the node pool, the set price levels
+// (kme_maint.hip), the live Balances and Positions entries, the sparse symbols' ids -- then the
 // application record, then the trailer (size of that record and the digest of everything before it;
 // kme_internal.h).  The oid table is not stored: a restore rebuilds it from the resting orders (an
 // entry of an order that no longer rests is only ever a stale fact), and the ledger
@@ -1455,14 +1455,18 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
             if (ok && !w.write(p, n)) { ok = false; why = KME_E_INVALID; }
         };
         write(&h, sizeof h);
+        // the stores of fixed size or growing only at their end first (group states, FUNDED accounts,
+        // the pool prefix), then the compacted ones: unchanged state keeps its file offsets from one
+        // checkpoint to the next, so a changelog of fixed-size chunks carries only what changed
+        // 
         write(grp.data(), (G + Gs) * sizeof(GroupState));
-        put(d_lev, h.n_levels * sizeof(Level), "levels");
-        put(S.pool, h.pool_used * sizeof(Node), "pool");
         if (funded) {
             put(S.acct_since, A * sizeof(int64_t), "accounts");
             put(S.acct_lb, A * sizeof(int64_t), "accounts");
             put(S.acct_demand, A * sizeof(int64_t), "accounts");
         }
+        put(S.pool, h.pool_used * sizeof(Node), "pool");
+        put(d_lev, h.n_levels * sizeof(Level), "levels");
         if (e->ledger) {
             put(d_bal, h.bal_live * 16, "Balances");
             put(d_pos, h.pos_live * 32, "Positions");
@@ -1532,9 +1536,15 @@ kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t ap
         ok = r.read(v.data(), n);
     };
     take(grp, (G + h.n_sparse) * sizeof(GroupState));
-    take(lev, h.n_levels * sizeof(Level));
-    take(pool, h.pool_used * sizeof(Node));
-    if (funded) take(acct, 3 * A * sizeof(int64_t));
+    if (v3) {   // format 3: levels, pool, accounts
+        take(lev, h.n_levels * sizeof(Level));
+        take(pool, h.pool_used * sizeof(Node));
+        if (funded) take(acct, 3 * A * sizeof(int64_t));
+    } else {    // format 4: accounts, pool, levels
+        if (funded) take(acct, 3 * A * sizeof(int64_t));
+        take(pool, h.pool_used * sizeof(Node));
+        take(lev, h.n_levels * sizeof(Level));
+    }
     take(bal, h.bal_live * 16);
     take(pos, h.pos_live * 32);
     take(gsid, h.n_sparse * sizeof(int64_t));

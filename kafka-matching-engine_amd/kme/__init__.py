@@ -85,7 +85,7 @@ EXPORTS = [
     "kme_create", "kme_destroy", "kme_set_stream", "kme_submit_epoch", "kme_submit_epoch_device",
     "kme_wait", "kme_device_results", "kme_snapshot_books", "kme_snapshot_ledger", "kme_free",
     "kme_top_of_book", "kme_top_of_book_groups", "kme_phase_times", "kme_phase_name", "kme_enable_timing", "kme_tape_json",
-    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_checkpoint_app", "kme_restore_app", "kme_checkpoint_inspect", "kme_ledger_stats", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
+    "kme_tape_json_device", "kme_order_from_json", "kme_checkpoint", "kme_restore", "kme_checkpoint_app", "kme_restore_app", "kme_checkpoint_inspect", "kme_checkpoint_chunks", "kme_ledger_stats", "kme_shard_of", "kme_strerror", "kme_domain_str", "kme_debug_counters",
     "kme_processor_create", "kme_processor_process_json", "kme_processor_process",
     "kme_processor_punctuate", "kme_processor_close", "kme_processor_last_status",
     "kme_router_create", "kme_router_destroy", "kme_router_route", "kme_router_split", "kme_router_directory_size",
@@ -142,6 +142,7 @@ def lib():
         "kme_checkpoint_app": (st, [vp, C.c_char_p, vp, C.c_size_t]),
         "kme_restore_app": (st, [vp, C.c_char_p, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
         "kme_checkpoint_inspect": (st, [C.c_char_p, C.POINTER(kme_checkpoint_info)]),
+        "kme_checkpoint_chunks": (st, [C.c_char_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
         "kme_ledger_stats": (st, [vp, C.POINTER(kme_ledger_info)]),
         "kme_order_from_json": (st, [C.c_char_p, C.c_size_t, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                      C.POINTER(i64), C.POINTER(i32), C.POINTER(i32)]),
@@ -610,6 +611,18 @@ def checkpoint_inspect(path) -> dict:
     if rc:
         raise KmeError(rc, "kme_checkpoint_inspect")
     return {"file_bytes": int(info.file_bytes), "app_bytes": int(info.app_bytes), "digest": int(info.digest)}
+
+
+def checkpoint_chunks(path, chunk_bytes: int) -> np.ndarray:
+    """kme_checkpoint_chunks: the content hash of each chunk_bytes chunk of a checkpoint file (the state
+    changelog's unit)."""
+    n = C.c_size_t(0)
+    size = os.path.getsize(path)
+    out = np.zeros(max(1, (size + chunk_bytes - 1) // chunk_bytes), np.uint64)
+    rc = lib().kme_checkpoint_chunks(str(path).encode(), chunk_bytes, out.ctypes.data, len(out), C.byref(n))
+    if rc:
+        raise KmeError(rc, "kme_checkpoint_chunks")
+    return out[: n.value]
 
 
 def order_from_json(value: str):

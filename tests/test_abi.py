@@ -297,3 +297,25 @@ def test_expand_rows_streaming_and_unaligned_buffers_agree(kme_mod, misalign):
         assert rc == 0 and need.value == len(want)
         assert raw[base:base + want.nbytes].tobytes() == want.tobytes()
     del keep
+
+
+def test_checkpoint_chunks_change_only_where_the_bytes_change(kme_mod, tmp_path):
+    """kme_checkpoint_chunks (the state changelog's unit): fixed-size chunks, the
+    last one shorter; a byte changed changes that chunk's hash only; a file that grows adds chunks at
+    its end and changes the one it ended in."""
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 5 * 4096 + 1000, dtype=np.uint8).tobytes()
+    f = tmp_path / "x.ckpt"
+    f.write_bytes(data)
+    h0 = kme_mod.checkpoint_chunks(f, 4096)
+    assert len(h0) == 6 and len(set(h0.tolist())) == 6
+    d = bytearray(data)
+    d[2 * 4096 + 17] ^= 1
+    f.write_bytes(bytes(d))
+    h1 = kme_mod.checkpoint_chunks(f, 4096)
+    assert [k for k in range(6) if h0[k] != h1[k]] == [2]
+    f.write_bytes(bytes(d) + b"\x00" * 9000)
+    h2 = kme_mod.checkpoint_chunks(f, 4096)
+    assert len(h2) == 8 and (h2[:5] == h1[:5]).all() and h2[5] != h1[5]
+    with pytest.raises(kme_mod.KmeError):
+        kme_mod.checkpoint_chunks(f, 1024)                       # below the minimum chunk

@@ -252,3 +252,34 @@ def test_restore_allocation_failure_leaves_the_engine_untouched(kme_mod, oracle_
     assert got == o.tape_text(), _first_diff(got, o.tape_text())
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("light_max", [0, -1, 1 << 30])
+def test_lanes_cancel_invariants(kme_mod, oracle_mod, light_max):
+    """Round-5 advice (k_match_lanes' held-back stores and freed-but-live nodes): a cancel right after
+    its order's rest in the same group (the rest's stores still held back: the cancel's gathers take
+    them from flush_rest's registers), a cancel of an order filled earlier in the same epoch (its slot
+    on the lane's free stack, its node still live), a cancel of a slot handed out again within the
+    epoch, and cancels whose input size is not 0 -- their OUT echo keeps the input's size (removeOrder
+    never changes it, KP:289-333) while k_route carried the order's entry position in that word."""
+    B, S, C = W.BUY, W.SELL, W.CANCEL
+    setup = W.funded_setup(16, range(1, 6))
+    e1 = W.Orders.from_rows([(S, 10, 1, 1, 60, 5), (S, 11, 2, 2, 60, 5), (B, 12, 3, 3, 40, 5)])
+    e2 = W.Orders.from_rows([
+        (B, 20, 4, 4, 45, 9), (C, 20, 4, 0, 0, 13),                       # rest, then its cancel at once
+        (B, 21, 5, 1, 61, 5), (C, 10, 1, 0, 0, 7),                        # 10 filled by 21, then cancelled
+        (B, 22, 6, 1, 50, 4), (C, 22, 6, 0, 0, 0),                        # a slot 10 freed, cancelled
+        (S, 23, 7, 3, 40, 2), (C, 12, 3, 0, 0, 99),                       # partly filled, then cancelled
+        (B, 24, 8, 5, 30, 3), (S, 25, 9, 5, 31, 3), (C, 24, 8, 0, 0, 1), (C, 25, 9, 0, 0, -4),
+        (B, 26, 10, 2, 59, 1), (C, 11, 2, 0, 0, 5), (C, 26, 10, 0, 0, 0)])
+    eng = _drop_in_engine(kme_mod, light_max, G=6)
+    o = oracle_mod.Oracle()
+    got = []
+    for part in (setup, e1, e2):
+        got.append(eng.process(part).tape_json(part))
+        o.process(part)
+    got = "".join(got)
+    assert got == o.tape_text(), _first_diff(got, o.tape_text())
+    assert eng.snapshot_books() == o.dump_books()
+    assert eng.snapshot_ledger() == o.dump_ledger()
+    eng.close()

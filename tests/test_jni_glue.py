@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
 CHECK_LIB = os.path.join(ROOT, "integration", "jni", "libkme_jni_check.so")
 SYMBOLS = ["create", "destroy", "buffer", "submit", "poll", "complete", "forwarded", "statusText", "checkpoint",
-           "restore"]
+           "restore", "stateChunks", "inspect"]
 ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
                       ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
 assert ROW_DTYPE.itemsize == 48
@@ -120,6 +120,10 @@ def _lib():
     lib.Java_GpuMatchingEngine_complete.restype = I
     lib.Java_GpuMatchingEngine_statusText.argtypes = [P, P, I]
     lib.Java_GpuMatchingEngine_statusText.restype = P
+    lib.Java_GpuMatchingEngine_stateChunks.argtypes = [P, P, L, P, I, P, P]
+    lib.Java_GpuMatchingEngine_stateChunks.restype = I
+    lib.Java_GpuMatchingEngine_inspect.argtypes = [P, P, P, P]
+    lib.Java_GpuMatchingEngine_inspect.restype = I
     return lib
 
 
@@ -284,10 +288,16 @@ class JavaProcessor:
     offset (context.offset()); forwarded rows are collected in `out`; commit_point() is the commit
     hook's StateStore.flush(), which Kafka Streams calls before it commits the consumed offsets.
     `commit_log` is the changelogged commit-log store (a dict that survives the process: Kafka
-    Streams restores it from its changelog wherever the task runs)."""
+    Streams restores it from its changelog wherever the task runs): the record naming the committed
+    checkpoint, and the checkpoint file's chunks keyed by index and content hash (the state changelog:
+    a restart whose state directory lost the file rebuilds it from them)."""
 
-    def __init__(self, lib, j, path, epoch, max_trades, create_args, commit_log=None):
+    CHUNK_BYTES = 512 << 10
+
+    def __init__(self, lib, j, path, epoch, max_trades, create_args, commit_log=None, chunk_bytes=None):
         self.lib, self.j, self.path, self.epoch = lib, j, str(path), epoch
+        if chunk_bytes:
+            self.CHUNK_BYTES = chunk_bytes
         self.commit_log = {} if commit_log is None else commit_log
         self.h = lib.Java_GpuMatchingEngine_create(j.env, None, *create_args)
         assert self.h and not j.thrown, j.thrown
@@ -298,7 +308,10 @@ class JavaProcessor:
         self.last_offset = self.skip_through = self.checkpointed = -1
         self.generation = 0
         self.out = []
-        want = self.commit_log.get("checkpoint")          # (generation, offset, bytes, digest)
+        want = self.commit_log.get("checkpoint")          # (generation, offset, bytes, digest, chunk bytes, hashes)
+        self.chunk_hashes = list(want[5]) if want is not None else []
+        if want is not None and not self._is_committed(self.path, want):
+            self._rebuild_from_log(want)                    # the task moved, or an older file
         if os.path.exists(self.path):
             r = j.arr(np.zeros(9, np.int64))
             rc = lib.Java_GpuMatchingEngine_restore(j.env, None, self.h, _jstr(j, self.path), r)
@@ -309,6 +322,8 @@ class JavaProcessor:
                 self._fail(f"checkpoint generation {o[6]} is not the committed one {want}")
             self.generation = int(o[6])
             self.skip_through = self.checkpointed = self.last_offset = int(o[0])
+            if want is not None and self._is_committed(self.path, want):
+                self._state_chunks(int(o[7]))               # (the chunks the changelog holds)
             for k in range(int(o[1])):
                 s = int(o[2 + 2 * k])
                 self.ready_rows[s] = int(o[3 + 2 * k])
@@ -316,7 +331,38 @@ class JavaProcessor:
                 self.busy[s] = True
                 self.ready.append(s)
         elif want is not None:
-            self._fail(f"the commit log names checkpoint generation {want[0]} but {self.path} is missing")
+            self._fail(f"the commit log names checkpoint generation {want[0]} but neither {self.path} nor the chunks hold it")
+
+    @staticmethod
+    def _chunk_key(k, h):
+        return f"c:{k}:{h & 0xFFFFFFFFFFFFFFFF:x}"
+
+    def _is_committed(self, path, want):
+        if not os.path.exists(path):
+            return False
+        t = self.j.arr(np.zeros(3, np.int64))
+        rc = self.lib.Java_GpuMatchingEngine_inspect(self.j.env, None, _jstr(self.j, str(path)), t)
+        return rc == 0 and int(self.j.objs[t][0]) == want[2] and int(self.j.objs[t][2]) == want[3]
+
+    def _rebuild_from_log(self, want):
+        if want[4] != self.CHUNK_BYTES:
+            return
+        parts = [self.commit_log.get(self._chunk_key(k, h)) for k, h in enumerate(want[5])]
+        if any(b is None for b in parts):
+            return
+        tmp = self.path + ".log"
+        with open(tmp, "wb") as f:
+            f.write(b"".join(parts))
+        if self._is_committed(tmp, want):
+            os.replace(tmp, self.path)
+
+    def _state_chunks(self, file_bytes):
+        n = (file_bytes + self.CHUNK_BYTES - 1) // self.CHUNK_BYTES
+        hs, ch = self.j.arr(np.zeros(max(n, 1), np.int64)), self.j.arr(np.zeros(n + 1, np.int64))
+        got = self.lib.Java_GpuMatchingEngine_stateChunks(self.j.env, None, self.h, _jstr(self.j, self.path), self.CHUNK_BYTES, hs, ch)
+        assert got == n, (got, n)
+        changed = self.j.objs[ch]
+        return [int(x) for x in self.j.objs[hs][:n]], [int(x) for x in changed[1:1 + int(changed[0])]]
 
     def _fail(self, msg):
         """init() throws; the task is torn down (close -> destroy)."""
@@ -397,7 +443,19 @@ class JavaProcessor:
         self.generation += 1
         fb, dg = (int(x) for x in self.j.objs[info])
         assert fb == os.path.getsize(self.path)
-        self.commit_log["checkpoint"] = (self.generation, self.last_offset, fb, dg)
+        # the state changelog: the chunks that changed, then the record naming every chunk, then the
+        # keys the record no longer names
+        hashes, changed = self._state_chunks(fb)
+        with open(self.path, "rb") as f:
+            for k in changed:
+                f.seek(k * self.CHUNK_BYTES)
+                self.commit_log[self._chunk_key(k, hashes[k])] = f.read(self.CHUNK_BYTES)
+        self.chunks_put = len(changed)
+        self.commit_log["checkpoint"] = (self.generation, self.last_offset, fb, dg, self.CHUNK_BYTES, tuple(hashes))
+        for k, h in enumerate(self.chunk_hashes):
+            if k >= len(hashes) or hashes[k] != h:
+                self.commit_log.pop(self._chunk_key(k, h), None)
+        self.chunk_hashes = hashes
         self.checkpointed = self.last_offset
 
     def close(self):
@@ -621,13 +679,17 @@ def test_multi_gpu_drop_in_re_splits_credit(oracle_mod, tmp_path, monkeypatch, r
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("damage", ["missing", "stale", "foreign"])
-def test_restart_refuses_a_checkpoint_the_commit_log_does_not_name(oracle_mod, tmp_path, damage):
-    """Round-4 verdict: a commit point that cannot diverge silently.  Each commit point logs (generation,
-    offset, size, digest) of its checkpoint to the changelogged commit log; a restart whose file is
-    missing (task moved without its state directory), older (a stale copy) or another file of the same
-    generation fails the processor loudly instead of starting from an empty or wrong book at a committed
-    offset.  A file newer than the log's record is taken (the crash fell between the file's rename and
-    the changelog write)."""
+def test_restart_takes_the_committed_state_from_the_changelog(oracle_mod, tmp_path, damage):
+    """Round-5 verdict (What's missing 2, row f next-3): the state follows the task.  Each commit point
+    puts the checkpoint's changed chunks and then a record naming every chunk (generation, offset,
+    size, digest, chunk hashes) into the changelogged commit log.  A restart whose state directory
+    lost the file (the task moved: `missing`), holds an older one (`stale`) or another run's file of the
+    same generation (`foreign`) rebuilds the committed file from the changelog and resumes: its rows
+    after the restart plus the rows forwarded before the commit point are the oracle's tape.  Only the
+    chunks that changed go to the changelog: a commit after a few records puts few of them.  When the
+    changelog's chunks are incomplete too, the processor fails loudly instead of starting from an empty
+    or wrong book; a file newer than the log's record is then taken (the crash fell between the file's
+    rename and the changelog writes)."""
     import shutil
 
     lib = _lib()
@@ -638,33 +700,58 @@ def test_restart_refuses_a_checkpoint_the_commit_log_does_not_name(oracle_mod, t
     args = (1, 17, epoch, 1 << 15, max_trades, 64, 3, 0, 1, 1 << 12)
     ckpt = tmp_path / "kme-0_1.ckpt"
     log = {}
-    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
+    CB = 1 << 14                                                    # (small chunks: a small state shows the delta)
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log, CB)
     n = len(orders)
     _drive(p, orders, 0, n // 3)
     p.commit_point()
+    full = p.chunks_put
     shutil.copy(ckpt, tmp_path / "gen1.ckpt")
-    _drive(p, orders, n // 3, 2 * n // 3)
+    _drive(p, orders, n // 3, n // 3 + 5)                         # a few records: few chunks change
     p.commit_point()
-    assert log["checkpoint"][0] == 2
+    assert 0 < p.chunks_put < full // 2, (p.chunks_put, full)
+    _drive(p, orders, n // 3 + 5, 2 * n // 3)
+    p.commit_point()
+    c2 = p.last_offset
+    F = sum(len(x) for x in p.out)
+    assert log["checkpoint"][0] == 3
+    assert sorted(k for k in log if k.startswith("c:")) == sorted(p._chunk_key(k, h) for k, h in enumerate(log["checkpoint"][5]))
+    _drive(p, orders, 2 * n // 3, 2 * n // 3 + 500)
+    first = p.rows_out()[:F]
     p.crash()
     if damage == "missing":
         os.remove(ckpt)
     elif damage == "stale":
         shutil.copy(tmp_path / "gen1.ckpt", ckpt)
     else:   # a file of the same generation written by another run: same name, other content
-        other = JavaProcessor(lib, j, tmp_path / "other.ckpt", epoch, max_trades, args, {})
-        _drive(other, orders, 0, n // 3)
-        other.commit_point()
-        _drive(other, orders, n // 3, n // 2)
-        other.commit_point()
+        other = JavaProcessor(lib, j, tmp_path / "other.ckpt", epoch, max_trades, args, {}, CB)
+        for a, b in ((0, n // 3), (n // 3, n // 2), (n // 2, n // 2 + 10)):
+            _drive(other, orders, a, b)
+            other.commit_point()
         other.crash()
         shutil.copy(tmp_path / "other.ckpt", ckpt)
+    q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log, CB)
+    assert q.generation == 3 and q.skip_through == c2
+    _drive(q, orders, c2 + 1, n)
+    q.close()
+    got = np.concatenate([first, q.rows_out()])
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
+    # the changelog's chunks incomplete as well: refused loudly (the damaged local file is not taken)
+    broken = dict(log)
+    broken.pop(next(k for k in broken if k.startswith("c:")))
+    if damage == "missing":
+        os.remove(ckpt)
+    else:
+        shutil.copy(tmp_path / "gen1.ckpt", ckpt)
     with pytest.raises(IllegalState):
-        JavaProcessor(lib, j, ckpt, epoch, max_trades, args, log)
-    # the intact file restarts (control), and a file one generation ahead of the log is taken
-    q = JavaProcessor(lib, j, tmp_path / "gen1.ckpt", epoch, max_trades, args, {"checkpoint": (0, -1, 0, 0)})
-    assert q.generation == 1 and q.skip_through == n // 3 - 1
-    q.crash()
+        JavaProcessor(lib, j, ckpt, epoch, max_trades, args, broken, CB)
+    # a file one generation ahead of the log's record, whose chunks are incomplete, is taken
+    r = JavaProcessor(lib, j, tmp_path / "gen1.ckpt", epoch, max_trades, args,
+                      {"checkpoint": (0, -1, 0, 0, CB, (7,))}, CB)
+    assert r.generation == 1 and r.skip_through == n // 3 - 1
+    r.crash()
 
 
 @pytest.mark.gpu
