@@ -424,9 +424,12 @@ kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c);
  * -- except, with EXACT_LEDGER | SERIAL_FALLBACK, a refusal of the funded proof (KME_E_UNFUNDED): the
  * shards are retired and one engine of those flags on devices[0] takes the stream (SURVEY §8e:
  * outside the funded domain only one engine is exact), built by replaying the input history kept
- * since the start (env KME_MULTI_HISTORY records at most, default 2^25; past it, or after a restore
- * of a sharded checkpoint, the refusal stays fatal); it answers the rest of that epoch and every later
- * one, synchronously at submit.  Its checkpoints are the one engine's (the manifest says so). */
+ * since the start (env KME_MULTI_HISTORY records at most, default 2^25; past it the refusal stays
+ * fatal, kme_multi_info says so and stderr says it once); it answers the rest of that epoch and every
+ * later one, synchronously at submit.  Its checkpoints are the one engine's (the manifest says so).
+ * The history survives restarts: each checkpoint appends the records since the previous one to
+ * `path`.hist (fsync'd before the manifest naming its length and digest is committed), and a restore
+ * reads it back. */
 typedef struct kme_multi kme_multi;
 kme_status kme_multi_create(const kme_config* cfg, uint32_t n, const int32_t* devices, kme_multi** out);
 kme_status kme_multi_destroy(kme_multi* m);
@@ -434,13 +437,22 @@ kme_status kme_multi_destroy(kme_multi* m);
 kme_status kme_multi_submit_epoch_host(kme_multi* m, const kme_orders* in_host, uint32_t n, const kme_epoch_result* out_host);
 kme_status kme_multi_poll(kme_multi* m, int* done);
 kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st);
-/* as kme_checkpoint_app / kme_restore_app: every engine to `path`.g<generation>.<k>, then a manifest at
- * `path` (written and renamed last: the commit of the set); a restore also rebuilds the router's
- * oid directory from the engines' resting orders */
+/* as kme_checkpoint_app / kme_restore_app: every engine to `path`.g<generation>.<k>, the input history
+ * onto `path`.hist, then a manifest at `path` (written and renamed last: the commit of the set); a
+ * restore also rebuilds the router's oid directory from the engines' resting orders and reads the
+ * history back (a missing or damaged `path`.hist does not fail the restore: consolidation is off) */
 kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* app, size_t app_bytes);
 kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size_t app_cap, size_t* app_bytes);
 /* engine k (snapshots, diagnostics) */
 kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out);
+/* Whether an epoch the shards cannot prove is survivable now (can_consolidate: the flags allow it, the
+ * shards still run and the input history since the start is complete), the history's size and cap, the
+ * records of it the last checkpoint made durable, and the checkpoint generation. */
+typedef struct kme_multi_status {
+    uint32_t n_engines, consolidated, can_consolidate, failed;
+    uint64_t history_records, history_cap, history_saved, generation;
+} kme_multi_status;
+kme_status kme_multi_info(kme_multi* m, kme_multi_status* out);
 
 /* Wall-clock (HIP event) duration in ms of each kernel phase of the last epoch; index by name
  * (kme_phase_names).  Used by bench.py for the roofline of the dominant kernel. */

@@ -105,6 +105,7 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
     static native int restore(long h, String path, long[] out);
     static native int stateChunks(long h, String path, int chunkBytes, long[] hashes, long[] changed);
     static native int inspect(String path, long[] out);
+    static native int shardStatus(long h, long[] out);
 
     private final int epoch;
     private final int maxTrades;
@@ -364,6 +365,14 @@ public final class GpuMatchingEngine implements Processor<String, Order> {
         } catch (IOException e) {
             throw new UncheckedIOException(e);
         }
+    }
+
+    // nDevices > 1: {engines, consolidated, can consolidate, failed, history records, history cap,
+    // history records made durable, checkpoint generation} -- whether an epoch no shard can prove is
+    // survivable now (kme_multi_info); null for one engine
+    public long[] shardStatus() {
+        final long[] out = new long[8];
+        return shardStatus(h, out) == KME_OK ? out : null;
     }
 
     @Override

@@ -29,6 +29,9 @@
  *                             in their slots (out[1] = how many, then (slot, rows) pairs, oldest first);
  *                             out[6..8] = the file's generation, size and digest (checked by the
  *                             processor against the commit store's record)
+ *   shardStatus(h, out)       nDevices > 1: whether an epoch no shard can prove is survivable now
+ *                             (kme_multi_info: the input history since the start is complete), the
+ *                             history's size, cap and durable part; a single engine: status INVALID
  *   stateChunks(h, path, chunkBytes, changed)
  *                             the checkpoint file as fixed-size chunks: which ones changed since the
  *                             last call (a content hash per chunk); the processor puts those into its
@@ -474,5 +477,18 @@ JNIEXPORT jint JNICALL Java_GpuMatchingEngine_inspect(JNIEnv* env, jclass cls, j
     (*env)->ReleaseStringUTFChars(env, path, p);
     const jlong o[3] = {(jlong)ci.file_bytes, (jlong)ci.app_bytes, (jlong)ci.digest};
     (*env)->SetLongArrayRegion(env, out, 0, 3, o);
+    return (jint)s;
+}
+
+JNIEXPORT jint JNICALL Java_GpuMatchingEngine_shardStatus(JNIEnv* env, jclass cls, jlong handle, jlongArray out) {
+    (void)cls;
+    jkme* h = (jkme*)(intptr_t)handle;
+    if (!h || !h->m || !out || (*env)->GetArrayLength(env, out) < 8) return KME_E_INVALID;
+    kme_multi_status ms;
+    memset(&ms, 0, sizeof ms);
+    const kme_status s = kme_multi_info(h->m, &ms);
+    const jlong o[8] = {(jlong)ms.n_engines, (jlong)ms.consolidated, (jlong)ms.can_consolidate, (jlong)ms.failed,
+                        (jlong)ms.history_records, (jlong)ms.history_cap, (jlong)ms.history_saved, (jlong)ms.generation};
+    (*env)->SetLongArrayRegion(env, out, 0, 8, o);
     return (jint)s;
 }

@@ -16,8 +16,13 @@
 // (the drop-in's default) the first epoch some shard cannot prove is not fatal: the shards are
 // retired and ONE engine of those flags (the consolidated engine, on devices[0]) takes the stream --
 // built by replaying the input history kept since the start into it, then answering the records the
-// shards did not, and every epoch after (consolidate()).
+// shards did not, and every epoch after (consolidate()).  The history survives restarts: every
+// checkpoint appends the records since the last one to `path`.hist (fsync'd before the manifest that
+// names its length and digest is committed), and a restore reads it back (kme_multi_info reports
+// whether consolidation is still possible, and a loss of the history is logged once on stderr).
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -52,15 +57,31 @@ struct Part {
 
 enum : int { kSlotIdle = 0, kSlotQueued, kSlotCollected, kSlotDone };
 
-constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '2'};
+constexpr char kMultiMagic2[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '2'};
+constexpr char kMultiMagic[8] = {'K', 'M', 'E', 'M', 'U', 'L', 'T', '3'};
 // the manifest: this header, n shard records (the digest and size of each shard's file: the
-// manifest's own digest covers them), the application record, the trailer (kme_internal.h)
-struct MultiHeader {
+// manifest's own digest covers them), the application record, the trailer (kme_internal.h).
+// Format 3 adds the input history's length and digest (`path`.hist: HistRec records, appended at
+// each checkpoint; 0 records: no history, consolidation is off); format-2 manifests restore as 0.
+struct MultiHeader2 {
     char magic[8];
     uint32_t n, _pad;
     uint64_t generation;
     uint64_t app_bytes;
 };
+struct MultiHeader {
+    char magic[8];
+    uint32_t n, _pad;
+    uint64_t generation;
+    uint64_t app_bytes;
+    uint64_t hist_records, hist_digest;
+};
+// one record of `path`.hist (the Order fields of one input record, in input order)
+struct HistRec {
+    int64_t oid, aid, sid;
+    int32_t action, price, size, _pad;
+};
+static_assert(sizeof(HistRec) == 40, "history record");
 struct MultiShard {
     uint64_t file_bytes, digest;
 };
@@ -97,6 +118,10 @@ struct kme_multi {
     bool hist_valid = false;               // the history starts at the stream's start and is complete
     uint64_t hist_cap = 0;                 // records it may hold (env KME_MULTI_HISTORY)
     uint64_t hist_start[2] = {};           // per slot: the history position of its epoch's first record
+    std::string hist_file;                 // the file the history was last appended to ("": none yet)
+    uint64_t hist_saved = 0;               // records of the history in hist_file (fsync'd)
+    kme::Digest hist_dg;                   // over those records' bytes
+    bool hist_lost_logged = false;
     kme_epoch_result scratch{};            // host results of one consolidated run
     std::vector<char> scratch_mem;
 };
@@ -384,12 +409,24 @@ static kme_epoch_status merge(kme_multi* m, int slot, uint32_t n, const kme_epoc
 }
 
 // ------------------------------------------------------------------ consolidation
+static void hist_clear(kme_multi* m) {
+    m->hist_valid = false;
+    std::vector<int32_t>().swap(m->h_action); std::vector<int32_t>().swap(m->h_price); std::vector<int32_t>().swap(m->h_size);
+    std::vector<int64_t>().swap(m->h_oid); std::vector<int64_t>().swap(m->h_aid); std::vector<int64_t>().swap(m->h_sid);
+}
+// the history is gone while the shards still run: an unprovable epoch is fatal from here on (once on stderr)
+static void hist_lost(kme_multi* m, const char* why) {
+    hist_clear(m);
+    if (m->can_consolidate && !m->cons && !m->hist_lost_logged) {
+        std::fprintf(stderr, "kme_multi: input history %s: an epoch the shards cannot prove is fatal from here on "
+                             "(KME_E_UNFUNDED)\n", why);
+        m->hist_lost_logged = true;
+    }
+}
 static void hist_append(kme_multi* m, const kme_orders* in, uint32_t n) {
     if (!m->hist_valid) return;
     if (m->h_action.size() + n > m->hist_cap) {   // too long to replay: consolidation is off from here on
-        m->hist_valid = false;
-        std::vector<int32_t>().swap(m->h_action); std::vector<int32_t>().swap(m->h_price); std::vector<int32_t>().swap(m->h_size);
-        std::vector<int64_t>().swap(m->h_oid); std::vector<int64_t>().swap(m->h_aid); std::vector<int64_t>().swap(m->h_sid);
+        hist_lost(m, "past KME_MULTI_HISTORY records");
         return;
     }
     m->h_action.insert(m->h_action.end(), in->action, in->action + n);
@@ -486,9 +523,7 @@ static kme_status consolidate(kme_multi* m, uint64_t upto) {
     kme_epoch_status st{};
     const kme_status rc = cons_run(m, hist_at(m, 0), (uint32_t)upto, nullptr, 0, &st);
     if (rc != KME_OK) return rc;   // (the history took effect once already: it cannot fault now)
-    m->hist_valid = false;         // not needed any more
-    std::vector<int32_t>().swap(m->h_action); std::vector<int32_t>().swap(m->h_price); std::vector<int32_t>().swap(m->h_size);
-    std::vector<int64_t>().swap(m->h_oid); std::vector<int64_t>().swap(m->h_aid); std::vector<int64_t>().swap(m->h_sid);
+    hist_clear(m);                 // not needed any more
     return KME_OK;
 }
 
@@ -699,16 +734,110 @@ kme_status kme_multi_wait(kme_multi* m, kme_epoch_status* st) {
     return (kme_status)tot.status;
 }
 
+kme_status kme_multi_info(kme_multi* m, kme_multi_status* out) {
+    if (!m || !out) return KME_E_INVALID;
+    *out = kme_multi_status{};
+    out->n_engines = m->n;
+    out->consolidated = m->cons ? 1u : 0u;
+    out->can_consolidate = m->can_consolidate && !m->cons && m->hist_valid ? 1u : 0u;
+    out->failed = m->failed ? 1u : 0u;
+    out->history_records = m->hist_valid ? (uint64_t)m->h_action.size() : 0;
+    out->history_cap = m->can_consolidate ? m->hist_cap : 0;
+    out->history_saved = m->hist_valid ? m->hist_saved : 0;
+    out->generation = m->generation;
+    return KME_OK;
+}
+
 kme_status kme_multi_engine(kme_multi* m, uint32_t k, kme_engine** out) {
     if (!m || !out || k >= m->n) return KME_E_INVALID;
     *out = m->cons ? m->cons : m->eng[k];   // (consolidated: the one engine)
     return KME_OK;
 }
 
-// Checkpoint: every engine into path.g<generation>.<k>, then the manifest at `path` (CkptWriter:
-// written to path.tmp, fsync'd, renamed, the directory fsync'd -- the commit of the set), and only then
-// are the previous generation's files removed: a crash at any point leaves a manifest whose shard
-// files all exist.
+// pwrite of all n bytes (a regular file takes them whole unless the disk is full)
+static bool pwrite_all(int fd, const void* p, size_t n, uint64_t off) {
+    const char* c = static_cast<const char*>(p);
+    while (n) {
+        const ssize_t w = pwrite(fd, c, n, (off_t)off);
+        if (w <= 0) return false;
+        c += w; n -= (size_t)w; off += (uint64_t)w;
+    }
+    return true;
+}
+
+// The history's records since the last checkpoint appended to `base`.hist and fsync'd (the whole
+// history when the last append went to another file; a tail a failed checkpoint left past the saved
+// records is cut first).  *records / *digest: what the manifest names (0: no history to keep).
+static kme_status hist_save(kme_multi* m, const std::string& base, uint64_t* records, uint64_t* digest) {
+    *records = 0;
+    *digest = 0;
+    if (!m->can_consolidate || m->cons || !m->hist_valid) return KME_OK;
+    const std::string f = base + ".hist";
+    if (m->hist_file != f) { m->hist_file = f; m->hist_saved = 0; m->hist_dg = kme::Digest(); }
+    const uint64_t n = m->h_action.size();
+    const int fd = open(f.c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fd < 0) return KME_E_INVALID;
+    bool ok = ftruncate(fd, (off_t)(m->hist_saved * sizeof(HistRec))) == 0;
+    std::vector<HistRec> buf((size_t)std::min<uint64_t>(n - m->hist_saved, 1u << 16));
+    kme::Digest dg = m->hist_dg;
+    for (uint64_t a = m->hist_saved; ok && a < n;) {
+        const size_t k = (size_t)std::min<uint64_t>(buf.size(), n - a);
+        for (size_t i = 0; i < k; ++i)
+            buf[i] = HistRec{m->h_oid[a + i], m->h_aid[a + i], m->h_sid[a + i], m->h_action[a + i], m->h_price[a + i], m->h_size[a + i], 0};
+        ok = pwrite_all(fd, buf.data(), k * sizeof(HistRec), a * sizeof(HistRec));
+        dg.update(buf.data(), k * sizeof(HistRec));
+        a += k;
+    }
+    ok = ok && fsync(fd) == 0;
+    ok = close(fd) == 0 && ok;
+    ok = ok && (m->hist_saved > 0 || kme::sync_dir_of(f));   // (a new file: its directory entry too)
+    if (!ok) return KME_E_INVALID;
+    m->hist_saved = n;
+    m->hist_dg = dg;
+    *records = n;
+    *digest = dg.final();
+    return KME_OK;
+}
+
+// The history the manifest names read back from `base`.hist: false when the file is missing, short,
+// or its first `records` records are not the ones the manifest's digest covers.
+static bool hist_load(kme_multi* m, const std::string& base, uint64_t records, uint64_t digest) {
+    if (records > m->hist_cap) return false;
+    const std::string f = base + ".hist";
+    FILE* fp = std::fopen(f.c_str(), "rb");
+    if (!fp) return false;
+    const size_t n = (size_t)records;
+    m->h_action.resize(n); m->h_price.resize(n); m->h_size.resize(n);
+    m->h_oid.resize(n); m->h_aid.resize(n); m->h_sid.resize(n);
+    std::vector<HistRec> buf(std::min<size_t>(n, 1u << 16));
+    kme::Digest dg;
+    bool ok = true;
+    for (size_t a = 0; ok && a < n;) {
+        const size_t k = std::min(buf.size(), n - a);
+        ok = std::fread(buf.data(), sizeof(HistRec), k, fp) == k;
+        dg.update(buf.data(), k * sizeof(HistRec));
+        for (size_t i = 0; ok && i < k; ++i) {
+            const HistRec& r = buf[i];
+            m->h_oid[a + i] = r.oid; m->h_aid[a + i] = r.aid; m->h_sid[a + i] = r.sid;
+            m->h_action[a + i] = r.action; m->h_price[a + i] = r.price; m->h_size[a + i] = r.size;
+        }
+        a += k;
+    }
+    std::fclose(fp);
+    if (!ok || dg.final() != digest) { hist_clear(m); return false; }
+    m->hist_valid = true;
+    m->hist_file = f;
+    m->hist_saved = records;
+    m->hist_dg = dg;
+    m->hist_lost_logged = false;
+    return true;
+}
+
+// Checkpoint: every engine into path.g<generation>.<k>, the input history's new records onto
+// path.hist, then the manifest at `path` (CkptWriter: written to path.tmp, fsync'd, renamed, the
+// directory fsync'd -- the commit of the set), and only then are the previous generation's files
+// removed: a crash at any point leaves a manifest whose shard files all exist and whose history is a
+// prefix of path.hist.
 kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* app, size_t app_bytes) {
     if (!m || !path || (app_bytes && !app)) return KME_E_INVALID;
     if (m->failed) return KME_E_FAILED;
@@ -731,6 +860,7 @@ kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* 
     h._pad = m->cons ? 1u : 0u;            // 1: consolidated (one engine's file)
     h.generation = gen;
     h.app_bytes = app_bytes;
+    if (kme_status s = hist_save(m, base, &h.hist_records, &h.hist_digest)) return s;
     {
         kme::CkptWriter w(path);
         bool ok = w.write(&h, sizeof h) && w.write(shards.data(), shards.size() * sizeof(MultiShard)) && w.write(app, app_bytes) &&
@@ -739,6 +869,10 @@ kme_status kme_multi_checkpoint_app(kme_multi* m, const char* path, const void* 
     }
     for (uint32_t k = 0; k < m->n && m->generation; ++k)   // (the older generation may have had n files)
         std::remove((base + ".g" + std::to_string(m->generation) + "." + std::to_string(k)).c_str());
+    if (h.hist_records == 0) {   // no history kept (consolidated, or lost): no file either
+        std::remove((base + ".hist").c_str());
+        if (m->hist_file == base + ".hist") { m->hist_file.clear(); m->hist_saved = 0; }
+    }
     m->generation = gen;
     return KME_OK;
 }
@@ -750,8 +884,17 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
     if (app_bytes) *app_bytes = 0;
     kme::CkptReader r(path);
     MultiHeader h{};
-    bool ok = r.read(&h, sizeof h) && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 && h.n == m->n &&
-              h.app_bytes < (1ull << 40) && h._pad <= 1 && (h._pad == 0 || m->can_consolidate) && (h._pad == 1 || !m->cons);
+    bool ok = r.read(h.magic, sizeof h.magic);
+    if (ok && std::memcmp(h.magic, kMultiMagic2, sizeof h.magic) == 0) {   // format 2: no history
+        MultiHeader2 h2{};
+        ok = r.read(reinterpret_cast<char*>(&h2) + sizeof h2.magic, sizeof h2 - sizeof h2.magic);
+        h.n = h2.n; h._pad = h2._pad; h.generation = h2.generation; h.app_bytes = h2.app_bytes;
+    } else {
+        ok = ok && std::memcmp(h.magic, kMultiMagic, sizeof h.magic) == 0 &&
+             r.read(reinterpret_cast<char*>(&h) + sizeof h.magic, sizeof h - sizeof h.magic);
+    }
+    ok = ok && h.n == m->n && h.app_bytes < (1ull << 40) && h._pad <= 1 && (h._pad == 0 || m->can_consolidate) &&
+         (h._pad == 1 || !m->cons);
     const uint32_t nf = h._pad ? 1 : m->n;
     std::vector<MultiShard> shards(ok ? nf : 0);
     std::vector<char> rec;
@@ -774,7 +917,7 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
             ci.digest != shards[k].digest)
             return KME_E_INVALID;
     }
-    m->hist_valid = false;   // the history since the stream's start is gone: no consolidation from here
+    hist_clear(m);           // (the history of the checkpoint's stream is read back below)
     if (h._pad) {            // a consolidated stream: the one engine
         if (!m->cons) {
             free_parts(m);
@@ -802,6 +945,11 @@ kme_status kme_multi_restore_app(kme_multi* m, const char* path, void* app, size
         std::vector<int64_t> oids;
         if (kme_status s = kme::resting_oids(m->eng[k], oids)) { m->failed = 1; return s; }
         kme::router_seed(m->router, oids.data(), oids.size(), k);
+    }
+    // the input history up to the checkpoint: consolidation stays possible after the restart
+    if (m->can_consolidate) {
+        if (h.hist_records == 0) hist_lost(m, "not in the checkpoint (lost before it, or a format-2 manifest)");
+        else if (!hist_load(m, base, h.hist_records, h.hist_digest)) hist_lost(m, "unreadable (path.hist missing, short or not the manifest's)");
     }
     m->generation = h.generation;
     if (rec.size()) std::memcpy(app, rec.data(), rec.size());

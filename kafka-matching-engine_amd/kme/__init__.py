@@ -72,6 +72,12 @@ class kme_checkpoint_info(C.Structure):
     _fields_ = [("file_bytes", C.c_uint64), ("app_bytes", C.c_uint64), ("digest", C.c_uint64)]
 
 
+class kme_multi_status(C.Structure):
+    _fields_ = [("n_engines", C.c_uint32), ("consolidated", C.c_uint32), ("can_consolidate", C.c_uint32),
+                ("failed", C.c_uint32), ("history_records", C.c_uint64), ("history_cap", C.c_uint64),
+                ("history_saved", C.c_uint64), ("generation", C.c_uint64)]
+
+
 class kme_ledger_info(C.Structure):
     _fields_ = [("bal_slots", C.c_uint64), ("pos_slots", C.c_uint64), ("bal_used", C.c_uint64),
                 ("pos_used", C.c_uint64), ("grows", C.c_uint32), ("_pad", C.c_uint32)]
@@ -93,7 +99,7 @@ EXPORTS = [
     "kme_rccl_load", "kme_rccl_last_error", "kme_comm_unique_id", "kme_comm_init", "kme_comm_destroy", "kme_market_data_allgather", "kme_credit_state",
     "kme_credit_adjust", "kme_credit_rebalance",
     "kme_multi_create", "kme_multi_destroy", "kme_multi_submit_epoch_host", "kme_multi_poll", "kme_multi_wait",
-    "kme_multi_checkpoint_app", "kme_multi_restore_app", "kme_multi_engine",
+    "kme_multi_checkpoint_app", "kme_multi_restore_app", "kme_multi_engine", "kme_multi_info",
 ]
 
 _lib = None
@@ -187,6 +193,7 @@ def lib():
         "kme_multi_checkpoint_app": (st, [vp, C.c_char_p, vp, C.c_size_t]),
         "kme_multi_restore_app": (st, [vp, C.c_char_p, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
         "kme_multi_engine": (st, [vp, u32, C.POINTER(vp)]),
+        "kme_multi_info": (st, [vp, C.POINTER(kme_multi_status)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -623,6 +630,16 @@ def checkpoint_chunks(path, chunk_bytes: int) -> np.ndarray:
     if rc:
         raise KmeError(rc, "kme_checkpoint_chunks")
     return out[: n.value]
+
+
+def multi_info(m) -> dict:
+    """kme_multi_info of a kme_multi handle (an address): whether an unprovable epoch is survivable now,
+    the input history's size, cap and durable part, the checkpoint generation."""
+    out = kme_multi_status()
+    rc = lib().kme_multi_info(C.c_void_p(m), C.byref(out))
+    if rc:
+        raise KmeError(rc, "kme_multi_info")
+    return {f: getattr(out, f) for f, _ in kme_multi_status._fields_}
 
 
 def order_from_json(value: str):

@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "integration", "jni", "kme_jni.c")
 CHECK_LIB = os.path.join(ROOT, "integration", "jni", "libkme_jni_check.so")
 SYMBOLS = ["create", "destroy", "buffer", "submit", "poll", "complete", "forwarded", "statusText", "checkpoint",
-           "restore", "stateChunks", "inspect"]
+           "restore", "stateChunks", "inspect", "shardStatus"]
 ROW_DTYPE = np.dtype([("oid", "<i8"), ("aid", "<i8"), ("sid", "<i8"), ("prev", "<i8"), ("action", "<i4"),
                       ("price", "<i4"), ("size", "<i4"), ("kind", "u1"), ("has_prev", "u1"), ("_pad", "u1", 2)])
 assert ROW_DTYPE.itemsize == 48
@@ -124,6 +124,8 @@ def _lib():
     lib.Java_GpuMatchingEngine_stateChunks.restype = I
     lib.Java_GpuMatchingEngine_inspect.argtypes = [P, P, P, P]
     lib.Java_GpuMatchingEngine_inspect.restype = I
+    lib.Java_GpuMatchingEngine_shardStatus.argtypes = [P, P, C.c_int64, P]
+    lib.Java_GpuMatchingEngine_shardStatus.restype = I
     return lib
 
 
@@ -343,6 +345,15 @@ class JavaProcessor:
         t = self.j.arr(np.zeros(3, np.int64))
         rc = self.lib.Java_GpuMatchingEngine_inspect(self.j.env, None, _jstr(self.j, str(path)), t)
         return rc == 0 and int(self.j.objs[t][0]) == want[2] and int(self.j.objs[t][2]) == want[3]
+
+    def shard_status(self):
+        """GpuMatchingEngine.shardStatus(): None for one engine, else the kme_multi_info fields."""
+        t = self.j.arr(np.zeros(8, np.int64))
+        if self.lib.Java_GpuMatchingEngine_shardStatus(self.j.env, None, self.h, t) != 0:
+            return None
+        keys = ("n_engines", "consolidated", "can_consolidate", "failed", "history_records", "history_cap",
+                "history_saved", "generation")
+        return dict(zip(keys, (int(x) for x in self.j.objs[t])))
 
     def _rebuild_from_log(self, want):
         if want[4] != self.CHUNK_BYTES:
@@ -879,6 +890,68 @@ def test_multi_gpu_drop_in_consolidates_an_unprovable_stream(oracle_mod, tmp_pat
         _drive(q, orders, c1 + 1, n)
         q.close()
         got = np.concatenate([first[:F], q.rows_out()])
+    o = oracle_mod.Oracle()
+    o.process(orders)
+    _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hist", ["kept", "lost"])
+def test_multi_gpu_drop_in_consolidates_after_a_restart(oracle_mod, tmp_path, monkeypatch, hist):
+    """Round-5 verdict (Next 8): a nDevices = -4 processor with the drop-in's default flags commits,
+    crashes, restores from its sharded checkpoint, and only then meets an epoch no shard can prove
+    (BUY/SELL priced 101..125, outside the funded domain: KP:167-182, 200-223).  The input history
+    since the start went to `path`.hist with every commit point (its length and digest in the
+    manifest), so the restored processor still consolidates onto one exact engine and its MatchOut rows
+    equal the oracle's.  shardStatus() says so before and after.  With the history file gone at the
+    restart (`lost`) the restore still succeeds, shardStatus() says consolidation is off, and the
+    unprovable epoch fails loudly (KME_E_UNFUNDED) instead of answering wrongly."""
+    lib = _lib()
+    j = FakeJni()
+    n_sym, n_acc, epoch, max_trades = 16, 64, 1 << 11, 1 << 13
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    funded = W.uniform(12_000, n_symbols=n_sym, n_accounts=n_acc, seed=23)
+    late = W.uniform(4_000, n_symbols=n_sym, n_accounts=n_acc, seed=24, oid_base=1 << 20)
+    rng = np.random.default_rng(5)
+    odd = rng.choice(np.flatnonzero((late.action == W.BUY) | (late.action == W.SELL)), 40, replace=False)
+    late.price[odd] = rng.integers(101, 126, len(odd)).astype(late.price.dtype)
+    orders = W.Orders.concat([setup, funded, late])
+    args = (1, n_sym + 1, epoch, 1 << 15, max_trades, n_acc, 3, 0, -4, 1 << 12)
+    ckpt = tmp_path / "m.ckpt"
+    p = JavaProcessor(lib, j, ckpt, epoch, max_trades, args)
+    c1 = len(setup) + len(funded) // 2
+    _drive(p, orders, 0, c1 + 1)
+    p.commit_point()
+    st = p.shard_status()
+    assert st["n_engines"] == 4 and st["consolidated"] == 0 and st["can_consolidate"] == 1
+    assert st["history_saved"] == st["history_records"] == c1 + 1
+    assert os.path.exists(str(ckpt) + ".hist")
+    F = sum(len(x) for x in p.out)
+    crash_at = len(setup) + len(funded) - 7
+    _drive(p, orders, c1 + 1, crash_at)
+    first = p.rows_out()[:F]
+    p.crash()
+    if hist == "lost":
+        os.remove(str(ckpt) + ".hist")
+    q = JavaProcessor(lib, j, ckpt, epoch, max_trades, args, p.commit_log)
+    assert q.skip_through == c1
+    st = q.shard_status()
+    assert st["consolidated"] == 0 and st["can_consolidate"] == (1 if hist == "kept" else 0)
+    if hist == "lost":
+        with pytest.raises(AssertionError):           # the unprovable epoch's status: UNFUNDED
+            _drive(q, orders, c1 + 1, len(orders))
+            q.close()
+        q.crash()
+        return
+    _drive(q, orders, c1 + 1, len(orders))
+    q.forward_ready()
+    q.flush()
+    while q.inflight:
+        q.complete_oldest(True)
+    st = q.shard_status()
+    assert st["consolidated"] == 1 and st["can_consolidate"] == 0
+    q.close()
+    got = np.concatenate([first, q.rows_out()])
     o = oracle_mod.Oracle()
     o.process(orders)
     _cmp_fields(_as_tape(got, oracle_mod.REC_DTYPE), o.tape())
