@@ -27,13 +27,18 @@ void router_seed(kme_router* r, const int64_t* oids, size_t n, uint32_t partitio
 // ------------------------------------------------------------------ checkpoint files
 // Every checkpoint file (an engine's, a kme_multi manifest) ends with a trailer: the application
 // record's size and a 64-bit digest of every byte before the trailer, computed while writing
-// (kme_checkpoint_inspect reads it without the rest; a restore recomputes it over what it reads).
+// (kme_checkpoint_inspect reads it without the rest; a restore recomputes it over what it read).
+// Trailer "KMEDGST2" (round 6): a tree digest -- every kDigestBlock bytes of the file hashed on their
+// own, then the block digests and the length -- so that writer and reader hash blocks on many host
+// threads; "KMEDGST1" files (one Digest over the whole stream) are still read.
 struct CkptTrailer {
     uint64_t app_bytes;
     uint64_t digest;
     char magic[8];
 };
 constexpr char kTrailerMagic[8] = {'K', 'M', 'E', 'D', 'G', 'S', 'T', '1'};
+constexpr char kTrailerMagic2[8] = {'K', 'M', 'E', 'D', 'G', 'S', 'T', '2'};
+constexpr uint64_t kDigestBlock = 1ull << 20;
 
 // Four independent multiply-rotate lanes over 8-byte words (a dependency chain per lane, so the
 // host hashes at several GB/s); the tail bytes of a stream are zero-padded into a last word.
@@ -73,23 +78,48 @@ struct Digest {
     }
 };
 
-// Writes `path`.tmp through a digest, then (commit) the trailer, fsync of the file, rename over
-// `path` and fsync of the directory: after commit() returns true the new file is the durable one.
+// the tree digest's root: the block digests in file order, then the length
+uint64_t tree_digest(const uint64_t* blocks, size_t n_blocks, uint64_t bytes);
+
+// Pinned host slots for a writer's device reads (an engine keeps one, made at its first checkpoint):
+// kRingSlots slots of kRingSlot bytes, each with an event marking its copies done.
+constexpr int kRingSlots = 8;
+constexpr size_t kRingSlot = 8ull << 20;   // (a multiple of kDigestBlock)
+struct PinnedRing {
+    char* slot[kRingSlots] = {};
+    hipEvent_t ev[kRingSlots] = {};
+    int device = 0;
+    bool ready = false;
+    bool init(int dev);      // allocates on first use
+    void release();
+};
+
+// Writes `path`.tmp, then (commit) the trailer, fsync of the file, rename over `path` and fsync of
+// the directory: after commit() returns true the new file is the durable one.  The file is assembled
+// in slots of kRingSlot bytes, each one file range: host bytes are copied in (write), device bytes
+// land by stream-ordered copies (write_dev, a PinnedRing's slots); a full slot goes to a pool of host
+// threads that wait for its copies, hash its digest blocks and pwrite it at its offset, while the
+// next slot fills.  Without a ring the slots are heap memory and each is written as it fills.
 struct CkptWriter {
-    std::string path, tmp;
-    FILE* f = nullptr;
-    Digest dg;
+    struct Impl;
+    Impl* im = nullptr;
     bool ok = false;
-    explicit CkptWriter(const char* p);
+    explicit CkptWriter(const char* p, PinnedRing* ring = nullptr, hipStream_t stream = nullptr);
     ~CkptWriter();
     bool write(const void* data, size_t len);
+    bool write_dev(const void* dev, size_t len);   // (a writer made with a ring)
     bool commit(uint64_t app_bytes, uint64_t* digest_out);
+    const char* error() const;                      // what failed, when something did
 };
-// Reads a checkpoint file through a digest; verify() checks the trailer against it at the end.
+// Reads a checkpoint file; verify() checks the trailer's digest (KMEDGST2: every block hashed again on
+// host threads from the file; KMEDGST1: the stream hashed as it was read).
 struct CkptReader {
     FILE* f = nullptr;
     Digest dg;
+    std::string path;
     uint64_t size = 0;         // the file's size (trailer included)
+    uint64_t pos = 0;          // bytes read
+    bool tree = false;         // the trailer is KMEDGST2
     bool ok = false;
     explicit CkptReader(const char* p);
     ~CkptReader();

@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -83,6 +84,7 @@ struct kme_engine {
     unsigned long long* d_ser_total = nullptr;
     unsigned long long* h_ser_total = nullptr;
     char* h_stage = nullptr;              // pinned bounce buffer of the snapshots' device reads (kStage bytes)
+    kme::PinnedRing ring;                 // the checkpoint writer's pinned slots (made at the first checkpoint)
     std::vector<void*> allocs;
     int64_t seq_base = 0;
     // epochs in flight: submitted to the stream, not yet waited for (at most two; slot = submission
@@ -538,6 +540,7 @@ kme_status kme_destroy(kme_engine* e) {
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->h_ser_total) (void)hipHostFree(e->h_ser_total);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    e->ring.release();
     for (auto& evs : e->ev)
         for (auto& ev : evs) if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : e->ev_end) if (ev) (void)hipEventDestroy(ev);
@@ -1287,74 +1290,10 @@ struct CkptHeader4 {
     uint64_t _reserved[3];
 };
 
-// n bytes of device memory at `dev` into the writer, through a host staging buffer; *file_fail is set
-// when the write failed (else a false return is the device's)
-bool put_dev(kme_engine* e, kme::CkptWriter& w, const void* dev, size_t n, const char* what, bool* file_fail) {
-    return staged_read(e, dev, n, what, [&](const char* chunk, size_t c, size_t) {
-        const bool ok = w.write(chunk, c);
-        if (!ok) *file_fail = true;
-        return ok;
-    });
-}
 }  // namespace
 }  // extern "C"
 
 namespace kme {
-CkptWriter::CkptWriter(const char* p) : path(p), tmp(std::string(p) + ".tmp") {
-    f = std::fopen(tmp.c_str(), "wb");
-    ok = f != nullptr;
-}
-CkptWriter::~CkptWriter() {
-    if (f) { std::fclose(f); std::remove(tmp.c_str()); }
-}
-bool CkptWriter::write(const void* data, size_t len) {
-    if (!ok) return false;
-    dg.update(data, len);
-    ok = len == 0 || std::fwrite(data, 1, len, f) == len;
-    return ok;
-}
-bool CkptWriter::commit(uint64_t app_bytes, uint64_t* digest_out) {
-    if (!ok) return false;
-    CkptTrailer t{};
-    t.app_bytes = app_bytes;
-    t.digest = dg.final();
-    std::memcpy(t.magic, kTrailerMagic, sizeof t.magic);
-    ok = std::fwrite(&t, sizeof t, 1, f) == 1;
-    ok = std::fflush(f) == 0 && ok;
-    ok = fsync(fileno(f)) == 0 && ok;
-    ok = std::fclose(f) == 0 && ok;
-    f = nullptr;
-    ok = ok && std::rename(tmp.c_str(), path.c_str()) == 0;
-    if (!ok) { std::remove(tmp.c_str()); return false; }
-    ok = sync_dir_of(path);
-    if (digest_out) *digest_out = t.digest;
-    return ok;
-}
-CkptReader::CkptReader(const char* p) {
-    f = std::fopen(p, "rb");
-    if (!f) return;
-    ok = std::fseek(f, 0, SEEK_END) == 0;
-    const long sz = ok ? std::ftell(f) : -1;
-    ok = ok && sz >= (long)sizeof(CkptTrailer) && std::fseek(f, 0, SEEK_SET) == 0;
-    size = sz > 0 ? (uint64_t)sz : 0;
-}
-CkptReader::~CkptReader() {
-    if (f) std::fclose(f);
-}
-bool CkptReader::read(void* data, size_t len) {
-    if (!ok) return false;
-    if (dg.n + len + sizeof(CkptTrailer) > size) { ok = false; return false; }   // (never into the trailer)
-    ok = len == 0 || std::fread(data, 1, len, f) == len;
-    if (ok) dg.update(data, len);
-    return ok;
-}
-bool CkptReader::at_trailer() const { return ok && dg.n + sizeof(CkptTrailer) == size; }
-bool CkptReader::verify(CkptTrailer* t) {
-    if (!at_trailer()) return false;
-    ok = std::fread(t, sizeof *t, 1, f) == 1 && std::memcmp(t->magic, kTrailerMagic, sizeof t->magic) == 0 &&
-         t->digest == dg.final();
-    return ok;
-}
 bool sync_dir_of(const std::string& path) {
     const size_t slash = path.find_last_of('/');
     const std::string dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : path.substr(0, slash));
@@ -1400,6 +1339,13 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
     if (ctr[ci(C_ERR)] != ~0ull && (ctr[ci(C_ERR)] & 0xFF) != KME_E_UNFUNDED) return KME_E_FAILED;
     const size_t G = e->cfg.max_symbols, Gs = (size_t)S.Gs, A = e->cfg.max_accounts;
     const bool funded = e->cfg.mode == KME_MODE_FUNDED;
+    // (diagnostics: env KME_CKPT_TRACE=1 prints the phases' wall-clock ms on stderr)
+    static const bool trace = std::getenv("KME_CKPT_TRACE") && std::atoi(std::getenv("KME_CKPT_TRACE"));
+    const auto t_start = std::chrono::steady_clock::now();
+    double t_compact = 0, t_stores = 0;
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     CkptHeader4 h{};
     std::memcpy(h.magic, kCkptMagic4, sizeof h.magic);
     h.cfg = e->cfg;
@@ -1442,17 +1388,25 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
         if (!ok) why = KME_E_HIP;
     }
     (void)hipGetLastError();
+    t_compact = ms_since(t_start);
     h.n_levels = cnt[0];
     h.bal_live = cnt[1];
     h.pos_live = cnt[2];
     if (ok) {
-        kme::CkptWriter w(path);
-        bool file_fail = false;
+        // the file in slots: device stores by stream-ordered copies into the engine's pinned ring,
+        // hashed and written by host threads while the next slot fills (kme_ckpt.cpp)
+        if (!e->ring.init(e->device)) { ok = false; why = KME_E_CAPACITY; }
+        kme::CkptWriter w(path, &e->ring, e->stream);
+        auto fail_of = [&]() { return std::strcmp(w.error(), "device read") == 0 ? KME_E_HIP : KME_E_INVALID; };
         auto put = [&](const void* dev, size_t n, const char* what) {
-            if (ok && !put_dev(e, w, dev, n, what, &file_fail)) { ok = false; why = file_fail ? KME_E_INVALID : KME_E_HIP; }
+            if (ok && !w.write_dev(dev, n)) {
+                ok = false;
+                why = fail_of();
+                std::fprintf(stderr, "kme_checkpoint: %s of %s (%zu bytes) failed\n", w.error(), what, n);
+            }
         };
         auto write = [&](const void* p, size_t n) {
-            if (ok && !w.write(p, n)) { ok = false; why = KME_E_INVALID; }
+            if (ok && !w.write(p, n)) { ok = false; why = fail_of(); }
         };
         write(&h, sizeof h);
         // the stores of fixed size or growing only at their end first (group states, FUNDED accounts,
@@ -1473,8 +1427,13 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
         }
         if (Gs) put(S.gsid, Gs * sizeof(int64_t), "sparse symbols");
         write(app, app_bytes);
-        if (ok && !w.commit(app_bytes, nullptr)) { ok = false; why = KME_E_INVALID; }
+        t_stores = ms_since(t_start);
+        if (ok && !w.commit(app_bytes, nullptr)) { ok = false; why = fail_of(); }
     }
+    if (trace)
+        std::fprintf(stderr, "kme_checkpoint: compaction %.2f ms, stores (D2H, digest, write) %.2f ms, commit (fsync, rename) %.2f ms, "
+                             "%llu bytes\n", t_compact, t_stores - t_compact, ms_since(t_start) - t_stores,
+                     (unsigned long long)(sizeof h + (G + Gs) * sizeof(GroupState) + h.pool_used * sizeof(Node)));
     (void)hipFree(d_lev);
     if (d_bal) (void)hipFree(d_bal);
     if (d_pos) (void)hipFree(d_pos);

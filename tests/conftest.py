@@ -33,7 +33,7 @@ def oracle_mod():
 # the sources kme_build_id() hashes (kafka-matching-engine_amd/csrc/Makefile SRCS, same order)
 LIB_SOURCES = ["kme_kernels.hip", "kme_serialize.hip", "kme_runtime.cpp", "kme_host.cpp", "kme_processor.cpp",
                "kme_router.cpp", "kme_device.h", "kme_launch.h", "kme_processor.hpp", "../../include/kme.h",
-               "../../include/kme_processor.h", "kme_multi.cpp", "kme_internal.h", "kme_ledger.hip", "kme_jarith.h", "kme_maint.hip"]
+               "../../include/kme_processor.h", "kme_multi.cpp", "kme_internal.h", "kme_ledger.hip", "kme_jarith.h", "kme_maint.hip", "kme_ckpt.cpp"]
 
 
 def source_hash() -> str:
