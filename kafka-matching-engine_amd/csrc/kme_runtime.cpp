@@ -1316,7 +1316,7 @@ kme_status kme_checkpoint_inspect(const char* path, kme_checkpoint_info* out) {
     bool ok = std::fseek(f, 0, SEEK_END) == 0;
     const long sz = ok ? std::ftell(f) : -1;
     ok = ok && sz >= (long)sizeof t && std::fseek(f, sz - (long)sizeof t, SEEK_SET) == 0 && std::fread(&t, sizeof t, 1, f) == 1 &&
-         std::memcmp(t.magic, kme::kTrailerMagic, sizeof t.magic) == 0;
+         (std::memcmp(t.magic, kme::kTrailerMagic, sizeof t.magic) == 0 || std::memcmp(t.magic, kme::kTrailerMagic2, sizeof t.magic) == 0);
     std::fclose(f);
     if (!ok) return KME_E_INVALID;
     out->file_bytes = (uint64_t)sz;
