@@ -288,11 +288,12 @@ def measure_host_path(eng, stream, first, n_epochs, E, max_trades):
                     "two epochs in flight; PCIe- and host-inclusive, not the headline value"}
 
 
-def measure_checkpoint(kme, eng, cfg, directory):
+def measure_checkpoint(kme, eng, cfg, directory, next_epoch=None):
     """The commit point's cost at this shape: kme_checkpoint_app of the engine's
-    state (format 4: the live stores, a digest trailer; fsync'd and renamed), the state changelog's chunk
-    hashes, and its restore into a
-    fresh engine of the same configuration; both books must then agree."""
+    state (format 4: the live stores, a tree digest trailer; fsync'd and renamed), the state changelog's
+    chunk hashes, and its restore into a fresh engine of the same configuration; both books must then
+    agree.  With next_epoch: one more epoch, a second commit, and how many of its 512-KiB chunks
+    changed -- what the state changelog carries for a commit one epoch after the last."""
     os.makedirs(directory, exist_ok=True)
     path = os.path.join(directory, "bench.ckpt")
     t0 = time.perf_counter()
@@ -304,6 +305,19 @@ def measure_checkpoint(kme, eng, cfg, directory):
     tc0 = time.perf_counter()
     chunks = kme.checkpoint_chunks(path, 512 << 10)
     tc1 = time.perf_counter()
+    delta = None
+    if next_epoch is not None:
+        before = set(enumerate(chunks.tolist()))
+        next_epoch()
+        path2 = os.path.join(directory, "bench2.ckpt")
+        t4 = time.perf_counter()
+        eng.checkpoint_app(path2, b"offset")
+        t5 = time.perf_counter()
+        chunks2 = kme.checkpoint_chunks(path2, 512 << 10)
+        changed = sum(1 for kc in enumerate(chunks2.tolist()) if kc not in before)
+        delta = {"write_ms": (t5 - t4) * 1e3, "chunks": len(chunks2), "chunks_changed": changed,
+                 "changed_bytes": changed * (512 << 10)}
+        os.remove(path2)
     other = kme.Engine(cfg)
     t2 = time.perf_counter()
     assert other.restore_app(path) == b"offset"
@@ -314,7 +328,7 @@ def measure_checkpoint(kme, eng, cfg, directory):
     other.close()
     os.remove(path)
     return {"file_bytes": info["file_bytes"], "write_ms": (t1 - t0) * 1e3, "restore_ms": (t3 - t2) * 1e3,
-            "chunks": len(chunks), "chunk_hash_ms": (tc1 - tc0) * 1e3,
+            "chunks": len(chunks), "chunk_hash_ms": (tc1 - tc0) * 1e3, "after_one_more_epoch": delta,
             "restored_state_equal": same,
             "path": "kme_checkpoint_app (device compaction, D2H, digest, fsync, rename) / kme_restore_app into a new engine"}
 
@@ -402,7 +416,8 @@ def main():
         args.host_path_epochs = max(3, (1 << 24) // E)
     host_epochs = args.host_path_epochs if world == 1 else 0
     # + 1: the phase-breakdown epoch; then the host-path epochs
-    total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs) * E)
+    # (+ 1 with --checkpoint: the epoch between its two commits)
+    total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs + (1 if args.checkpoint else 0)) * E)
     # --shard R/N (one GPU): the records rank R of an N-GPU run would match, e.g. C4's hot shard
     w_rank, w_world = (rank, world) if not args.shard else tuple(int(x) for x in args.shard.split("/"))
     if args.shard and world > 1:
@@ -573,7 +588,9 @@ def main():
     host_path = measure_host_path(eng, stream, args.warmup + args.steps + 1, host_epochs, E, cfg.max_trades) \
         if host_epochs else None
     router = measure_router(stream, E) if world == 1 and host_epochs else None   # (host CPU only)
-    ckpt = measure_checkpoint(kme, eng, cfg, args.checkpoint) if args.checkpoint and world == 1 else None
+    ckpt = measure_checkpoint(kme, eng, cfg, args.checkpoint,
+                              lambda: eng.submit_device(epoch_ptrs(args.warmup + args.steps + 1 + host_epochs), E) or eng.wait()) \
+        if args.checkpoint and world == 1 else None
     ledger_tables = eng.ledger_stats() if flags & 1 else None
 
     if args.lane_stamps:  # -DKME_LANE_STAMPS build: k_match_lanes wavefront steps (kme_kernels.hip LST)

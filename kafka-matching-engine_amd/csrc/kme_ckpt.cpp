@@ -124,6 +124,9 @@ struct CkptWriter::Impl {
         const char* p = slot_ptr(j.slot);
         block_digests(p, j.len, j.dg);
         if (!pwrite_full(fd, p, j.len, j.off)) { set_err("file write"); return false; }
+        // start the slot's write-back now, so that commit()'s fsync finds most of the file on disk
+        // (the disk works while later slots are copied and hashed)
+        (void)::sync_file_range(fd, (off64_t)j.off, (off64_t)j.len, SYNC_FILE_RANGE_WRITE);
         return true;
     }
     void worker() {
@@ -158,7 +161,7 @@ struct CkptWriter::Impl {
             if (!fail) (void)run(jobs.back());
         } else {
             if (th.empty()) {
-                const unsigned T = host_threads(8);
+                const unsigned T = host_threads(12);
                 for (unsigned t = 0; t < T; ++t) th.emplace_back([this] { worker(); });
             }
             std::lock_guard<std::mutex> g(mu);
