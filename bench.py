@@ -305,6 +305,15 @@ def measure_checkpoint(kme, eng, cfg, directory, next_epoch=None):
     tc0 = time.perf_counter()
     chunks = kme.checkpoint_chunks(path, 512 << 10)
     tc1 = time.perf_counter()
+    other = kme.Engine(cfg)
+    t2 = time.perf_counter()
+    assert other.restore_app(path) == b"offset"
+    t3 = time.perf_counter()
+    same = other.snapshot_books() == eng.snapshot_books()
+    if cfg.flags & 1:
+        same = same and other.snapshot_ledger() == eng.snapshot_ledger()
+    other.close()
+    os.remove(path)
     delta = None
     if next_epoch is not None:
         before = set(enumerate(chunks.tolist()))
@@ -318,15 +327,6 @@ def measure_checkpoint(kme, eng, cfg, directory, next_epoch=None):
         delta = {"write_ms": (t5 - t4) * 1e3, "chunks": len(chunks2), "chunks_changed": changed,
                  "changed_bytes": changed * (512 << 10)}
         os.remove(path2)
-    other = kme.Engine(cfg)
-    t2 = time.perf_counter()
-    assert other.restore_app(path) == b"offset"
-    t3 = time.perf_counter()
-    same = other.snapshot_books() == eng.snapshot_books()
-    if cfg.flags & 1:
-        same = same and other.snapshot_ledger() == eng.snapshot_ledger()
-    other.close()
-    os.remove(path)
     return {"file_bytes": info["file_bytes"], "write_ms": (t1 - t0) * 1e3, "restore_ms": (t3 - t2) * 1e3,
             "chunks": len(chunks), "chunk_hash_ms": (tc1 - tc0) * 1e3, "after_one_more_epoch": delta,
             "restored_state_equal": same,

@@ -325,10 +325,13 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 // (the ops themselves were gathered into sorted order by the sort's last pass: lsrt)
 // lseg[a] = the number of sorted ops of accounts below a, for a in [0, A]: thread k (an op, or k = n)
 // writes k for the accounts after op k - 1's up to op k's.  A gap longer than LSEG_RUN accounts goes
-// to a list that k_lseg_gaps fills a workgroup per gap: one thread walking it was the serial tail when
-// the ops name a few of many accounts (the last op's thread walked to A: 13 ms per epoch at A = 2^20
-// with 65,536 accounts in use).
+// to a list that k_lseg_gaps fills a workgroup per entry, in pieces of at most LSEG_PIECE accounts:
+// one thread walking a gap was the serial tail when the ops name a few of many accounts (the last
+// op's thread walked to A: 13 ms per epoch at A = 2^20 with 65,536 accounts in use), and so was one
+// workgroup per gap (the gap past the last account in use, ~2^20 accounts: 0.11 ms of the drop-in's
+// 0.45-ms epoch, round 6).
 constexpr uint32_t LSEG_RUN = 256;
+constexpr uint32_t LSEG_PIECE = 4096;
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -339,8 +342,15 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     if (cur - prev <= (int64_t)LSEG_RUN) {
         for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
     } else {
-        const unsigned long long x = atomicAdd(lc(S, LC_GAPS), 1ull);   // < (A + 1) / LSEG_RUN + 1 entries
-        S.lgap[x] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
+        // entries: < (A + 1) / LSEG_RUN gaps, plus (A + 1) / LSEG_PIECE pieces past their first
+        const uint32_t lo = (uint32_t)(prev + 1), len = (uint32_t)(cur - prev);
+        const uint32_t np = (len + LSEG_PIECE - 1) / LSEG_PIECE;
+        const unsigned long long x = atomicAdd(lc(S, LC_GAPS), (unsigned long long)np);
+        for (uint32_t q = 0; q < np; ++q) {
+            const uint32_t a0 = lo + q * LSEG_PIECE;
+            const uint32_t a1 = q + 1 == np ? (uint32_t)cur : a0 + LSEG_PIECE - 1;
+            S.lgap[x + q] = make_uint4(a0, a1, k, 0);
+        }
     }
 }
 __global__ void __launch_bounds__(256) k_lseg_gaps(DevState S) {

@@ -434,7 +434,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lchain, nops); ALLOC(S.lhead, nops);
             ALLOC(S.lvw, nops); ALLOC(S.lvw_meta, nops); ALLOC(S.lvw_tgt, nops);
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
-            ALLOC(S.lgap, (size_t)cfg->max_accounts / 256 + 4);
+            ALLOC(S.lgap, (size_t)cfg->max_accounts / 256 + (size_t)cfg->max_accounts / 4096 + 8);   // (k_lseg's gaps)
             ALLOC(S.ldelta, cfg->max_accounts);
             ALLOC(S.lvk, vk);
             HIP_TRY(hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * vk, e->stream));   // (tags from 1 on)
