@@ -209,6 +209,8 @@ struct DevState {
     KG uint32_t* rkeys[2];
     KG uint32_t* rvals[2];
     KG uint32_t* ghist;
+    KG uint32_t* rtcnt;               // small partition sorts: per-tile digit counts of every pass (RadixIO::tcnt)
+    KG unsigned long long* rlb;       // and their look-back words (RadixIO::lb)
     KG uint32_t* seg;
     KG uint32_t* gflag;               // per group: 1 = k_match takes it this epoch (then its scanned offset)
     KG uint32_t* glist;               // those groups, in id order (k_match's dense grid); gcount[0] = how many.
@@ -229,6 +231,8 @@ struct DevState {
     KG uint32_t* lkey[2];
     KG uint32_t* lval[2];
     KG uint32_t* lghist;
+    KG uint32_t* ltcnt;               // the op sort's look-back buffers (small epochs; nullptr: none)
+    KG unsigned long long* llb;
     KG LOp* lrec;                     // per op, arrival order
     KG LOp* lsrt;                     // per op, sorted order (k_lseg gathers them once)
     KG LChain* lchain;                // per sorted op (written at chain heads only)

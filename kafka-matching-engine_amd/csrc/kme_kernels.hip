@@ -22,6 +22,8 @@
 // (values land in SGPRs); atomics are issued by lane 0 only and broadcast.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 
 #include "kme.h"
@@ -756,7 +758,30 @@ __global__ void __launch_bounds__(256) k_radix_hist(RadixIO R, int pass, int src
     for (int q = 0; q < RADIX_PER_T; ++q) R.ghist[(t + 256 * q) * gridDim.x + blockIdx.x] = h[t + 256 * q];
 }
 
-KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
+// Small sorts: every pass's digit counts of this tile of the unpermuted keys (R.tcnt, pass-major,
+// then tile, then digit) -- what radix_lb_offsets sums into the digit totals.
+template <int TILE>
+__global__ void __launch_bounds__(256) k_radix_tcnt(RadixIO R) {
+    __shared__ uint32_t h[RADIX_MAXP][RADIX_DIGITS];
+    const int t = threadIdx.x;
+    const uint32_t base = blockIdx.x * TILE, n = radix_n(R);
+    if (base >= n) return;
+    for (int p = 0; p < RADIX_MAXP; ++p)
+        for (int q = 0; q < RADIX_PER_T; ++q) h[p][t + 256 * q] = 0;
+    constexpr int RJ = TILE / 256;
+    uint32_t keys[RJ], unused[RJ];
+    radix_load<RJ, false>(R, 0, 0, n, base + t, 256, keys, unused);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        if (base + j * 256 + t >= n) continue;
+        for (int p = 0; p < R.passes; ++p) atomicAdd(&h[p][(keys[j] >> (RADIX_BITS * p)) & (RADIX_DIGITS - 1)], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < R.passes; ++p)
+        for (int q = 0; q < RADIX_PER_T; ++q)
+            R.tcnt[((size_t)p * gridDim.x + blockIdx.x) * RADIX_DIGITS + t + 256 * q] = h[p][t + 256 * q];
+}
 
 // One tile's scatter, staged in LDS: the tile is first ordered by digit in LDS (stable), then
 // written out in that order, so that each digit's run of the tile leaves in consecutive lanes
@@ -765,8 +790,71 @@ KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
 // round, lane) and counts its digits in its own LDS row round by round (match-any over the digit
 // bits; the first lane of each digit adds the run), so the only block barriers are the few
 // between the counting, the per-digit offsets and the placement.
-template <int TILE>
-__global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int src) {
+// Small sorts (launch_radix, R.tcnt): each pass's global digit offsets without the histogram and
+// scan launches -- the digit totals from the unpermuted keys' per-tile counts (k_radix_tcnt: a
+// permutation does not change them), and the tiles before this one by look-back: each tile publishes
+// its digit counts as (count | stamp << 32) words as soon as it has ranked its keys, and reads those of
+// every earlier tile (all resident: a small sort is a few dozen tiles, and an earlier tile never
+// waits for a later one).  t0 / t1: this tile's counts of digits 2t, 2t + 1; returns their offsets.
+KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
+constexpr int LB_BATCH = 16;
+KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t ntiles, uint32_t t0, uint32_t t1,
+                           uint32_t* wsum, uint32_t& g0, uint32_t& g1) {
+    const int t = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    KG unsigned long long* lb = R.lb;
+    const unsigned long long st = (unsigned long long)stamp << 32;
+    __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t], st | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t + 1], st | t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the digits' totals over the sort's tiles, exclusive over the digits
+    const KG uint32_t* tc = R.tcnt + (size_t)pass * gridDim.x * RADIX_DIGITS;
+    uint32_t T0 = 0, T1 = 0;
+    for (uint32_t q0 = 0; q0 < ntiles; q0 += LB_BATCH) {
+        uint2 v[LB_BATCH];
+#pragma unroll
+        for (int b = 0; b < LB_BATCH; ++b) {
+            const uint32_t q = q0 + b < ntiles ? q0 + b : 0;
+            v[b] = *reinterpret_cast<const KG uint2*>(&tc[(size_t)q * RADIX_DIGITS + 2 * t]);
+        }
+#pragma unroll
+        for (int b = 0; b < LB_BATCH; ++b)
+            if (q0 + b < ntiles) { T0 += v[b].x; T1 += v[b].y; }
+    }
+    uint32_t tot;
+    const uint32_t gx = block_excl_scan_256(T0 + T1, wsum, tot);
+    // the earlier tiles' counts (their words carry this launch's stamp once written)
+    uint32_t P0 = 0, P1 = 0;
+    for (uint32_t q0 = 0; q0 < tile; q0 += LB_BATCH) {
+        unsigned long long w[2 * LB_BATCH];
+        uint32_t spins = 0;
+        for (;;) {
+            bool all = true;
+#pragma unroll
+            for (int b = 0; b < LB_BATCH; ++b) {
+                const uint32_t q = q0 + b < tile ? q0 + b : 0;
+                w[2 * b] = __hip_atomic_load(&lb[(size_t)q * RADIX_DIGITS + 2 * t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w[2 * b + 1] = __hip_atomic_load(&lb[(size_t)q * RADIX_DIGITS + 2 * t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int b = 0; b < LB_BATCH; ++b)
+                all = all && (q0 + b >= tile || ((w[2 * b] >> 32) == stamp && (w[2 * b + 1] >> 32) == stamp));
+            if (all) break;
+            if (++spins == (1u << 24)) {   // (cannot happen: an earlier tile never waits for this one)
+                printf("kme: radix look-back: tile %u waits for tiles %u.. (stamp %u)\n", tile, q0, stamp);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int b = 0; b < LB_BATCH; ++b)
+            if (q0 + b < tile) { P0 += (uint32_t)w[2 * b]; P1 += (uint32_t)w[2 * b + 1]; }
+    }
+    g0 = gx + P0;
+    g1 = gx + T0 + P1;
+}
+
+template <int TILE, bool LB = false>
+__global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int src, uint32_t stamp = 0) {
     static_assert(RADIX_DIGITS == 512, "two digits per thread");
     static_assert(TILE % 256 == 0, "whole rounds");
     __shared__ uint32_t wh[4][RADIX_DIGITS];     // wavefront w's count of digit d, then its first local slot
@@ -775,6 +863,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint32_t base = blockIdx.x * TILE, n = radix_n(R);
+    if (LB && base >= n) return;   // (a tile past the keys: no later tile waits for it)
     const int dst = src ^ 1;
     const int shift = RADIX_BITS * pass;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -816,8 +905,15 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
         uint32_t tot;
         const uint32_t ex = block_excl_scan_256(t0 + t1, wsum, tot);
         uint32_t r0 = ex, r1 = ex + t0;
-        gdelta[2 * t] = R.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - r0;
-        gdelta[2 * t + 1] = R.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - r1;
+        if constexpr (LB) {
+            uint32_t g0, g1;
+            radix_lb_offsets(R, pass, stamp, (n + TILE - 1) / TILE, t0, t1, wsum, g0, g1);
+            gdelta[2 * t] = g0 - r0;
+            gdelta[2 * t + 1] = g1 - r1;
+        } else {
+            gdelta[2 * t] = R.ghist[(size_t)(2 * t) * gridDim.x + blockIdx.x] - r0;
+            gdelta[2 * t + 1] = R.ghist[(size_t)(2 * t + 1) * gridDim.x + blockIdx.x] - r1;
+        }
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) { wh[ww][2 * t] = r0; wh[ww][2 * t + 1] = r1; r0 += c0[ww]; r1 += c1[ww]; }
     }
@@ -4188,6 +4284,20 @@ template <int TILE>
 static void radix_passes(const RadixIO& R, hipStream_t st) {
     const uint32_t ntiles = cdiv(R.n > 0 ? R.n : 1, TILE);
     int src = 0;
+    if (R.tcnt && R.lb && R.passes <= RADIX_MAXP && TILE == RADIX_TILE_SMALL) {
+        // a small sort: the per-tile counts of every pass in one launch, then one launch per pass
+        // (look-back offsets) instead of three (histogram, two scan kernels) before each scatter
+        static std::atomic<uint32_t> stamps{1};   // (one per scatter launch, any engine or thread: look-back
+                                                  // words of older launches never match)
+        hipLaunchKernelGGL(k_radix_tcnt<TILE>, dim3(ntiles), dim3(256), 0, st, R);
+        for (int pass = 0; pass < R.passes; ++pass) {
+            uint32_t stamp = stamps.fetch_add(1);
+            if (stamp == 0) stamp = stamps.fetch_add(1);
+            hipLaunchKernelGGL((k_radix_scatter<TILE, true>), dim3(ntiles), dim3(256), 0, st, R, pass, src, stamp);
+            src ^= 1;
+        }
+        return;
+    }
     for (int pass = 0; pass < R.passes; ++pass) {
         hipLaunchKernelGGL(k_radix_hist<TILE>, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
@@ -4216,6 +4326,8 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int l
     R.n = io.n;
     R.n_dev = nullptr;
     R.passes = S.passes;
+    R.tcnt = S.rtcnt;
+    R.lb = S.rlb;
     launch_radix(R, st);
     const int src = S.passes & 1;
     const uint32_t nthreads = (io.n + 1) > (uint32_t)S.G + 2 ? io.n + 1 : (uint32_t)S.G + 2;

@@ -39,7 +39,13 @@ struct RadixIO {
     const KG unsigned long long* n_dev;
     int passes;
     int small;                       // 2,048-key tiles (a small sort; n may be a capacity far above it)
+    // small sorts, one launch per pass (launch_radix): every pass's per-tile digit counts of the
+    // unpermuted keys (passes x tiles x digits: the digit totals), and the look-back words (tiles x
+    // digits: count | launch stamp << 32).  nullptr: the hist / scan / scatter launches per pass.
+    KG uint32_t* tcnt;
+    KG unsigned long long* lb;
 };
+constexpr int RADIX_MAXP = 4;        // passes of a look-back sort (tcnt's rows)
 void launch_radix(const RadixIO& R, hipStream_t st);
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st);
 // FUNDED + exact ledger: the epoch's ledger effects in parallel (kme_ledger.hip); the serial replay

@@ -805,6 +805,8 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.n_dev = S.lctr + ci(LC_OPS);
     R.passes = S.lpasses;
     R.small = n <= (1u << 17) ? 1 : 0;   // (~2 ops per record: the sort is small though nops is a capacity)
+    R.tcnt = R.small ? S.ltcnt : nullptr;   // (allocated for engines whose epochs are all small)
+    R.lb = R.small ? S.llb : nullptr;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lseg_gaps, dim3(std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024)), dim3(256), 0, st, S);

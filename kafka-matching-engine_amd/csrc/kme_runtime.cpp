@@ -430,6 +430,12 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lkey[0], nops); ALLOC(S.lkey[1], nops);
             ALLOC(S.lval[0], nops); ALLOC(S.lval[1], nops);
             ALLOC(S.lghist, lh + lh / 4096 + 4096);
+            // the op sort of a small epoch (launch_ledger_parallel: R.small) in one launch per pass
+            const uint64_t lt = (nops + RADIX_TILE_SMALL - 1) / RADIX_TILE_SMALL;
+            if (E <= (1u << 17) && lt <= 1024 && S.lpasses <= RADIX_MAXP) {
+                ALLOC(S.ltcnt, (size_t)RADIX_MAXP * lt * (1 << RADIX_BITS));
+                ALLOC(S.llb, (size_t)lt * (1 << RADIX_BITS));
+            }
             ALLOC(S.lrec, nops); ALLOC(S.lsrt, nops);
             ALLOC(S.lchain, nops); ALLOC(S.lhead, nops);
             ALLOC(S.lvw, nops); ALLOC(S.lvw_meta, nops); ALLOC(S.lvw_tgt, nops);
@@ -485,6 +491,11 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     }
     const uint64_t ntiles = (E + RADIX_TILE_SMALL - 1) / RADIX_TILE_SMALL;
     ALLOC(S.ghist, (size_t)(1 << RADIX_BITS) * ntiles + 2 * (E / 2048 + 16) + 4096);
+    {   // the partition's small sorts (at most RADIX_SMALL_N keys): look-back buffers
+        const uint64_t st = (std::min<uint64_t>(E, RADIX_SMALL_N) + RADIX_TILE_SMALL - 1) / RADIX_TILE_SMALL;
+        ALLOC(S.rtcnt, (size_t)RADIX_MAXP * st * (1 << RADIX_BITS));
+        ALLOC(S.rlb, (size_t)st * (1 << RADIX_BITS));
+    }
     ALLOC(S.seg, (size_t)G + 2);
     ALLOC(S.gflag, (size_t)G + 1); ALLOC(S.glist, (size_t)G + 1); ALLOC(S.gcount, 64 + (size_t)G / 4096 + 64);
     ALLOC(S.ctr, (size_t)C_NCTR * CTR_STRIDE);
