@@ -475,8 +475,9 @@ __global__ void k_ledger_funded(DevState S, EpochIO io) {
 // and UNPROVEN (18) is the largest: a fault of record 0 (e.g. a duplicate oid) is reported instead.
 // That is the reference's outcome -- it throws at record 0 whatever the ledger holds (KP:96) -- and
 // either way no record of the epoch takes effect.
-__global__ void k_check_funded(DevState S, EpochIO io) {
-    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// (Run by k_route's blocks past its records: the check is independent of the routing, and a launch of
+// its own cost ~4 us of the drop-in's 65,536-record epochs.)
+KDEV void check_funded(const DevState& S, const EpochIO& io, int64_t a) {
     if (a >= S.A) return;
     const int64_t need = S.acct_need[a];
     if (need <= 0) return;
@@ -486,14 +487,13 @@ __global__ void k_check_funded(DevState S, EpochIO io) {
         else raise_thread(S.ctr, KME_E_UNFUNDED, KME_D_UNPROVEN, 0);
     }
 }
-// The bounds roll forward once the whole proof is in (a kernel boundary after k_check_funded):
+// The bounds roll forward once the whole proof is in (k_settle_funded, after the epoch's matching:
+// nothing between reads the bounds, and the roll-forward was a launch of its own before k_route):
 // lb = lb_start - need + transfers.  An epoch none of whose records takes effect (refused by the
 // proof, or faulting at its first record) changes no bound, and the accounts its CREATE_BALANCE
 // records created (k_ledger_funded, for the acct_ok of the epoch's later orders) are absent again:
 // nothing of it took effect, so the caller can resubmit it (KME_E_UNFUNDED is not fatal).
-__global__ void k_commit_funded(DevState S, EpochIO io) {
-    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= S.A) return;
+KDEV void commit_funded(const DevState& S, const EpochIO& io, int64_t a) {
     const unsigned long long c = S.ctr[ci(C_ERR)];
     const bool refused = c != ~0ull && (c >> 16) == 0;
     if (refused && S.ctr[ci(C_ACCT_OPS)] != 0) {
@@ -512,7 +512,7 @@ __global__ void k_commit_funded(DevState S, EpochIO io) {
 
 // ------------------------------------------------------------------ credit between symbol shards
 // With symbols keyed over N engines (credit_shards = N) each engine proves its orders against its
-// own share of an account's cash (k_ledger_funded / k_check_funded), and the funded bound only falls
+// own share of an account's cash (k_ledger_funded / check_funded), and the funded bound only falls
 // inside the proof (refunds are not credited back, KP:269, 286, 331), so a share can run dry while
 // the account's other shares still hold most of its cash.  Between epochs the shares are pooled and
 // split again: every engine contributes (funded bound, demand so far), all-gathers them
@@ -523,7 +523,7 @@ __global__ void k_commit_funded(DevState S, EpochIO io) {
 // pooled bound, so the invariant the proof rests on -- the account's cash is at least the sum of the
 // shards' bounds -- holds across the re-split.
 // An account absent on a shard (never created there, or created by an epoch only that shard refused,
-// k_commit_funded) reports demand -1: it takes no share, and the rounding left-over goes to a shard
+// commit_funded) reports demand -1: it takes no share, and the rounding left-over goes to a shard
 // that holds the account, so no credit leaves the pool.
 __global__ void __launch_bounds__(256) k_credit_state(DevState S, int64_t* out) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -574,6 +574,11 @@ __global__ void __launch_bounds__(256) k_credit_adjust(DevState S, const int64_t
 // (exchange_test.js:101): removeOrder finds it by oid alone (KP:290).  Target = an order of this
 // epoch submitted earlier (encoded -(j+2)), else a resting order from the oid table, else none.
 __global__ void k_route(DevState S, EpochIO io, int funded) {
+    const uint32_t nb = (io.n + blockDim.x - 1) / blockDim.x;
+    if (blockIdx.x >= nb) {   // FUNDED: the blocks past the records check the accounts' proof
+        check_funded(S, io, (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x);
+        return;
+    }
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= io.n) return;
     const int32_t a = io.action[i];
@@ -3950,11 +3955,14 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
     }
 }
 
-// FUNDED + KME_FLAG_SERIAL_FALLBACK, after an epoch k_serial took: the funded bounds restart from
-// the exact ledger (balance = the tightest lower bound; an account exists from the epoch's end).
-__global__ void __launch_bounds__(256) k_resync_funded(DevState S, EpochIO io) {
+// FUNDED, after the epoch's matching: the bounds roll forward (commit_funded), and with
+// KME_FLAG_SERIAL_FALLBACK, after an epoch k_serial took, they restart from the exact ledger
+// (balance = the tightest lower bound; an account exists from the epoch's end).
+__global__ void __launch_bounds__(256) k_settle_funded(DevState S, EpochIO io) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= S.A || !S.ctr[ci(C_FALLBACK)] || failed(S.ctr)) return;
+    if (a >= S.A) return;
+    commit_funded(S, io, a);
+    if (!S.fallback || !S.ctr[ci(C_FALLBACK)] || failed(S.ctr)) return;
     uint32_t h = (uint32_t)mix64((uint64_t)a) & S.bal_mask;   // Core::bal_find
     int64_t bal = 0;
     bool found = false;
@@ -4255,14 +4263,11 @@ void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_funded, dim3(1), dim3(64), 0, st, S, io);
 }
-void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
-    if (S.A == 0) return;
-    hipLaunchKernelGGL(k_check_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_commit_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
-}
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st) {
-    if (io.n == 0) return;
-    hipLaunchKernelGGL(k_route, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io, funded ? 1 : 0);
+    // FUNDED: the accounts' check of the funded proof in the blocks past the records
+    const uint32_t nb = cdiv(io.n, 256) + (funded && io.n > 0 ? cdiv((uint32_t)S.A, 256) : 0);
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_route, dim3(nb), dim3(256), 0, st, S, io, funded ? 1 : 0);
 }
 void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, uint32_t* total, hipStream_t st) {
     const uint32_t nb = cdiv(L > 0 ? L : 1, SCAN_BLOCK);
@@ -4390,8 +4395,9 @@ void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStrea
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, int only_fallback) {
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev, only_fallback);
 }
-void launch_resync_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
-    hipLaunchKernelGGL(k_resync_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
+void launch_settle_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
+    if (S.A == 0) return;
+    hipLaunchKernelGGL(k_settle_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
 }
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
     (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);

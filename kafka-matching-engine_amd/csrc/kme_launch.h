@@ -56,7 +56,6 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
 void launch_epoch_reset(const DevState& S, hipStream_t st);   // the per-epoch counters, one launch
 void launch_emap(const DevState& S, const EpochIO& io, bool funded, EpochIO* io_dev, hipStream_t st);
 void launch_ledger_funded(const DevState& S, const EpochIO& io, hipStream_t st);
-void launch_check_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 void launch_route(const DevState& S, const EpochIO& io, bool funded, hipStream_t st);
 // returns the buffer index (0/1) holding the sorted input permutation
 // list_min >= 0: k_segments also lists the groups with more than list_min records (glist, C_GLIST)
@@ -75,7 +74,7 @@ void launch_table(const DevState& S, const EpochIO& io, hipStream_t st);
 // EXACT pipeline (emap + route shared)
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, int only_fallback = 0);
 // FUNDED + KME_FLAG_SERIAL_FALLBACK: funded bounds from the exact ledger after a serial epoch
-void launch_resync_funded(const DevState& S, const EpochIO& io, hipStream_t st);
+void launch_settle_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 // FUNDED + KME_FLAG_EXACT_LEDGER: the epoch's ledger effects in arrival order (after compaction)
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
 // exclusive scan of L u32 values (DPP wave scans): out[k] = sum(in[0..k)); bsum needs

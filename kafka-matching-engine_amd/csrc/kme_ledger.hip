@@ -6,7 +6,7 @@
 // and the position store's value-keyed writes KP:434-436 (hazard H2).
 //
 // After the parallel matching every outcome of the epoch is fixed (accept / reject, every trade):
-// the funded proof (k_check_funded) guarantees each checkBalance passes.  What remains are the
+// the funded proof (check_funded, in k_route) guarantees each checkBalance passes.  What remains are the
 // ledger's values, and they decompose:
 //
 //   * Balances: every effect is an addition (checkBalance's -risk, a fill's size * price, a refund,
@@ -325,13 +325,15 @@ __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
 // (the ops themselves were gathered into sorted order by the sort's last pass: lsrt)
 // lseg[a] = the number of sorted ops of accounts below a, for a in [0, A]: thread k (an op, or k = n)
 // writes k for the accounts after op k - 1's up to op k's.  A gap longer than LSEG_RUN accounts goes
-// to a list that k_lseg_gaps fills a workgroup per entry, in pieces of at most LSEG_PIECE accounts:
-// one thread walking a gap was the serial tail when the ops name a few of many accounts (the last
-// op's thread walked to A: 13 ms per epoch at A = 2^20 with 65,536 accounts in use), and so was one
-// workgroup per gap (the gap past the last account in use, ~2^20 accounts: 0.11 ms of the drop-in's
-// 0.45-ms epoch, round 6).
+// to a list that k_lseg_gaps fills a workgroup per gap, and a gap longer than LSEG_HUGE to a second
+// list (from the top of lgap) that every workgroup of k_lseg_gaps fills a slice of: one thread walking
+// a gap was the serial tail when the ops name a few of many accounts (the last op's thread walked to
+// A: 13 ms per epoch at A = 2^20 with 65,536 accounts in use), and so was one workgroup per gap (the
+// gap past the last account in use: 0.11 ms of the drop-in's 0.45-ms epoch, round 6).  One counter
+// word counts both lists (low / high 32 bits).
 constexpr uint32_t LSEG_RUN = 256;
-constexpr uint32_t LSEG_PIECE = 4096;
+constexpr uint32_t LSEG_HUGE = 1u << 16;
+KDEV uint32_t lgap_cap(const DevState& S) { return (uint32_t)S.A / 256 + (uint32_t)S.A / 4096 + 8; }   // (its allocation)
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,20 +343,21 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
     if (cur - prev <= (int64_t)LSEG_RUN) {
         for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
+    } else if (cur - prev <= (int64_t)LSEG_HUGE) {
+        const uint32_t x = (uint32_t)atomicAdd(lc(S, LC_GAPS), 1ull);   // < (A + 1) / LSEG_RUN + 1
+        S.lgap[x] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
     } else {
-        // entries: < (A + 1) / LSEG_RUN gaps, plus (A + 1) / LSEG_PIECE pieces past their first
-        const uint32_t lo = (uint32_t)(prev + 1), len = (uint32_t)(cur - prev);
-        const uint32_t np = (len + LSEG_PIECE - 1) / LSEG_PIECE;
-        const unsigned long long x = atomicAdd(lc(S, LC_GAPS), (unsigned long long)np);
-        for (uint32_t q = 0; q < np; ++q) {
-            const uint32_t a0 = lo + q * LSEG_PIECE;
-            const uint32_t a1 = q + 1 == np ? (uint32_t)cur : a0 + LSEG_PIECE - 1;
-            S.lgap[x + q] = make_uint4(a0, a1, k, 0);
-        }
+        const uint32_t y = (uint32_t)(atomicAdd(lc(S, LC_GAPS), 1ull << 32) >> 32);   // < (A + 1) / LSEG_HUGE + 1
+        S.lgap[lgap_cap(S) - 1 - y] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
     }
 }
 __global__ void __launch_bounds__(256) k_lseg_gaps(DevState S) {
-    const uint32_t ng = (uint32_t)__hip_atomic_load(lc(S, LC_GAPS), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long c = __hip_atomic_load(lc(S, LC_GAPS), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ng = (uint32_t)c, nh = (uint32_t)(c >> 32);
+    for (uint32_t y = 0; y < nh; ++y) {   // the huge gaps: a slice of each per workgroup
+        const uint4 g = S.lgap[lgap_cap(S) - 1 - y];
+        for (uint32_t a = g.x + blockIdx.x * blockDim.x + threadIdx.x; a <= g.y; a += gridDim.x * blockDim.x) S.lseg[a] = g.z;
+    }
     for (uint32_t x = blockIdx.x; x < ng; x += gridDim.x) {
         const uint4 g = S.lgap[x];
         for (uint32_t a = g.x + threadIdx.x; a <= g.y; a += blockDim.x) S.lseg[a] = g.z;

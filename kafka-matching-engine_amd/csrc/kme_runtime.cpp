@@ -620,8 +620,7 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     // bound by the same random accesses.)
     if (funded) {
         phase_begin(e, PH_LEDGER);
-        launch_ledger_funded(S, io, st);
-        launch_check_funded(S, io, st);
+        launch_ledger_funded(S, io, st);   // (the per-account check runs in k_route's launch)
         phase_end(e, PH_LEDGER);
     }
     phase_begin(e, PH_ROUTE);
@@ -670,9 +669,9 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
         if (S.fallback) {   // an epoch whose funded proof failed: the serial engine takes it
             phase_begin(e, PH_SERIAL);
             launch_serial(e->d_S, e->d_io, st, 1);
-            launch_resync_funded(S, io, st);
             phase_end(e, PH_SERIAL);
         }
+        launch_settle_funded(S, io, st);   // the bounds roll forward (or restart after k_serial)
         if (S.ledger_replay) {
             phase_begin(e, PH_REPLAY);
             if (S.lpar) {
