@@ -262,10 +262,10 @@ KDEV int32_t find_chain(const DevState& S, int64_t k0, int64_t k1) {
 // maker's key) and taker fill, an accepted cancel's postRemoveAdjustments.
 __global__ void __launch_bounds__(256) k_lcount(DevState S, EpochIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    // the epoch's counters and per-account deltas start at 0 (was three fills before this launch)
+    // the epoch's counters start at 0 (was fills before this launch; the per-account deltas are 0
+    // already: k_lbalances takes each one it settles)
     if (i < (uint32_t)(LC_N * CTR_STRIDE)) S.lctr[i] = 0;
     if (i < (uint32_t)(LPOSC_LINES * CTR_STRIDE)) S.lposc[i] = 0;
-    for (int64_t a = i; a < S.A; a += (int64_t)gridDim.x * blockDim.x) S.ldelta[a] = 0;
     if (i >= io.n) return;
     uint32_t c = 0;
     if (!lskip(S)) {
@@ -759,10 +759,23 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
     if (full) raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
     wave_add_spread(S, grew);
 }
+// The accounts' balance deltas (k_lchains, the repairs, k_lacct's transfers) onto Balances: one thread
+// per account run of the sorted ops and per transfer record -- the accounts the epoch touched, not
+// all A of them (2^20 at the drop-in's defaults: a pass over every account's delta, and its clear at
+// k_lcount, were ~20 us of its 65,536-record epoch).  Each delta is taken with an exchange, so an
+// account reached twice is settled once and every delta is 0 again for the next epoch -- also when
+// this epoch's pass fell back or was skipped (then nothing is applied).
+KDEV void settle_delta(const DevState& S, const EpochIO& io, int64_t a, bool apply) {
+    const int64_t d = (int64_t)atomicExch(reinterpret_cast<KG unsigned long long*>(&S.ldelta[a]), 0ull);
+    if (d == 0 || !apply) return;
+    const int32_t h = bal_lookup(S, a);
+    if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); return; }   // (cannot happen)
+    S.bal_val[h] = jladd(S.bal_val[h], d);
+}
 __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
-    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= S.A || lskip(S) || lfell(S)) return;
-    if (a == 0) {   // the positions k_linsert created (its spread counters), and the tables' load, as Core's inserts check it
+    const bool apply = !(lskip(S) || lfell(S));
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, T = gridDim.x * blockDim.x;
+    if (t == 0 && apply) {   // the positions k_linsert created (its spread counters), and the tables' load, as Core's inserts check it
         unsigned long long grew = 0;
         for (int k = 0; k < LPOSC_LINES; ++k) grew += S.lposc[(size_t)k * CTR_STRIDE];
         const unsigned long long used = S.ctr[ci(C_POS_USED)] + grew;
@@ -770,11 +783,17 @@ __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
         if (used * 4 > ((unsigned long long)S.pos_mask + 1) * 3 || S.ctr[ci(C_BAL_USED)] * 2 > (unsigned long long)S.bal_mask + 1)
             raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
     }
-    const int64_t d = S.ldelta[a];
-    if (d == 0) return;
-    const int32_t h = bal_lookup(S, a);
-    if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); return; }   // (cannot happen)
-    S.bal_val[h] = jladd(S.bal_val[h], d);
+    const uint32_t no = lops(S);
+    const KG uint32_t* K = skeys(S);
+    for (uint32_t k = t; k < no; k += T) {
+        const uint32_t a = K[k] >> S.lhbits;
+        if (k == 0 || (K[k - 1] >> S.lhbits) != a) settle_delta(S, io, (int64_t)a, apply);
+    }
+    if (S.ctr[ci(C_ACCT_OPS)] == 0) return;
+    for (uint32_t i = t; i < io.n; i += T) {
+        const int64_t a = io.aid[i];
+        if (io.action[i] == TRANSFER && a >= 0 && a < S.A) settle_delta(S, io, a, apply);
+    }
 }
 
 // ---------------------------------------------------------------- launcher
@@ -834,7 +853,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_linsert, dim3(gl), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lbalances, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_lbalances, dim3(std::max(gs, cdiv(n, 256))), dim3(256), 0, st, S, io);
 }
 
 }  // namespace kme

@@ -442,6 +442,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
             ALLOC(S.lseg, (size_t)cfg->max_accounts + 2);
             ALLOC(S.lgap, (size_t)cfg->max_accounts / 256 + (size_t)cfg->max_accounts / 4096 + 8);   // (k_lseg's gaps)
             ALLOC(S.ldelta, cfg->max_accounts);
+            HIP_TRY(hipMemsetAsync(S.ldelta, 0, sizeof(int64_t) * cfg->max_accounts, e->stream));   // (then kept 0: k_lbalances)
             ALLOC(S.lvk, vk);
             HIP_TRY(hipMemsetAsync(S.lvk, 0, sizeof(ulonglong4) * vk, e->stream));   // (tags from 1 on)
             ALLOC(S.lx, S.lx_cap); ALLOC(S.lxn, S.lx_cap);
