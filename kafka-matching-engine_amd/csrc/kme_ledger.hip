@@ -120,16 +120,6 @@ KDEV void wave_add_spread(const DevState& S, uint32_t v) {
     const uint32_t line = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (LPOSC_LINES - 1);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(&S.lposc[(size_t)line * CTR_STRIDE], (unsigned long long)v);
 }
-KDEV int32_t bal_lookup(const DevState& S, int64_t aid) {
-    uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
-    for (uint32_t p = 0; p <= S.bal_mask; ++p) {
-        const uint32_t st = ld_state(&S.bal_state[h]);
-        if (st == 0) return -1;
-        if (st == 1 && S.bal_key[h] == aid) return (int32_t)h;
-        h = (h + 1) & S.bal_mask;
-    }
-    return -1;
-}
 // createBalance's put (KP:134), same protocol (balances are never deleted: no tombstones)
 KDEV bool bal_create(const DevState& S, int64_t aid) {
     for (int attempt = 0; attempt < 4096; ++attempt) {
@@ -765,14 +755,29 @@ __global__ void __launch_bounds__(256) k_linsert(DevState S, EpochIO io) {
 // k_lcount, were ~20 us of its 65,536-record epoch).  Each delta is taken with an exchange, so an
 // account reached twice is settled once and every delta is 0 again for the next epoch -- also when
 // this epoch's pass fell back or was skipped (then nothing is applied).
+// (Balances are not inserted into during k_lbalances -- k_lacct's creates are a launch earlier -- so the
+// probe takes plain loads: bal_lookup's acquire loads invalidate the CU's caches per instruction, which
+// for one active lane per wavefront made this pass 0.48 ms at C3.)
+KDEV int32_t bal_find_settled(const DevState& S, int64_t aid) {
+    uint32_t h = (uint32_t)mix64((uint64_t)aid) & S.bal_mask;
+    for (uint32_t p = 0; p <= S.bal_mask; ++p) {
+        const uint32_t st = S.bal_state[h];
+        if (st == 0) return -1;
+        if (st == 1 && S.bal_key[h] == aid) return (int32_t)h;
+        h = (h + 1) & S.bal_mask;
+    }
+    return -1;
+}
 KDEV void settle_delta(const DevState& S, const EpochIO& io, int64_t a, bool apply) {
     const int64_t d = (int64_t)atomicExch(reinterpret_cast<KG unsigned long long*>(&S.ldelta[a]), 0ull);
     if (d == 0 || !apply) return;
-    const int32_t h = bal_lookup(S, a);
+    const int32_t h = bal_find_settled(S, a);
     if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); return; }   // (cannot happen)
     S.bal_val[h] = jladd(S.bal_val[h], d);
 }
-__global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
+// all = 1 (accounts not many more than the epoch's records, C3): one thread per account instead --
+// the touched accounts' run heads are then a sparse lane or two per wavefront.
+__global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io, int all) {
     const bool apply = !(lskip(S) || lfell(S));
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, T = gridDim.x * blockDim.x;
     if (t == 0 && apply) {   // the positions k_linsert created (its spread counters), and the tables' load, as Core's inserts check it
@@ -782,6 +787,18 @@ __global__ void __launch_bounds__(256) k_lbalances(DevState S, EpochIO io) {
         S.ctr[ci(C_POS_USED)] = used;
         if (used * 4 > ((unsigned long long)S.pos_mask + 1) * 3 || S.ctr[ci(C_BAL_USED)] * 2 > (unsigned long long)S.bal_mask + 1)
             raise_thread(S.ctr, KME_E_CAPACITY, KME_D_CAP_LEDGER, io.n);
+    }
+    if (all) {
+        for (int64_t a = t; a < S.A; a += T) {
+            const int64_t d = S.ldelta[a];
+            if (d == 0) continue;
+            S.ldelta[a] = 0;
+            if (!apply) continue;
+            const int32_t h = bal_find_settled(S, a);
+            if (h < 0) { raise_thread(S.ctr, KME_E_DOMAIN, KME_D_NPE_BALANCE, io.n); continue; }   // (cannot happen)
+            S.bal_val[h] = jladd(S.bal_val[h], d);
+        }
+        return;
     }
     const uint32_t no = lops(S);
     const KG uint32_t* K = skeys(S);
@@ -853,7 +870,8 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_linsert, dim3(gl), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lbalances, dim3(std::max(gs, cdiv(n, 256))), dim3(256), 0, st, S, io);
+    const int all = (uint64_t)S.A <= 4ull * n ? 1 : 0;
+    hipLaunchKernelGGL(k_lbalances, dim3(all ? cdiv((uint32_t)S.A, 256) : std::max(gs, cdiv(n, 256))), dim3(256), 0, st, S, io, all);
 }
 
 }  // namespace kme
