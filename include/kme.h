@@ -73,8 +73,10 @@ enum kme_domain {
                                 (sid << 8) | price (KP:379-381) then aliases other books' buckets */
     KME_D_GUARD_OTPOS = 20,  /* internal consistency check (k_match_lanes): an oid-table position
                                 outside the table; never expected (a bug report, not an input fault) */
-    KME_D_GUARD_SLOT = 21    /* internal consistency check (k_match_lanes): a node slot outside the
+    KME_D_GUARD_SLOT = 21,   /* internal consistency check (k_match_lanes): a node slot outside the
                                 pool; never expected */
+    KME_D_GUARD_LOOKBACK = 22  /* internal check (KME_E_HIP): a small sort's or scan's look-back found
+                                an earlier tile's word missing for ~1 s; never expected */
 };
 
 /* Engine modes.

@@ -846,6 +846,7 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
             if (all) break;
             if (++spins == (1u << 24)) {   // (cannot happen: an earlier tile never waits for this one)
                 printf("kme: radix look-back: tile %u waits for tiles %u.. (stamp %u)\n", tile, q0, stamp);
+                if (R.ctr) raise_thread(R.ctr, KME_E_HIP, KME_D_GUARD_LOOKBACK, -1);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1029,7 +1030,8 @@ __global__ void __launch_bounds__(256) k_tile_sums(const uint32_t* in, uint32_t 
 constexpr uint32_t LB_MAX_TILES = 64;
 template <bool LB = false>
 __global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t* out, uint32_t L, const uint32_t* sums,
-                                                    uint32_t* total_out, int write_end, uint32_t stamp = 0) {
+                                                    uint32_t* total_out, int write_end, uint32_t stamp = 0,
+                                                    unsigned long long* ctr = nullptr) {
     __shared__ uint32_t buf[LB_TILE + LB_TILE / 32];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x;
@@ -1059,6 +1061,7 @@ __global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t
                 if ((uint32_t)(v >> 32) == stamp) break;
                 if (spins == (1u << 24)) {   // (cannot happen: an earlier tile never waits for this one)
                     printf("kme: scan look-back: tile %u waits for tile %d (stamp %u)\n", tile, t, stamp);
+                    if (ctr) raise_thread(ctr, KME_E_HIP, KME_D_GUARD_LOOKBACK, -1);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -4306,17 +4309,19 @@ void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, 
 // Exclusive scan of in[0, L) into out (in place allowed): tile sums, then the tiles (sums scratch:
 // cdiv(L, LB_TILE) words).
 static void launch_scan2(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, int write_end,
-                         hipStream_t st) {
+                         hipStream_t st, unsigned long long* ctr) {
     const uint32_t nb = cdiv(L > 0 ? L : 1, LB_TILE);
     if (nb <= LB_MAX_TILES && ((uintptr_t)sums & 7) == 0) {   // a small scan: one launch (look-back)
         static std::atomic<uint32_t> stamps{1};
         uint32_t stamp = stamps.fetch_add(1);
         if (stamp == 0) stamp = stamps.fetch_add(1);
-        hipLaunchKernelGGL(k_scan_tiles<true>, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end, stamp);
+        hipLaunchKernelGGL(k_scan_tiles<true>, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end, stamp,
+                           ctr);
         return;
     }
     hipLaunchKernelGGL(k_tile_sums, dim3(nb), dim3(256), 0, st, in, L, sums);
-    hipLaunchKernelGGL(k_scan_tiles<false>, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end, 0u);
+    hipLaunchKernelGGL(k_scan_tiles<false>, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end, 0u,
+                       ctr);
 }
 // Stable LSD radix sort of (key, value) pairs, R.passes digit passes; the result is in keys / vals
 // [R.passes & 1].
@@ -4342,7 +4347,7 @@ static void radix_passes(const RadixIO& R, hipStream_t st) {
         hipLaunchKernelGGL(k_radix_hist<TILE>, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         // exclusive scan of the digit-major histogram, in place (scratch at the tail of ghist)
         const uint32_t L = RADIX_DIGITS * ntiles;
-        launch_scan2(R.ghist, R.ghist, L, R.ghist + L, nullptr, 0, st);
+        launch_scan2(R.ghist, R.ghist, L, R.ghist + L, nullptr, 0, st, R.ctr);
         hipLaunchKernelGGL(k_radix_scatter<TILE>, dim3(ntiles), dim3(256), 0, st, R, pass, src);
         src ^= 1;
     }
@@ -4351,8 +4356,9 @@ void launch_radix(const RadixIO& R, hipStream_t st) {
     if (R.small || R.n <= RADIX_SMALL_N) radix_passes<RADIX_TILE_SMALL>(R, st);
     else radix_passes<RADIX_TILE>(R, st);
 }
-void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st) {
-    launch_scan2(in, out, L, sums, total, 0, st);
+void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st,
+                      unsigned long long* ctr) {
+    launch_scan2(in, out, L, sums, total, 0, st, ctr);
 }
 int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int list_min) {
     RadixIO R{};
@@ -4368,6 +4374,7 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int l
     R.passes = S.passes;
     R.tcnt = S.rtcnt;
     R.lb = S.rlb;
+    R.ctr = S.ctr;
     launch_radix(R, st);
     const int src = S.passes & 1;
     const uint32_t nthreads = (io.n + 1) > (uint32_t)S.G + 2 ? io.n + 1 : (uint32_t)S.G + 2;
@@ -4394,7 +4401,7 @@ void launch_match(const DevState& S, const DevState* S_dev, const EpochIO* io_de
         hipLaunchKernelGGL(k_glist_flags, dim3(cdiv(G, 256)), dim3(256), 0, st, S, all);
         // exclusive scan of G + 1 flags (the last one 0: pos[G] = the count), in place
         (void)hipMemsetAsync(S.gflag + G, 0, sizeof(uint32_t), st);
-        launch_excl_scan(S.gflag, S.gflag, G + 1, S.gcount + 64, S.gcount, st);
+        launch_excl_scan(S.gflag, S.gflag, G + 1, S.gcount + 64, S.gcount, st, S.ctr);
         hipLaunchKernelGGL(k_glist_scatter, dim3(cdiv(G, 256)), dim3(256), 0, st, S, (const uint32_t*)S.gflag);
     }
     if (two) hipLaunchKernelGGL((k_match<true, 4>), dim3((uint32_t)S.G), dim3(128), 0, st, S_dev, io_dev, buf, all, dense);
@@ -4413,7 +4420,7 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n > 0) hipLaunchKernelGGL(k_unsort, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);
     // trade_off[0..n] = exclusive scan of n_trades; bsum/total scratch in ghist
     uint32_t* total = S.ghist;   // (the partition's histograms are dead by now)
-    launch_scan2(io.n_trades, io.trade_off, io.n, S.ghist + 64, total, 1, st);
+    launch_scan2(io.n_trades, io.trade_off, io.n, S.ghist + 64, total, 1, st, S.ctr);
     hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1, SCATTER_SUB), dim3(256), 0, st, S, io, (const uint32_t*)total);
     static_assert(TSHARDS == 256, "k_tsh_fold: one thread per shard line");
     hipLaunchKernelGGL(k_tsh_fold, dim3(1), dim3(256), 0, st, S);

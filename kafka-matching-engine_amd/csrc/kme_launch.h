@@ -44,10 +44,12 @@ struct RadixIO {
     // digits: count | launch stamp << 32).  nullptr: the hist / scan / scatter launches per pass.
     KG uint32_t* tcnt;
     KG unsigned long long* lb;
+    KG unsigned long long* ctr;      // the engine's counters: a look-back that never completes is raised there
 };
 constexpr int RADIX_MAXP = 4;        // passes of a look-back sort (tcnt's rows)
 void launch_radix(const RadixIO& R, hipStream_t st);
-void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st);
+void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st,
+                      unsigned long long* ctr);
 // FUNDED + exact ledger: the epoch's ledger effects in parallel (kme_ledger.hip); the serial replay
 // (launch_ledger_replay) runs after it and does the work only when this path fell back
 void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_trades, hipStream_t st);

@@ -828,7 +828,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     static_assert(LC_N * CTR_STRIDE <= 256 && LPOSC_LINES * CTR_STRIDE <= 1024, "k_lcount's first threads clear them");
     hipLaunchKernelGGL(k_lcount, dim3(std::max<uint32_t>(cdiv(n, 256), 4)), dim3(256), 0, st, S, io);
     // offsets (in place) and the op count (LC_OPS, low word)
-    launch_excl_scan(S.lcnt, S.lcnt, n, S.lscan, reinterpret_cast<uint32_t*>(S.lctr + ci(LC_OPS)), st);
+    launch_excl_scan(S.lcnt, S.lcnt, n, S.lscan, reinterpret_cast<uint32_t*>(S.lctr + ci(LC_OPS)), st, S.ctr);
     hipLaunchKernelGGL(k_lgen, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
     RadixIO R{};
     R.key0 = reinterpret_cast<const KG int32_t*>(S.lk0);
@@ -846,6 +846,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.small = n <= (1u << 17) ? 1 : 0;   // (~2 ops per record: the sort is small though nops is a capacity)
     R.tcnt = R.small ? S.ltcnt : nullptr;   // (allocated for engines whose epochs are all small)
     R.lb = R.small ? S.llb : nullptr;
+    R.ctr = S.ctr;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lseg_gaps, dim3(std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024)), dim3(256), 0, st, S);

@@ -193,7 +193,32 @@ static bool staged_d2h(kme_engine* e, void* dst, const void* src, size_t bytes, 
         return true;
     });
 }
+// Host -> device through the engine's pinned ring when it has one (the checkpoint writer's slots):
+// the copy of slot k overlaps the memcpy into slot k + 1, a slot reused once its event completed.
+static bool ring_h2d(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    kme::PinnedRing& R = e->ring;
+    bool used[kme::kRingSlots] = {};
+    int k = 0;
+    hipError_t r = hipSuccess;
+    for (size_t off = 0; off < bytes && r == hipSuccess; off += kme::kRingSlot) {
+        const size_t c = std::min(kme::kRingSlot, bytes - off);
+        if (used[k]) r = hipEventSynchronize(R.ev[k]);
+        if (r != hipSuccess) break;
+        std::memcpy(R.slot[k], (const char*)src + off, c);
+        r = hipMemcpyAsync((char*)dst + off, R.slot[k], c, hipMemcpyHostToDevice, e->stream);
+        if (r == hipSuccess) r = hipEventRecord(R.ev[k], e->stream);
+        used[k] = true;
+        k = (k + 1) % kme::kRingSlots;
+    }
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);   // (the slots are reused by the next call)
+    if (r != hipSuccess) {
+        std::fprintf(stderr, "kme: device write of %s (%zu bytes at %p) failed: %s\n", what, bytes, dst, hipGetErrorString(r));
+        return false;
+    }
+    return true;
+}
 static bool staged_h2d(kme_engine* e, void* dst, const void* src, size_t bytes, const char* what) {
+    if (bytes > kStage && e->ring.init(e->device)) return ring_h2d(e, dst, src, bytes, what);
     if (!stage_ready(e)) return false;
     for (size_t off = 0; off < bytes; off += kStage) {
         const size_t c = std::min(kStage, bytes - off);
