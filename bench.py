@@ -527,19 +527,26 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     t_sub = {}
+    sub_cpu = []   # the host's time inside each submit call (launches), beside the epoch's wall time
     for j in range(args.steps):
         k = args.warmup + j
         if pipelined:
             if j == 0:
                 t_sub[k] = time.perf_counter()
                 submit_epoch(k)
+                sub_cpu.append(time.perf_counter() - t_sub[k])
             if j + 1 < args.steps:
                 t_sub[k + 1] = time.perf_counter()
                 submit_epoch(k + 1)
+                sub_cpu.append(time.perf_counter() - t_sub[k + 1])
             st = eng.wait()
         else:
             t_sub[k] = time.perf_counter()
-            st = run_epoch(k)
+            submit_epoch(k)
+            sub_cpu.append(time.perf_counter() - t_sub[k])
+            st = eng.wait()
+            if args.serialize:  # MatchOut text of the epoch, printed on the GPU, left in HBM
+                tape_bytes.append(eng.tape_json_device_into(epoch_ptrs(k), E, tape_buf.data_ptr(), tape_buf.numel()))
         lat.append((time.perf_counter() - t_sub[k]) * 1e3)   # submit -> results ready
         ph = eng.phase_times()
         match_ms.append(ph["match"])
@@ -677,6 +684,7 @@ def main():
             "build_id": build_id,
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),
+            "host_submit_ms": float(np.mean(sub_cpu) * 1e3),   # the host's time in each submit (kernel launches)
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
             "market_data": {"symbols": int(sum(len(p) for p in per_rank)), "bytes_per_epoch": int(world * rows * 16),

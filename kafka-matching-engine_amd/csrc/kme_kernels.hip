@@ -3989,7 +3989,10 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
 // FUNDED, after the epoch's matching: the bounds roll forward (commit_funded), and with
 // KME_FLAG_SERIAL_FALLBACK, after an epoch k_serial took, they restart from the exact ledger
 // (balance = the tightest lower bound; an account exists from the epoch's end).
+KDEV void tsh_fold(const DevState& S);
 __global__ void __launch_bounds__(256) k_settle_funded(DevState S, EpochIO io) {
+    static_assert(TSHARDS == 256, "tsh_fold: one thread per shard line");
+    if (blockIdx.x == 0) tsh_fold(S);   // the trade shards' counters (was k_tsh_fold, a launch of its own)
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
     commit_funded(S, io, a);
@@ -4168,7 +4171,9 @@ __global__ void __launch_bounds__(256) k_scatter(DevState S, EpochIO io, const u
     }
 }
 // The shard lines' rest / cancel counts into the counters block; the lines zeroed for the next epoch.
-__global__ void __launch_bounds__(256) k_tsh_fold(DevState S) {
+// (Run by k_settle_funded's first block: after k_scatter read TS_USED and after k_serial, whose
+// counters of a fallback epoch it leaves as they are -- the parallel kernels left the lines at 0.)
+KDEV void tsh_fold(const DevState& S) {
     __shared__ uint32_t red[4];
     KG unsigned long long* line = S.tsh + (size_t)threadIdx.x * CTR_STRIDE;   // TSHARDS == 256 threads
     const unsigned long long rests = line[TS_RESTS], cancels = line[TS_CANCELS], light = line[TS_LIGHT];
@@ -4422,8 +4427,7 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
     uint32_t* total = S.ghist;   // (the partition's histograms are dead by now)
     launch_scan2(io.n_trades, io.trade_off, io.n, S.ghist + 64, total, 1, st, S.ctr);
     hipLaunchKernelGGL(k_scatter, dim3(TSHARDS + 1, SCATTER_SUB), dim3(256), 0, st, S, io, (const uint32_t*)total);
-    static_assert(TSHARDS == 256, "k_tsh_fold: one thread per shard line");
-    hipLaunchKernelGGL(k_tsh_fold, dim3(1), dim3(256), 0, st, S);
+    // (the shard counters are folded by k_settle_funded's first block)
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
@@ -4438,8 +4442,7 @@ void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st,
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev, only_fallback);
 }
 void launch_settle_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
-    if (S.A == 0) return;
-    hipLaunchKernelGGL(k_settle_funded, dim3(cdiv((uint32_t)S.A, 256)), dim3(256), 0, st, S, io);
+    hipLaunchKernelGGL(k_settle_funded, dim3(std::max<uint32_t>(1, cdiv((uint32_t)S.A, 256))), dim3(256), 0, st, S, io);
 }
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
     (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);

@@ -341,14 +341,16 @@ __global__ void __launch_bounds__(256) k_lseg(DevState S) {
         S.lgap[lgap_cap(S) - 1 - y] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
     }
 }
-__global__ void __launch_bounds__(256) k_lseg_gaps(DevState S) {
+// (run by k_lchains' blocks past its own, blk of nblk: k_lchains does not read lseg -- k_ldetect's
+// find_chain is the first reader -- and a launch of its own was ~5 us of a small epoch)
+KDEV void lseg_gaps(const DevState& S, uint32_t blk, uint32_t nblk) {
     const unsigned long long c = __hip_atomic_load(lc(S, LC_GAPS), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t ng = (uint32_t)c, nh = (uint32_t)(c >> 32);
     for (uint32_t y = 0; y < nh; ++y) {   // the huge gaps: a slice of each per workgroup
         const uint4 g = S.lgap[lgap_cap(S) - 1 - y];
-        for (uint32_t a = g.x + blockIdx.x * blockDim.x + threadIdx.x; a <= g.y; a += gridDim.x * blockDim.x) S.lseg[a] = g.z;
+        for (uint32_t a = g.x + blk * blockDim.x + threadIdx.x; a <= g.y; a += nblk * blockDim.x) S.lseg[a] = g.z;
     }
-    for (uint32_t x = blockIdx.x; x < ng; x += gridDim.x) {
+    for (uint32_t x = blk; x < ng; x += nblk) {
         const uint4 g = S.lgap[x];
         for (uint32_t a = g.x + threadIdx.x; a <= g.y; a += blockDim.x) S.lseg[a] = g.z;
     }
@@ -361,12 +363,13 @@ __global__ void __launch_bounds__(256) k_lseg_gaps(DevState S) {
 // chain's name); an op's value write is kept at the op's sorted position.  The account's balance
 // delta: a segmented sum over the wavefront's lanes (the ops are sorted by account), one atomic per
 // account run.
-__global__ void __launch_bounds__(256) k_lchains(DevState S) {
+__global__ void __launch_bounds__(256) k_lchains(DevState S, uint32_t nb) {
+    if (blockIdx.x >= nb) { lseg_gaps(S, blockIdx.x - nb, gridDim.x - nb); return; }   // (the blocks past nb)
     const uint32_t no = lops(S);
     if (lskip(S) || no == 0) return;
     const KG uint32_t* K = skeys(S);
     const int lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < no; base += gridDim.x * blockDim.x) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < no; base += nb * blockDim.x) {
         const uint32_t j = base + threadIdx.x;
         int64_t aid = -1, cd = 0;
         bool head = false;
@@ -657,9 +660,9 @@ __global__ void __launch_bounds__(256) k_lvw_check(DevState S) {
         if (v < 0 || (int64_t)S.lvk[v].z != w.x || (int64_t)S.lvk[v].w != w.y) { lfallback(S); return; }
     }
 }
-// Account records (createBalance / transfer, KP:131-146): outcomes fixed by k_ledger_funded.
-__global__ void __launch_bounds__(256) k_lacct(DevState S, EpochIO io) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// Account records (createBalance / transfer, KP:131-146): outcomes fixed by k_ledger_funded.  (Run by
+// k_lcommit's blocks past its own: Balances here, Positions there.)
+KDEV void lacct(const DevState& S, const EpochIO& io, uint32_t i) {
     if (i >= io.n || lskip(S) || lfell(S) || S.ctr[ci(C_ACCT_OPS)] == 0) return;
     const int32_t a = io.action[i];
     if (io.out_action[i] != a) return;
@@ -685,10 +688,11 @@ KDEV bool chain_final(const DevState& S, const KG LChain& c, int64_t& fa, int64_
     return fp;
 }
 }  // namespace
-__global__ void __launch_bounds__(256) k_lcommit(DevState S) {
+__global__ void __launch_bounds__(256) k_lcommit(DevState S, EpochIO io, uint32_t nb) {
+    if (blockIdx.x >= nb) { lacct(S, io, (blockIdx.x - nb) * blockDim.x + threadIdx.x); return; }
     if (lskip(S) || lops(S) == 0 || lfell(S)) return;
     const uint32_t no = lops(S);
-    const uint32_t stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = nb * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
     // the winning value write of each key no chain reads
     for (uint32_t p = t0; p < no; p += stride) {
         const uint32_t meta = S.lvw_meta[p];
@@ -849,7 +853,6 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.ctr = S.ctr;
     launch_radix(R, st);
     hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_lseg_gaps, dim3(std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024)), dim3(256), 0, st, S);
     // grid of k_lchains / k_linsert: more blocks (their work per thread is a chain of dependent loads:
     // more threads in flight hide it; 8,192 -> 32,768 blocks: k_lchains 0.52 -> 0.42 ms).
     // KME_LEDGER_GRID: A/B runs.
@@ -863,13 +866,13 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
         return v ? (uint32_t)std::max(64, std::atoi(v)) : 8192u;
     }();
     const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), grid_s), gl = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
-    hipLaunchKernelGGL(k_lchains, dim3(gl), dim3(256), 0, st, S);
+    const uint32_t ngap = std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024);   // (k_lseg's gaps)
+    hipLaunchKernelGGL(k_lchains, dim3(gl + ngap), dim3(256), 0, st, S, gl);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lr_rounds, dim3(1), dim3(1024), 0, st, S);
     hipLaunchKernelGGL(k_lvw_classify, dim3(gs), dim3(256), 0, st, S);
     hipLaunchKernelGGL(k_lvw_check, dim3(gs), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(k_lacct, dim3(cdiv(n, 256)), dim3(256), 0, st, S, io);
-    hipLaunchKernelGGL(k_lcommit, dim3(gs), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(k_lcommit, dim3(gs + cdiv(n, 256)), dim3(256), 0, st, S, io, gs);   // (+ the account records)
     hipLaunchKernelGGL(k_linsert, dim3(gl), dim3(256), 0, st, S, io);
     const int all = (uint64_t)S.A <= 4ull * n ? 1 : 0;
     hipLaunchKernelGGL(k_lbalances, dim3(all ? cdiv((uint32_t)S.A, 256) : std::max(gs, cdiv(n, 256))), dim3(256), 0, st, S, io, all);
