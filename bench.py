@@ -410,7 +410,8 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     if args.java_defaults:
-        args.epoch, args.flags = 1 << 16, "exact_ledger,serial_fallback"
+        # GpuMatchingEngine()'s configuration and schedule: two epochs in flight (its two slots)
+        args.epoch, args.flags, args.pipeline = 1 << 16, "exact_ledger,serial_fallback", True
     E = args.epoch
     if args.host_path_epochs < 0:
         args.host_path_epochs = max(3, (1 << 24) // E)
@@ -680,7 +681,8 @@ def main():
                                + (" + serial fallback" if flags & 2 else ""),
                        "parallelism": f"symbol-keyed x{world} (murmur2, Kafka's keyed partitioner)",
                        "credit_shards": shards, "flags": args.flags or "none",
-                       "engine": "GpuMatchingEngine() defaults" if args.java_defaults else "bench"},
+                       "engine": "GpuMatchingEngine() defaults" if args.java_defaults else "bench",
+                       "epochs_in_flight": 2 if pipelined else 1},
             "build_id": build_id,
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),

@@ -809,11 +809,14 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
     const uint32_t tile = blockIdx.x;
     KG unsigned long long* lb = R.lb;
     const unsigned long long st = (unsigned long long)stamp << 32;
-    __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t], st | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t + 1], st | t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the digits' totals over the sort's tiles, exclusive over the digits
+    if (pass > 0) {   // (pass 0's tiles are the unpermuted keys': their counts are tcnt's row 0 already)
+        __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t], st | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t + 1], st | t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the digits' totals over the sort's tiles, exclusive over the digits (pass 0: and the earlier
+    // tiles' counts, from the same rows)
     const KG uint32_t* tc = R.tcnt + (size_t)pass * gridDim.x * RADIX_DIGITS;
-    uint32_t T0 = 0, T1 = 0;
+    uint32_t T0 = 0, T1 = 0, P0 = 0, P1 = 0;
     for (uint32_t q0 = 0; q0 < ntiles; q0 += LB_BATCH) {
         uint2 v[LB_BATCH];
 #pragma unroll
@@ -822,14 +825,15 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
             v[b] = *reinterpret_cast<const KG uint2*>(&tc[(size_t)q * RADIX_DIGITS + 2 * t]);
         }
 #pragma unroll
-        for (int b = 0; b < LB_BATCH; ++b)
+        for (int b = 0; b < LB_BATCH; ++b) {
             if (q0 + b < ntiles) { T0 += v[b].x; T1 += v[b].y; }
+            if (pass == 0 && q0 + b < tile) { P0 += v[b].x; P1 += v[b].y; }
+        }
     }
     uint32_t tot;
     const uint32_t gx = block_excl_scan_256(T0 + T1, wsum, tot);
     // the earlier tiles' counts (their words carry this launch's stamp once written)
-    uint32_t P0 = 0, P1 = 0;
-    for (uint32_t q0 = 0; q0 < tile; q0 += LB_BATCH) {
+    for (uint32_t q0 = 0; pass > 0 && q0 < tile; q0 += LB_BATCH) {
         unsigned long long w[2 * LB_BATCH];
         uint32_t spins = 0;
         for (;;) {
