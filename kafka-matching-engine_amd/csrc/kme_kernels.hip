@@ -3994,8 +3994,16 @@ __global__ void __launch_bounds__(64) k_serial(const DevState* __restrict__ Sp, 
 // KME_FLAG_SERIAL_FALLBACK, after an epoch k_serial took, they restart from the exact ledger
 // (balance = the tightest lower bound; an account exists from the epoch's end).
 KDEV void tsh_fold(const DevState& S);
-__global__ void __launch_bounds__(256) k_settle_funded(DevState S, EpochIO io) {
+KDEV void table_final(const DevState& S, const EpochIO& io, uint32_t t0, uint32_t stride);
+// nb: the account blocks; the blocks past them (KME_FLAG_SERIAL_FALLBACK engines) finalise the oid-table
+// entries of an epoch k_serial took (was k_table, a launch per epoch that mostly found nothing to do)
+__global__ void __launch_bounds__(256) k_settle_funded(DevState S, EpochIO io, uint32_t nb) {
     static_assert(TSHARDS == 256, "tsh_fold: one thread per shard line");
+    if (blockIdx.x >= nb) {
+        if (S.ctr[ci(C_FALLBACK)])
+            table_final(S, io, (blockIdx.x - nb) * blockDim.x + threadIdx.x, (gridDim.x - nb) * blockDim.x);
+        return;
+    }
     if (blockIdx.x == 0) tsh_fold(S);   // the trade shards' counters (was k_tsh_fold, a launch of its own)
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= S.A) return;
@@ -4195,9 +4203,8 @@ KDEV void tsh_fold(const DevState& S) {
 // Each BUY/SELL's pending entry (k_emap) becomes its rest slot, or OT_DEAD if it did not rest: one
 // plain store at the recorded position, no probe.  An order that rested and left the book later in
 // the epoch keeps a stale slot entry, dropped by validation like every lazily deleted one.
-__global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io, int funded) {
-    if (funded && !S.ctr[ci(C_FALLBACK)]) return;   // k_unsort did it (FUNDED epochs matched in parallel)
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += gridDim.x * blockDim.x) {
+KDEV void table_final(const DevState& S, const EpochIO& io, uint32_t t0, uint32_t stride) {
+    for (uint32_t i = t0; i < io.n; i += stride) {
         const int32_t a = io.action[i];
         if (a != BUY && a != SELL) continue;
         const uint32_t h = S.epos[i];
@@ -4205,6 +4212,9 @@ __global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io, int funde
         const int32_t s = S.rest_slot[i];
         S.otab[h] = hentry(oid_fp(io.oid[i]), s >= 0 ? (uint32_t)s : OT_DEAD);
     }
+}
+__global__ void __launch_bounds__(256) k_table(DevState S, EpochIO io) {
+    table_final(S, io, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 // Rebuild: every live node of the pool's used prefix gets an entry.
 __global__ void __launch_bounds__(256) k_otab_refill(DevState S, uint32_t nslots) {
@@ -4435,9 +4445,9 @@ void launch_compact(const DevState& S, const EpochIO& io, hipStream_t st) {
 }
 void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (io.n == 0) return;
-    const int funded = S.mode == KME_MODE_FUNDED;
-    if (funded && !S.fallback) return;   // only a serial (fallback) epoch needs it after k_unsort
-    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io, funded);   // one thread per record, as k_unsort
+    // FUNDED: k_unsort finalised the entries, and after an epoch k_serial took k_settle_funded does
+    if (S.mode == KME_MODE_FUNDED) return;
+    hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);   // one thread per record, as k_unsort
 }
 void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
     hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);
@@ -4446,7 +4456,9 @@ void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st,
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev, only_fallback);
 }
 void launch_settle_funded(const DevState& S, const EpochIO& io, hipStream_t st) {
-    hipLaunchKernelGGL(k_settle_funded, dim3(std::max<uint32_t>(1, cdiv((uint32_t)S.A, 256))), dim3(256), 0, st, S, io);
+    const uint32_t nb = std::max<uint32_t>(1, cdiv((uint32_t)S.A, 256));
+    const uint32_t nt = S.fallback && io.n > 0 ? cdiv(io.n, 256) : 0;   // (k_table's work, fallback engines)
+    hipLaunchKernelGGL(k_settle_funded, dim3(nb + nt), dim3(256), 0, st, S, io, nb);
 }
 void launch_otab_rebuild(const DevState& S, uint32_t used_slots, hipStream_t st) {
     (void)hipMemsetAsync(S.otab, 0, sizeof(uint64_t) * ((size_t)S.otab_mask + 1), st);
