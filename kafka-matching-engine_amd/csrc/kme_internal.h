@@ -13,8 +13,6 @@
 namespace kme {
 
 hipStream_t engine_stream(kme_engine* e);
-// kme_submit_epoch_host's worker idle (every other engine call waits for it); a failed enqueue's status
-kme_status host_drain(kme_engine* e);
 int engine_device(kme_engine* e);
 const kme_config& engine_config(kme_engine* e);
 // (bound, demand) per account into dev_out[0, 2A), after everything queued on the engine stream

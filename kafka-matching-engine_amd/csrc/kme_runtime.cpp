@@ -14,13 +14,10 @@
 
 #include <algorithm>
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "kme.h"
@@ -55,19 +52,6 @@ bool test_hook_fail(const char* what) {
 struct kme_engine {
     kme_config cfg{};
     int device = 0;
-    // kme_submit_epoch_host's enqueue (its copies and kernel launches, ~0.15 ms of host time per
-    // 65,536-record epoch) runs on a worker thread and the caller returns at once; every other call
-    // first waits for the worker to be idle (host_drain), so the engine is single-threaded as before
-    // for a caller that makes its calls from one thread (KProcessor's stream thread)
-    std::thread hworker;
-    std::mutex hmu;
-    std::condition_variable hcv;
-    bool hjob = false;                    // a host epoch waiting for, or in, the worker
-    bool hstop = false;
-    kme_status herr = KME_OK;             // the worker's enqueue failed (reported by the next call)
-    kme_orders hj_in{};
-    uint32_t hj_n = 0;
-    kme_epoch_result hj_out{};
     hipStream_t own_stream = nullptr;
     hipStream_t lane_stream = nullptr;   // k_match_lanes runs here, beside k_match (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -581,9 +565,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     return KME_OK;
 }
 
-static void host_worker_stop(kme_engine* e);
 kme_status kme_destroy(kme_engine* e) {
-    if (e) host_worker_stop(e);   // (its last enqueue lands first)
     if (!e) return KME_E_INVALID;
     (void)hipSetDevice(e->device);
     // every queued copy and kernel of the engine finishes before its memory goes
@@ -616,15 +598,11 @@ kme_status kme_destroy(kme_engine* e) {
 
 kme_status kme_set_stream(kme_engine* e, void* s) {
     if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
-    if (!e) return KME_E_INVALID;
     e->stream = s ? reinterpret_cast<hipStream_t>(s) : e->own_stream;
     return KME_OK;
 }
 
 kme_status kme_enable_timing(kme_engine* e, int enable) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e) return KME_E_INVALID;
     e->timing = enable == KME_TIMING_MATCH ? KME_TIMING_MATCH : enable != 0 ? KME_TIMING_ALL : 0;
     return KME_OK;
@@ -755,8 +733,6 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
 }
 
 kme_status kme_submit_epoch_device(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !in) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
     return submit(e, in, n, out);
@@ -856,11 +832,6 @@ static kme_status ledger_reserve(kme_engine* e, uint64_t bal_used, uint64_t pos_
 
 kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
     if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) {   // the worker's enqueue of the last host epoch failed
-        if (st) { *st = kme_epoch_status{}; st->status = _r; st->error_index = -1; }
-        return _r;
-    }
-    if (!e) return KME_E_INVALID;
     kme_epoch_status s{};
     s.error_index = -1;
     if (e->inflight == 0) {
@@ -956,8 +927,6 @@ kme_status kme_wait(kme_engine* e, kme_epoch_status* st) {
 }
 
 kme_status kme_poll(kme_engine* e, int* done) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !done) return KME_E_INVALID;
     if (e->inflight == 0) { *done = 1; return KME_OK; }
     const int slot = (int)((e->sub_count - (uint32_t)e->inflight) & 1);   // the older epoch in flight
@@ -972,8 +941,6 @@ kme_status kme_poll(kme_engine* e, int* done) {
 // same range, and refuses a range that shares a page with a different one (KME_E_INVALID; callers
 // allocate page-aligned buffers -- the JNI glue allocates the processor's buffers itself).
 kme_status kme_host_register(kme_engine* e, void* host, size_t bytes) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !host || !bytes) return KME_E_INVALID;
     const uintptr_t p = (uintptr_t)host, pg = 4096;
     const uintptr_t lo = p & ~(pg - 1), hi = (p + bytes + pg - 1) & ~(pg - 1);
@@ -996,8 +963,6 @@ kme_status kme_host_register(kme_engine* e, void* host, size_t bytes) {
 }
 
 kme_status kme_host_unregister(kme_engine* e, void* host) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !host) return KME_E_INVALID;
     if (e->inflight) return KME_E_INVALID;
     for (size_t k = 0; k < e->host_regs.size(); ++k) {
@@ -1034,78 +999,7 @@ static kme_status host_slots(kme_engine* e) {
     return KME_OK;
 }
 
-// The worker's enqueue of one host epoch (the caller validated it and made it the engine's only
-// pending job); defined below.
-static kme_status host_enqueue(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out);
-}  // extern "C"
-namespace kme {
-// Every engine call but kme_submit_epoch_host waits here for the worker to be idle; a failed enqueue
-// is reported once (and leaves the engine failed: its epoch never reached the device).
-kme_status host_drain(kme_engine* e) {
-    if (!e->hworker.joinable()) return KME_OK;
-    std::unique_lock<std::mutex> lk(e->hmu);
-    e->hcv.wait(lk, [&] { return !e->hjob; });
-    const kme_status r = e->herr;
-    e->herr = KME_OK;
-    return r;
-}
-}  // namespace kme
-extern "C" {
-static void host_worker(kme_engine* e) {
-    (void)hipSetDevice(e->device);
-    std::unique_lock<std::mutex> lk(e->hmu);
-    for (;;) {
-        e->hcv.wait(lk, [&] { return e->hstop || e->hjob; });
-        if (!e->hjob) return;
-        lk.unlock();
-        const kme_status r = host_enqueue(e, &e->hj_in, e->hj_n, &e->hj_out);
-        lk.lock();
-        if (r != KME_OK) {
-            e->herr = r;
-            if (!e->failed) { e->failed = 1; e->fail_status = r; e->fail_detail = KME_D_NONE; }
-        }
-        e->hjob = false;
-        e->hcv.notify_all();
-    }
-}
-static void host_worker_stop(kme_engine* e) {
-    if (!e->hworker.joinable()) return;
-    {
-        std::unique_lock<std::mutex> lk(e->hmu);
-        e->hcv.wait(lk, [&] { return !e->hjob; });
-        e->hstop = true;
-    }
-    e->hcv.notify_all();
-    e->hworker.join();
-}
-
 kme_status kme_submit_epoch_host(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
-    if (!e || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
-        !out->trades)
-        return KME_E_INVALID;
-    if (kme_status r = kme::host_drain(e)) return r;   // (at most one epoch waits for the worker)
-    if (out->trades_cap < e->cfg.max_trades) return KME_E_INVALID;
-    if (e->failed) return KME_E_FAILED;
-    if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
-    if (e->inflight == 2) return KME_E_INVALID;
-    static const bool sync = [] {   // (KME_HOST_SYNC=1: enqueue on the caller's thread -- A/B runs)
-        const char* v = std::getenv("KME_HOST_SYNC");
-        return v && std::atoi(v);
-    }();
-    if (sync) return host_enqueue(e, in, n, out);
-    if (!e->hworker.joinable()) e->hworker = std::thread(host_worker, e);
-    {
-        std::lock_guard<std::mutex> g(e->hmu);
-        e->hj_in = *in;
-        e->hj_n = n;
-        e->hj_out = *out;
-        e->hjob = true;
-    }
-    e->hcv.notify_all();
-    return KME_OK;
-}
-
-static kme_status host_enqueue(kme_engine* e, const kme_orders* in, uint32_t n, const kme_epoch_result* out) {
     if (!e || !in || !out || !out->out_action || !out->out_size || !out->out_prev || !out->out_flags || !out->trade_off ||
         !out->trades)
         return KME_E_INVALID;
@@ -1244,8 +1138,6 @@ kme_status kme_comm_unique_id(void* id128) {
 }
 
 kme_status kme_comm_init(kme_engine* e, uint32_t n_ranks, uint32_t rank, const void* id128, kme_comm** out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !id128 || !out || n_ranks == 0 || rank >= n_ranks) return KME_E_INVALID;
     Rccl* r = rccl();
     if (!r) return KME_E_UNSUPPORTED;
@@ -1275,8 +1167,6 @@ kme_status kme_comm_destroy(kme_comm* c) {
 
 kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t* dev_groups, uint32_t n_groups,
                                      uint32_t rows_per_rank, kme_tob* dev_all) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !c || !dev_all || n_groups > rows_per_rank || (n_groups && !dev_groups)) return KME_E_INVALID;
     Rccl* r = rccl();
     if (!r) return KME_E_UNSUPPORTED;
@@ -1291,8 +1181,6 @@ kme_status kme_market_data_allgather(kme_engine* e, kme_comm* c, const uint32_t*
 }
 
 kme_status kme_credit_state(kme_engine* e, int64_t* dev_out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !dev_out || e->cfg.mode != KME_MODE_FUNDED) return KME_E_INVALID;
     if (e->inflight) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
@@ -1305,8 +1193,6 @@ kme_status kme_credit_state(kme_engine* e, int64_t* dev_out) {
 }
 
 kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_shards, uint32_t my_shard) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !dev_all || e->cfg.mode != KME_MODE_FUNDED || n_shards == 0 || my_shard >= n_shards) return KME_E_INVALID;
     if (e->inflight) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
@@ -1323,8 +1209,6 @@ kme_status kme_credit_adjust(kme_engine* e, const int64_t* dev_all, uint32_t n_s
 // and when any status is not OK no rank adjusts: that rank returns its own status, the others
 // KME_E_INVALID ("skipped on every rank").
 kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !c || e->cfg.mode != KME_MODE_FUNDED) return KME_E_INVALID;
     Rccl* r = rccl();
     if (!r) return KME_E_UNSUPPORTED;   // (a communicator exists only where RCCL loaded: the same on every rank)
@@ -1365,14 +1249,10 @@ kme_status kme_credit_rebalance(kme_engine* e, kme_comm* c) {
 
 // ------------------------------------------------------------------ internals for kme_multi (kme_internal.h)
 namespace kme {
-hipStream_t engine_stream(kme_engine* e) {
-    (void)host_drain(e);   // (work the caller queues on the stream goes behind every submitted epoch)
-    return e->stream;
-}
+hipStream_t engine_stream(kme_engine* e) { return e->stream; }
 int engine_device(kme_engine* e) { return e->device; }
 const kme_config& engine_config(kme_engine* e) { return e->cfg; }
 kme_status credit_state_enqueue(kme_engine* e, int64_t* dev_out) {
-    if (kme_status _r = host_drain(e)) return _r;
     HIP_TRY(hipSetDevice(e->device));
     launch_credit_state(e->S, dev_out, e->stream);
     HIP_TRY(hipGetLastError());
@@ -1382,14 +1262,12 @@ kme_status credit_state_enqueue(kme_engine* e, int64_t* dev_out) {
     return KME_OK;
 }
 kme_status credit_adjust_enqueue(kme_engine* e, const int64_t* dev_all, uint32_t n, uint32_t me, size_t stride) {
-    if (kme_status _r = host_drain(e)) return _r;
     HIP_TRY(hipSetDevice(e->device));
     launch_credit_adjust(e->S, dev_all, n, me, stride, e->stream);
     HIP_TRY(hipGetLastError());
     return KME_OK;
 }
 kme_status resting_oids(kme_engine* e, std::vector<int64_t>& out) {
-    if (kme_status _r = host_drain(e)) return _r;
     if (e->inflight) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1484,8 +1362,6 @@ kme_status kme_checkpoint_inspect(const char* path, kme_checkpoint_info* out) {
 }
 
 kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, size_t app_bytes) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !path || (app_bytes && !app)) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (e->inflight) return KME_E_INVALID;   // between epochs only: kme_wait the submitted epoch first
@@ -1603,8 +1479,6 @@ kme_status kme_checkpoint_app(kme_engine* e, const char* path, const void* app, 
 kme_status kme_checkpoint(kme_engine* e, const char* path) { return kme_checkpoint_app(e, path, nullptr, 0); }
 
 kme_status kme_restore_app(kme_engine* e, const char* path, void* app, size_t app_cap, size_t* app_bytes) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !path) return KME_E_INVALID;
     if (e->failed) return KME_E_FAILED;
     if (e->inflight) return KME_E_INVALID;
@@ -1797,8 +1671,6 @@ kme_status kme_restore(kme_engine* e, const char* path) {
 }
 
 kme_status kme_ledger_stats(kme_engine* e, kme_ledger_info* out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !out) return KME_E_INVALID;
     *out = kme_ledger_info{};
     if (!e->ledger) return KME_E_UNSUPPORTED;
@@ -1816,8 +1688,6 @@ kme_status kme_ledger_stats(kme_engine* e, kme_ledger_info* out) {
 
 kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_t n, const kme_epoch_result* res_dev,
                                 void* out_dev, size_t cap, size_t* len) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !in_dev || !len) return KME_E_INVALID;
     if (n > e->cfg.max_epoch) return KME_E_CAPACITY;
     HIP_TRY(hipSetDevice(e->device));
@@ -1840,8 +1710,6 @@ kme_status kme_tape_json_device(kme_engine* e, const kme_orders* in_dev, uint32_
 }
 
 kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !out) return KME_E_INVALID;
     const size_t cap = (size_t)e->cfg.max_symbols * KME_DBG_WORDS;
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1850,8 +1718,6 @@ kme_status kme_debug_counters(kme_engine* e, uint64_t* out, size_t n) {
 }
 
 kme_status kme_device_results(kme_engine* e, kme_epoch_result* r) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !r) return KME_E_INVALID;
     r->out_action = e->d_out_action; r->out_size = e->d_out_size; r->out_prev = e->d_out_prev;
     r->out_flags = e->d_out_flags; r->trade_off = e->d_trade_off;
@@ -1861,8 +1727,6 @@ kme_status kme_device_results(kme_engine* e, kme_epoch_result* r) {
 }
 
 kme_status kme_phase_times(kme_engine* e, float* ms, int* n) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !ms || !n) return KME_E_INVALID;
     for (int p = 0; p < PH_N; ++p) ms[p] = e->phase_ms[p];
     *n = PH_N;
@@ -1874,8 +1738,6 @@ const char* kme_phase_name(int i) { return (i >= 0 && i < PH_N) ? kPhaseNames[i]
 // records so that the reservation proof never has to reason across a CREATE/TRANSFER boundary.
 kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme_epoch_result* out,
                             kme_epoch_status* st) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (e && e->inflight) return KME_E_INVALID;   // device epochs still in flight: kme_wait them first
     if (!e || !in || !out) return KME_E_INVALID;
     HIP_TRY(hipSetDevice(e->device));
@@ -1978,8 +1840,6 @@ kme_status kme_submit_epoch(kme_engine* e, const kme_orders* in, uint32_t n, kme
 }
 
 kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !dev_out) return KME_E_INVALID;
     launch_tob(e->S, dev_out, e->stream);
     HIP_TRY(hipGetLastError());
@@ -1987,8 +1847,6 @@ kme_status kme_top_of_book(kme_engine* e, kme_tob* dev_out) {
 }
 
 kme_status kme_top_of_book_groups(kme_engine* e, const uint32_t* dev_groups, uint32_t n, kme_tob* dev_out) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || (n && (!dev_groups || !dev_out))) return KME_E_INVALID;
     launch_tob_groups(e->S, dev_groups, n, dev_out, e->stream);
     HIP_TRY(hipGetLastError());
@@ -2005,8 +1863,6 @@ static char* dup_string(const std::string& s, size_t* len) {
 }
 
 kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !text) return KME_E_INVALID;
     if (kme_status r = snap_begin(e, "kme_snapshot_books")) return r;
     const uint32_t G = e->cfg.max_symbols + (uint32_t)e->S.Gs;   // the dense groups, then the sparse ones
@@ -2101,8 +1957,6 @@ kme_status kme_snapshot_books(kme_engine* e, char** text, size_t* len) {
 }
 
 kme_status kme_snapshot_ledger(kme_engine* e, char** text, size_t* len) {
-    if (!e) return KME_E_INVALID;
-    if (kme_status _r = kme::host_drain(e)) return _r;   // (the worker idle: kme_submit_epoch_host)
     if (!e || !text) return KME_E_INVALID;
     if (e->cfg.mode != KME_MODE_EXACT && !e->S.ledger_replay) return KME_E_UNSUPPORTED;
     if (kme_status r = snap_begin(e, "kme_snapshot_ledger")) return r;
