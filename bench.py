@@ -416,6 +416,13 @@ def main():
     if args.host_path_epochs < 0:
         args.host_path_epochs = max(3, (1 << 24) // E)
     host_epochs = args.host_path_epochs if world == 1 else 0
+    if os.environ.get("KME_LIB") and host_epochs:
+        # integration/libkme_host_harness.so is linked against the tree's libkme.so: with another build
+        # loaded as the engine (KME_LIB, A/B runs) it would drive that engine through a library of
+        # another kme_engine layout -- a device fault, not a measurement.  No host path then.
+        print("bench.py: KME_LIB set: no host-path / router measurement (the harness links the tree's libkme.so)",
+              file=sys.stderr, flush=True)
+        host_epochs = 0
     # + 1: the phase-breakdown epoch; then the host-path epochs
     # (+ 1 with --checkpoint: the epoch between its two commits)
     total = max(args.orders, (args.warmup + args.steps + 1 + host_epochs + (1 if args.checkpoint else 0)) * E)
