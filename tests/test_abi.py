@@ -319,3 +319,21 @@ def test_checkpoint_chunks_change_only_where_the_bytes_change(kme_mod, tmp_path)
     assert len(h2) == 8 and (h2[:5] == h1[:5]).all() and h2[5] != h1[5]
     with pytest.raises(kme_mod.KmeError):
         kme_mod.checkpoint_chunks(f, 1024)                       # below the minimum chunk
+
+
+def test_checkpoint_inspect_reads_both_trailer_formats(kme_mod, tmp_path):
+    """kme_checkpoint_inspect reads the trailer only (the commit log checks a file against it): the
+    round-6 tree digest (KMEDGST2: block digests of the file, written and verified on host threads)
+    and the older stream digest (KMEDGST1) both; anything else is refused."""
+    import struct
+
+    body = bytes(range(256)) * 40
+    for magic in (b"KMEDGST1", b"KMEDGST2"):
+        f = tmp_path / ("t" + magic.decode()[-1] + ".ckpt")
+        f.write_bytes(body + struct.pack("<QQ8s", 7, 0x1234567890ABCDEF, magic))
+        info = kme_mod.checkpoint_inspect(f)
+        assert info["file_bytes"] == len(body) + 24 and info["app_bytes"] == 7 and info["digest"] == 0x1234567890ABCDEF
+    bad = tmp_path / "bad.ckpt"
+    bad.write_bytes(body + struct.pack("<QQ8s", 7, 1, b"KMEDGSTX"))
+    with pytest.raises(kme_mod.KmeError):
+        kme_mod.checkpoint_inspect(bad)
