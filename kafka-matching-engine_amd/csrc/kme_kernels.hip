@@ -802,17 +802,15 @@ __global__ void __launch_bounds__(256) k_radix_tcnt(RadixIO R) {
 // every earlier tile (all resident: a small sort is a few dozen tiles, and an earlier tile never
 // waits for a later one).  t0 / t1: this tile's counts of digits 2t, 2t + 1; returns their offsets.
 KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
-constexpr int LB_BATCH = 16;
+constexpr int LB_BATCH = 32;   // (tiles read per round trip)
 KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t ntiles, uint32_t t0, uint32_t t1,
                            uint32_t* wsum, uint32_t& g0, uint32_t& g1) {
     const int t = threadIdx.x;
     const uint32_t tile = blockIdx.x;
-    KG unsigned long long* lb = R.lb;
+    KG unsigned long long* lb = R.lb;   // per tile 256 words: thread t's two digit counts (12 bits each) | stamp << 32
     const unsigned long long st = (unsigned long long)stamp << 32;
-    if (pass > 0) {   // (pass 0's tiles are the unpermuted keys': their counts are tcnt's row 0 already)
-        __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t], st | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&lb[(size_t)tile * RADIX_DIGITS + 2 * t + 1], st | t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (pass > 0)   // (pass 0's tiles are the unpermuted keys': their counts are tcnt's row 0 already)
+        __hip_atomic_store(&lb[(size_t)tile * 256 + t], st | (t1 << 16) | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the digits' totals over the sort's tiles, exclusive over the digits (pass 0: and the earlier
     // tiles' counts, from the same rows)
     const KG uint32_t* tc = R.tcnt + (size_t)pass * gridDim.x * RADIX_DIGITS;
@@ -834,19 +832,17 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
     const uint32_t gx = block_excl_scan_256(T0 + T1, wsum, tot);
     // the earlier tiles' counts (their words carry this launch's stamp once written)
     for (uint32_t q0 = 0; pass > 0 && q0 < tile; q0 += LB_BATCH) {
-        unsigned long long w[2 * LB_BATCH];
+        unsigned long long w[LB_BATCH];
         uint32_t spins = 0;
         for (;;) {
             bool all = true;
 #pragma unroll
             for (int b = 0; b < LB_BATCH; ++b) {
                 const uint32_t q = q0 + b < tile ? q0 + b : 0;
-                w[2 * b] = __hip_atomic_load(&lb[(size_t)q * RADIX_DIGITS + 2 * t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                w[2 * b + 1] = __hip_atomic_load(&lb[(size_t)q * RADIX_DIGITS + 2 * t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w[b] = __hip_atomic_load(&lb[(size_t)q * 256 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
 #pragma unroll
-            for (int b = 0; b < LB_BATCH; ++b)
-                all = all && (q0 + b >= tile || ((w[2 * b] >> 32) == stamp && (w[2 * b + 1] >> 32) == stamp));
+            for (int b = 0; b < LB_BATCH; ++b) all = all && (q0 + b >= tile || (uint32_t)(w[b] >> 32) == stamp);
             if (all) break;
             if (++spins == (1u << 24)) {   // (cannot happen: an earlier tile never waits for this one)
                 printf("kme: radix look-back: tile %u waits for tiles %u.. (stamp %u)\n", tile, q0, stamp);
@@ -857,7 +853,7 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
         }
 #pragma unroll
         for (int b = 0; b < LB_BATCH; ++b)
-            if (q0 + b < tile) { P0 += (uint32_t)w[2 * b]; P1 += (uint32_t)w[2 * b + 1]; }
+            if (q0 + b < tile) { P0 += (uint32_t)w[b] & 0xFFFFu; P1 += (uint32_t)(w[b] >> 16) & 0xFFFFu; }
     }
     g0 = gx + P0;
     g1 = gx + T0 + P1;
@@ -867,6 +863,7 @@ template <int TILE, bool LB = false>
 __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int src, uint32_t stamp = 0) {
     static_assert(RADIX_DIGITS == 512, "two digits per thread");
     static_assert(TILE % 256 == 0, "whole rounds");
+    static_assert(TILE < 65536, "a tile's digit count fits a look-back word's 16 bits");
     __shared__ uint32_t wh[4][RADIX_DIGITS];     // wavefront w's count of digit d, then its first local slot
     __shared__ uint32_t gdelta[RADIX_DIGITS];    // digit d's global offset minus its local start
     __shared__ uint32_t lkey[TILE], lval[TILE];
