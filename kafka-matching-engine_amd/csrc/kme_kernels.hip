@@ -4324,13 +4324,19 @@ void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, 
 }
 // Exclusive scan of in[0, L) into out (in place allowed): tile sums, then the tiles (sums scratch:
 // cdiv(L, LB_TILE) words).
+// A look-back launch's stamp: one per launch, any engine or thread, never 0 (look-back words of older
+// launches, and zeroed memory, never match)
+uint32_t next_stamp() {
+    static std::atomic<uint32_t> stamps{1};
+    uint32_t s = stamps.fetch_add(1);
+    if (s == 0) s = stamps.fetch_add(1);
+    return s;
+}
 static void launch_scan2(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, int write_end,
                          hipStream_t st, unsigned long long* ctr) {
     const uint32_t nb = cdiv(L > 0 ? L : 1, LB_TILE);
     if (nb <= LB_MAX_TILES && ((uintptr_t)sums & 7) == 0) {   // a small scan: one launch (look-back)
-        static std::atomic<uint32_t> stamps{1};
-        uint32_t stamp = stamps.fetch_add(1);
-        if (stamp == 0) stamp = stamps.fetch_add(1);
+        const uint32_t stamp = next_stamp();
         hipLaunchKernelGGL(k_scan_tiles<true>, dim3(nb), dim3(256), 0, st, in, out, L, (const uint32_t*)sums, total, write_end, stamp,
                            ctr);
         return;
@@ -4348,12 +4354,9 @@ static void radix_passes(const RadixIO& R, hipStream_t st) {
     if (R.tcnt && R.lb && R.passes <= RADIX_MAXP && TILE == RADIX_TILE_SMALL) {
         // a small sort: the per-tile counts of every pass in one launch, then one launch per pass
         // (look-back offsets) instead of three (histogram, two scan kernels) before each scatter
-        static std::atomic<uint32_t> stamps{1};   // (one per scatter launch, any engine or thread: look-back
-                                                  // words of older launches never match)
         hipLaunchKernelGGL(k_radix_tcnt<TILE>, dim3(ntiles), dim3(256), 0, st, R);
         for (int pass = 0; pass < R.passes; ++pass) {
-            uint32_t stamp = stamps.fetch_add(1);
-            if (stamp == 0) stamp = stamps.fetch_add(1);
+            const uint32_t stamp = next_stamp();
             hipLaunchKernelGGL((k_radix_scatter<TILE, true>), dim3(ntiles), dim3(256), 0, st, R, pass, src, stamp);
             src ^= 1;
         }

@@ -48,6 +48,7 @@ struct RadixIO {
 };
 constexpr int RADIX_MAXP = 4;        // passes of a look-back sort (tcnt's rows)
 void launch_radix(const RadixIO& R, hipStream_t st);
+uint32_t next_stamp();               // a look-back launch's stamp (unique, never 0)
 void launch_excl_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* sums, uint32_t* total, hipStream_t st,
                       unsigned long long* ctr);
 // FUNDED + exact ledger: the epoch's ledger effects in parallel (kme_ledger.hip); the serial replay
