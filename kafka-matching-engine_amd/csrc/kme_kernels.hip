@@ -4032,9 +4032,7 @@ __global__ void __launch_bounds__(256) k_settle_funded(DevState S, EpochIO io, u
 // per trade in executeTrade order (KP:265-287), postRemoveAdjustments (KP:325-333) for each
 // accepted cancel -- all on the exact Balances / Positions tables of EXACT mode (Core), so the
 // value-keyed position writes (KP:434-436) clobber exactly what the reference clobbers.
-__global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop) {
-    const DevState& S = *Sp;
-    const EpochIO& io = *iop;
+KDEV void ledger_replay(const DevState& S, const EpochIO& io) {
     if (failed(S.ctr) || S.ctr[ci(C_FALLBACK)]) return;   // a serial epoch kept the exact ledger itself
     if (S.lpar && S.lctr[ci(LC_FALLBACK)] == 0) return;     // kme_ledger.hip applied it in parallel
     if (lane_id() == 0) S.ctr[ci(C_LSERIAL)] = 1;
@@ -4081,6 +4079,18 @@ __global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict
             }
         }
     }
+}
+// ctr_out (the epoch slot's pinned host copy of the counters, through its device mapping; set when
+// this is the epoch's last launch): the counters block copied there after the replay -- the
+// D2H copy that was a launch of its own after every epoch
+__global__ void __launch_bounds__(64) k_ledger_replay(const DevState* __restrict__ Sp, const EpochIO* __restrict__ iop,
+                                                      unsigned long long* ctr_out) {
+    const DevState& S = *Sp;
+    ledger_replay(S, *iop);
+    if (!ctr_out) return;
+    __syncthreads();   // (one wavefront: its own counter writes before the reads)
+    for (int k = threadIdx.x; k < C_NCTR * CTR_STRIDE; k += 64)
+        ctr_out[k] = __hip_atomic_load(&S.ctr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ (3') OUT echo to input order
@@ -4449,8 +4459,8 @@ void launch_table(const DevState& S, const EpochIO& io, hipStream_t st) {
     if (S.mode == KME_MODE_FUNDED) return;
     hipLaunchKernelGGL(k_table, dim3(cdiv(io.n, 256)), dim3(256), 0, st, S, io);   // one thread per record, as k_unsort
 }
-void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st) {
-    hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev);
+void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, unsigned long long* ctr_out) {
+    hipLaunchKernelGGL(k_ledger_replay, dim3(1), dim3(64), 0, st, S_dev, io_dev, ctr_out);
 }
 void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, int only_fallback) {
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, st, S_dev, io_dev, only_fallback);

@@ -79,7 +79,8 @@ void launch_serial(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st,
 // FUNDED + KME_FLAG_SERIAL_FALLBACK: funded bounds from the exact ledger after a serial epoch
 void launch_settle_funded(const DevState& S, const EpochIO& io, hipStream_t st);
 // FUNDED + KME_FLAG_EXACT_LEDGER: the epoch's ledger effects in arrival order (after compaction)
-void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st);
+// ctr_out: when the replay is the epoch's last launch, the counters' pinned host copy (device view)
+void launch_ledger_replay(const DevState* S_dev, const EpochIO* io_dev, hipStream_t st, unsigned long long* ctr_out = nullptr);
 // exclusive scan of L u32 values (DPP wave scans): out[k] = sum(in[0..k)); bsum needs
 // L / 2048 + 1 words of scratch, *total receives the sum
 void launch_scan(const uint32_t* in, uint32_t* out, uint32_t L, uint32_t* bsum, uint32_t* total, hipStream_t st);

@@ -78,6 +78,7 @@ struct kme_engine {
     uint32_t *d_ntrades = nullptr, *d_trade_off = nullptr;
     TradeRec* d_trades = nullptr;
     unsigned long long* h_ctr = nullptr;  // pinned copies of the counters block: one per epoch slot
+    unsigned long long* d_hctr = nullptr; // h_ctr's device mapping (k_ledger_replay's copy)
                                           // (two epochs may be in flight), a third for the rebuild
     // device serializer scratch: per-input byte counts, offsets, scan partials, u64 total
     uint32_t *d_ser_len = nullptr, *d_ser_off = nullptr, *d_ser_tmp = nullptr;
@@ -539,6 +540,7 @@ kme_status kme_create(const kme_config* cfg, kme_engine** out) {
     ALLOC(e->d_io, 1);
     HIP_TRY(hipHostMalloc((void**)&e->h_ser_total, sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&e->h_ctr, 3 * (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_TRY(hipHostGetDevicePointer((void**)&e->d_hctr, e->h_ctr, 0));
 
     // initial store contents: every group absent, empty tables
     hipStream_t st = e->stream;
@@ -709,7 +711,9 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
                 e->S.lvk_tag = e->lvk_next_tag++;
                 launch_ledger_parallel(S, io, e->cfg.max_trades, st);
             }
-            launch_ledger_replay(e->d_S, e->d_io, st);   // (works only when the parallel pass fell back)
+            // (works only when the parallel pass fell back; the epoch's last launch: it also copies
+            // the counters to the slot's host copy)
+            launch_ledger_replay(e->d_S, e->d_io, st, e->d_hctr + slot * (size_t)C_NCTR * CTR_STRIDE);
             phase_end(e, PH_REPLAY);
         }
     } else {
@@ -723,7 +727,8 @@ static kme_status submit(kme_engine* e, const kme_orders* in, uint32_t n, const 
     launch_table(S, io, st);
     phase_end(e, PH_TABLE);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->h_ctr + slot * (size_t)C_NCTR * CTR_STRIDE, S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    if (!(funded && S.ledger_replay))   // (otherwise k_ledger_replay, the last launch, copied them)
+        HIP_TRY(hipMemcpyAsync(e->h_ctr + slot * (size_t)C_NCTR * CTR_STRIDE, S.ctr, (size_t)C_NCTR * CTR_STRIDE * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(e->ev_end[slot], st));
     e->seq_base += n;
     e->fl_n[slot] = n;
