@@ -326,19 +326,19 @@ constexpr uint32_t LSEG_HUGE = 1u << 16;
 KDEV uint32_t lgap_cap(const DevState& S) { return (uint32_t)S.A / 256 + (uint32_t)S.A / 4096 + 8; }   // (its allocation)
 __global__ void __launch_bounds__(256) k_lseg(DevState S) {
     const uint32_t n = lops(S);
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > n) return;
     const KG uint32_t* K = skeys(S);
-    const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
-    const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
-    if (cur - prev <= (int64_t)LSEG_RUN) {
-        for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
-    } else if (cur - prev <= (int64_t)LSEG_HUGE) {
-        const uint32_t x = (uint32_t)atomicAdd(lc(S, LC_GAPS), 1ull);   // < (A + 1) / LSEG_RUN + 1
-        S.lgap[x] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
-    } else {
-        const uint32_t y = (uint32_t)(atomicAdd(lc(S, LC_GAPS), 1ull << 32) >> 32);   // < (A + 1) / LSEG_HUGE + 1
-        S.lgap[lgap_cap(S) - 1 - y] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= n; k += gridDim.x * blockDim.x) {
+        const int64_t prev = k == 0 ? -1 : (int64_t)(K[k - 1] >> S.lhbits);
+        const int64_t cur = k == n ? (int64_t)S.A : (int64_t)(K[k] >> S.lhbits);
+        if (cur - prev <= (int64_t)LSEG_RUN) {
+            for (int64_t a = prev + 1; a <= cur; ++a) S.lseg[a] = k;
+        } else if (cur - prev <= (int64_t)LSEG_HUGE) {
+            const uint32_t x = (uint32_t)atomicAdd(lc(S, LC_GAPS), 1ull);   // < (A + 1) / LSEG_RUN + 1
+            S.lgap[x] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
+        } else {
+            const uint32_t y = (uint32_t)(atomicAdd(lc(S, LC_GAPS), 1ull << 32) >> 32);   // < (A + 1) / LSEG_HUGE + 1
+            S.lgap[lgap_cap(S) - 1 - y] = make_uint4((uint32_t)(prev + 1), (uint32_t)cur, k, 0);
+        }
     }
 }
 // (run by k_lchains' blocks past its own, blk of nblk: k_lchains does not read lseg -- k_ldetect's
@@ -852,7 +852,11 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     R.lb = R.small ? S.llb : nullptr;
     R.ctr = S.ctr;
     launch_radix(R, st);
-    hipLaunchKernelGGL(k_lseg, dim3(cdiv(nops + 1, 256)), dim3(256), 0, st, S);
+    // The passes over the ops are grid-stride loops sized by nops, a capacity (n + 2 max_trades); a
+    // small epoch's ops are ~2n (2^19 + n of capacity at the drop-in's defaults: ~4 of 5 blocks found
+    // nothing), so its grids are sized by the records instead.
+    const uint64_t gops = R.small ? std::min<uint64_t>(nops, std::max<uint64_t>(2ull * n, 65536)) : nops;
+    hipLaunchKernelGGL(k_lseg, dim3(cdiv(gops + 1, 256)), dim3(256), 0, st, S);
     // grid of k_lchains / k_linsert: more blocks (their work per thread is a chain of dependent loads:
     // more threads in flight hide it; 8,192 -> 32,768 blocks: k_lchains 0.52 -> 0.42 ms).
     // KME_LEDGER_GRID: A/B runs.
@@ -865,7 +869,7 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
         const char* v = std::getenv("KME_LEDGER_GRID_S");
         return v ? (uint32_t)std::max(64, std::atoi(v)) : 8192u;
     }();
-    const uint32_t gs = std::min<uint32_t>(cdiv(nops, 256), grid_s), gl = std::min<uint32_t>(cdiv(nops, 256), grid_cap);
+    const uint32_t gs = std::min<uint32_t>(cdiv(gops, 256), grid_s), gl = std::min<uint32_t>(cdiv(gops, 256), grid_cap);
     const uint32_t ngap = std::min<uint32_t>(cdiv((uint64_t)S.A + 1, LSEG_RUN) + 1, 1024);   // (k_lseg's gaps)
     hipLaunchKernelGGL(k_lchains, dim3(gl + ngap), dim3(256), 0, st, S, gl);
     hipLaunchKernelGGL(k_ldetect, dim3(gs), dim3(256), 0, st, S);
