@@ -536,6 +536,7 @@ def main():
     t0 = time.perf_counter()
     t_sub = {}
     sub_cpu = []   # the host's time inside each submit call (launches), beside the epoch's wall time
+    wait_cpu = []  # ... and blocked in each wait (~0: the host, not the device, paces the epochs)
     for j in range(args.steps):
         k = args.warmup + j
         if pipelined:
@@ -547,12 +548,16 @@ def main():
                 t_sub[k + 1] = time.perf_counter()
                 submit_epoch(k + 1)
                 sub_cpu.append(time.perf_counter() - t_sub[k + 1])
+            t_w = time.perf_counter()
             st = eng.wait()
+            wait_cpu.append(time.perf_counter() - t_w)
         else:
             t_sub[k] = time.perf_counter()
             submit_epoch(k)
             sub_cpu.append(time.perf_counter() - t_sub[k])
+            t_w = time.perf_counter()
             st = eng.wait()
+            wait_cpu.append(time.perf_counter() - t_w)
             if args.serialize:  # MatchOut text of the epoch, printed on the GPU, left in HBM
                 tape_bytes.append(eng.tape_json_device_into(epoch_ptrs(k), E, tape_buf.data_ptr(), tape_buf.numel()))
         lat.append((time.perf_counter() - t_sub[k]) * 1e3)   # submit -> results ready
@@ -694,6 +699,7 @@ def main():
             "p99_epoch_ms": float(np.percentile(lat, 99)),
             "p50_epoch_ms": float(np.percentile(lat, 50)),
             "host_submit_ms": float(np.mean(sub_cpu) * 1e3),   # the host's time in each submit (kernel launches)
+            "host_wait_ms": float(np.mean(wait_cpu) * 1e3),    # ... and blocked in each wait
             "fills_per_s": 2 * n_trades_all / elapsed,
             "trades_per_s": n_trades_all / elapsed,
             "market_data": {"symbols": int(sum(len(p) for p in per_rank)), "bytes_per_epoch": int(world * rows * 16),
