@@ -268,46 +268,95 @@ __global__ void __launch_bounds__(256) k_lcount(DevState S, EpochIO io) {
 // At the scanned offsets, in arrival order: the op (LOp: chain sid and account, arrival number, the
 // effect's size / price / side) and its sort key aid * 256 + hash8(sid).  Record i's check / cancel
 // has arrival number i + 2 trade_off[i], trade q's maker and taker fills i + 2q + 1 and i + 2q + 2
-// (executeTrade's order, KP:265-274).
+// (executeTrade's order, KP:265-274).  A wavefront takes 64 records and spreads their ops over its
+// lanes: op j of the wavefront's range is lane j mod 64's, which finds its record by a binary search
+// over the 64 records' op offsets (shuffles) -- one lane walking its record's trades kept the other 63
+// waiting, and each lane stored a run of its own (partial lines); now a wavefront's stores are
+// consecutive.
 __global__ void __launch_bounds__(256) k_lgen(DevState S, EpochIO io) {
+    if (lskip(S)) return;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= io.n || lskip(S)) return;
-    const int32_t a = io.action[i], out = io.out_action[i];
-    uint32_t o = S.lcnt[i];
-    const uint32_t t0 = io.trade_off[i];
-    auto put = [&](int64_t aid, int64_t sid, uint32_t es, int32_t size, int32_t price, uint32_t flags) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t first = i - (uint32_t)lane;               // the wavefront's first record
+    if (first >= io.n) return;                               // (uniform)
+    const bool valid = i < io.n;
+    int32_t a = -1, out = -1;
+    if (valid) { a = io.action[i]; out = io.out_action[i]; }
+    const bool bs = (a == BUY || a == SELL) && out == a, cx = a == CANCEL && out == CANCEL;
+    uint32_t t0 = 0, c = 0, o = 0;
+    int64_t aid = 0, sid = 0;
+    int32_t price = 0, size = 0;
+    if (valid) {
+        t0 = io.trade_off[i];
+        o = S.lcnt[i];
+        if (bs) {
+            c = 1 + 2 * (io.trade_off[i + 1] - t0);
+            aid = io.aid[i]; sid = io.sid[i]; price = io.price[i]; size = io.size[i];
+        } else if (cx) {
+            c = 1;
+            aid = io.aid[i];
+        }
+    }
+    const uint32_t nv = io.n - first < 64 ? io.n - first : 64;
+    const uint32_t base = (uint32_t)__shfl((int)o, 0);
+    const uint32_t end = (uint32_t)__shfl((int)(o + c), (int)nv - 1);
+    const uint32_t off = valid ? o - base : 0xFFFFFFFFu;     // non-decreasing over the lanes
+    // (every shuffle runs on all 64 lanes: a lane past the range still takes part, its op discarded --
+    // a shuffle reads nothing defined from a lane that is not active)
+    for (uint32_t j0 = 0; j0 < end - base; j0 += 64) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        int L = 0;                                           // the last record whose ops start at or before j
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t f = (uint32_t)__shfl((int)off, L + step < 64 ? L + step : 63);
+            if (L + step < 64 && f <= j) L += step;
+        }
+        const uint32_t k = j - (uint32_t)__shfl((int)off, L);
+        const uint32_t r = first + (uint32_t)L;
+        const int32_t ra = __shfl(a, L);
+        const int64_t raid = __shfl(aid, L), rsid = __shfl(sid, L);
+        const int32_t rprice = __shfl(price, L), rsize = __shfl(size, L);
+        const uint32_t rt0 = (uint32_t)__shfl((int)t0, L);
+        if (j >= end - base) continue;
+        const uint32_t es0 = r + 2 * rt0;
+        int64_t oaid, osid;
+        uint32_t es, osize, oprice, flags;
+        if (ra == CANCEL) {
+            const int4 v = S.vic[r];                         // the removed order: action << 8 | price, size, sid
+            oaid = raid;
+            osid = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
+            es = es0; osize = (uint32_t)v.y; oprice = (uint32_t)(v.x & 0xFF);
+            flags = OP_CANCEL | ((v.x >> 8) == BUY ? 1u : 0u) << 2;                                       // KP:325-333
+        } else {
+            const uint32_t buy = ra == BUY ? 1u : 0u;
+            if (k == 0) {
+                oaid = raid; osid = rsid; es = es0;
+                osize = (uint32_t)rsize; oprice = (uint32_t)rprice;
+                flags = OP_CHECK | buy << 2;                                                              // KP:167-182
+            } else {
+                const uint32_t q = rt0 + (k - 1) / 2;
+                const TradeRec tr = io.trades[q];
+                osize = (uint32_t)tr.size;
+                if (((k - 1) & 1) == 0) {
+                    oaid = tr.maid; osid = tr.msid; es = r + 2 * q + 1; oprice = 0;
+                    flags = OP_FILL | (buy ^ 1u) << 2;                                                    // KP:266-267
+                } else {
+                    oaid = raid; osid = rsid; es = r + 2 * q + 2; oprice = (uint32_t)jisub(rprice, tr.mprice);
+                    flags = OP_FILL | buy << 2;                                                           // KP:268-269
+                }
+            }
+        }
         // an account outside [0, A) (a maker that rested in a serial epoch, KME_FLAG_SERIAL_FALLBACK) is
         // in the exact Balances only: the serial replay takes the epoch's ledger (the op stays, keyed in
         // range, for the passes that still run before they see the fallback)
-        if (aid < 0 || aid >= S.A) { lfallback(S); aid = 0; }
+        if (oaid < 0 || oaid >= S.A) { lfallback(S); oaid = 0; }
+        const uint32_t p = base + j;
         // one 16-B store: sid, arrival number, size, price term | flags << 16 (LOp's layout)
-        reinterpret_cast<KG uint4*>(S.lrec)[o] =
-            make_uint4((uint32_t)(int32_t)sid, es, (uint32_t)size, (uint32_t)(uint16_t)(int16_t)price | flags << 16);
-        S.lk0[o] = lkey_of(S, aid, sid);   // (its value in the sort: o itself, R.val0 = nullptr)
-        S.lvw_meta[o] = 0;                  // (per sorted position, and positions cover the same range)
-        S.lxmark[o] = 0;
-        ++o;
-    };
-    if ((a == BUY || a == SELL) && out == a) {
-        const int64_t aid = io.aid[i], sid = io.sid[i];
-        const int32_t price = io.price[i], size = io.size[i];
-        const uint32_t t1 = io.trade_off[i + 1];
-        const uint32_t buy = a == BUY ? 1u : 0u;
-        // each trade is loaded one step ahead of its ops' stores (a load behind this thread's stores
-        // waits for them: vmcnt counts both, in order)
-        TradeRec nx{};
-        if (t0 < t1) nx = io.trades[t0];
-        put(aid, sid, i + 2 * t0, size, price, OP_CHECK | buy << 2);                                // KP:167-182
-        for (uint32_t q = t0; q < t1; ++q) {
-            const TradeRec tr = nx;
-            if (q + 1 < t1) nx = io.trades[q + 1];
-            put(tr.maid, tr.msid, i + 2 * q + 1, tr.size, 0, OP_FILL | (buy ^ 1u) << 2);             // KP:266-267
-            put(aid, sid, i + 2 * q + 2, tr.size, jisub(price, tr.mprice), OP_FILL | buy << 2);      // KP:268-269
-        }
-    } else if (a == CANCEL && out == CANCEL) {
-        const int4 v = S.vic[i];                      // the removed order: action << 8 | price, size, sid
-        const int64_t vsid = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
-        put(io.aid[i], vsid, i + 2 * t0, v.y, v.x & 0xFF, OP_CANCEL | ((v.x >> 8) == BUY ? 1u : 0u) << 2);   // KP:325-333
+        reinterpret_cast<KG uint4*>(S.lrec)[p] =
+            make_uint4((uint32_t)(int32_t)osid, es, osize, (uint32_t)(uint16_t)(int16_t)(int32_t)oprice | flags << 16);
+        S.lk0[p] = lkey_of(S, oaid, osid);   // (its value in the sort: p itself, R.val0 = nullptr)
+        S.lvw_meta[p] = 0;                    // (per sorted position, and positions cover the same range)
+        S.lxmark[p] = 0;
     }
 }
 
