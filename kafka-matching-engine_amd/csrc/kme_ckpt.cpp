@@ -156,15 +156,18 @@ struct CkptWriter::Impl {
     void submit() {
         if (fill == 0) return;
         if (cur_dev && hipEventRecord(ring->ev[cur], stream) != hipSuccess) set_err("device read");
-        jobs.push_back(Job{cur, base, fill, cur_dev, {}});
         if (!ring) {
+            jobs.push_back(Job{cur, base, fill, cur_dev, {}});
             if (!fail) (void)run(jobs.back());
         } else {
             if (th.empty()) {
                 const unsigned T = host_threads(12);
                 for (unsigned t = 0; t < T; ++t) th.emplace_back([this] { worker(); });
             }
+            // (under the lock: a worker indexes `jobs` under it, and push_back may move the deque's
+            // block map -- the elements themselves stay where they are)
             std::lock_guard<std::mutex> g(mu);
+            jobs.push_back(Job{cur, base, fill, cur_dev, {}});
             busy[cur] = true;
             queue.push_back(jobs.size() - 1);
             cv.notify_all();

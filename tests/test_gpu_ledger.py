@@ -108,6 +108,34 @@ def test_c3_shape_ledger_in_parallel(kme_mod, oracle_mod, monkeypatch):
     print("c3-shape epochs (chains repaired, serial):", stats[1:])
 
 
+def test_one_record_with_hundreds_of_fills(kme_mod, oracle_mod, monkeypatch):
+    """k_lgen spreads a wavefront's records' ops over its lanes: here one BUY sweeps 300 one-lot makers
+    of a few accounts (601 ops of one record, ten rounds of the wavefront's lanes, the other 63
+    records' single ops around it), in the middle of a wavefront and again at its last lane, with
+    cancels and rejects beside it -- the ledger is the oracle's after each epoch."""
+    n_sym, n_acc, E = 7, 16, 1024
+    rows, oid = [], 1
+    for rep in range(2):
+        for k in range(300):                                       # the makers (rest; KP:200-223)
+            rows.append((W.SELL, oid, 1 + k % 5, 3, 40 + k % 7, 1)); oid += 1
+        rows.append((W.CANCEL, oid - 3, 1 + (297 % 5), 3, 0, 0))   # one of them removed (KP:289-333)
+        rows.append((W.BUY, 10_000 + rep, 9, 3, 60, 300))          # the sweep: 1 + 2 x 299 ops
+        rows.append((W.CANCEL, 555_555, 9, 3, 0, 0))              # a reject (no such order)
+        while len(rows) % 64 != 63:                                  # next: a sweep at a wavefront's last lane
+            rows.append((W.BUY, oid, 2, 5, 10, 1)); oid += 1
+    for k in range(300):
+        rows.append((W.SELL, oid, 3, 6, 45, 1)); oid += 1
+    while len(rows) % 64 != 63:
+        rows.append((W.SELL, oid, 4, 5, 90, 1)); oid += 1
+    rows.append((W.BUY, 20_000, 8, 6, 45, 300))
+    body = W.Orders.from_rows(rows)
+    setup = W.funded_setup(n_acc, range(1, n_sym + 1))
+    stats, led = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, False, monkeypatch)
+    _, led_serial = _run(kme_mod, oracle_mod, setup, body, n_sym, n_acc, E, kme_mod.FLAG_EXACT_LEDGER, True,
+                         monkeypatch, check_every=False)
+    assert led == led_serial
+
+
 @pytest.mark.parametrize("kind", ["uniform", "cancel_replace"])
 def test_parallel_ledger_with_cancels_and_fallback_epochs(kme_mod, oracle_mod, monkeypatch, kind):
     """Refunds (postRemoveAdjustments, value writes when a position blocks part of the order) and
