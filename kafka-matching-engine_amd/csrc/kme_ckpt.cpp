@@ -202,6 +202,9 @@ CkptWriter::CkptWriter(const char* p, PinnedRing* ring, hipStream_t stream) : im
 }
 CkptWriter::~CkptWriter() {
     if (!im) return;
+    // (a writer that failed may leave device copies into a slot it never submitted: drained, so that
+    // the next writer's host bytes in that slot cannot be overwritten by them)
+    if (im->ring && hipStreamSynchronize(im->stream) != hipSuccess) (void)hipGetLastError();
     im->drain();                             // (nothing may still read a slot or write the file)
     if (im->fd >= 0) {
         ::close(im->fd);

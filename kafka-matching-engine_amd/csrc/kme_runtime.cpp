@@ -213,6 +213,8 @@ static bool ring_h2d(kme_engine* e, void* dst, const void* src, size_t bytes, co
     }
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);   // (the slots are reused by the next call)
     if (r != hipSuccess) {
+        (void)hipStreamSynchronize(e->stream);   // (copies still in flight read the slots: drained first)
+        (void)hipGetLastError();
         std::fprintf(stderr, "kme: device write of %s (%zu bytes at %p) failed: %s\n", what, bytes, dst, hipGetErrorString(r));
         return false;
     }
