@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -429,12 +430,16 @@ static void hist_append(kme_multi* m, const kme_orders* in, uint32_t n) {
         hist_lost(m, "past KME_MULTI_HISTORY records");
         return;
     }
-    m->h_action.insert(m->h_action.end(), in->action, in->action + n);
-    m->h_oid.insert(m->h_oid.end(), in->oid, in->oid + n);
-    m->h_aid.insert(m->h_aid.end(), in->aid, in->aid + n);
-    m->h_sid.insert(m->h_sid.end(), in->sid, in->sid + n);
-    m->h_price.insert(m->h_price.end(), in->price, in->price + n);
-    m->h_size.insert(m->h_size.end(), in->size, in->size + n);
+    try {   // (up to KME_MULTI_HISTORY records of 40 B on the host: no exception may leave the C ABI)
+        m->h_action.insert(m->h_action.end(), in->action, in->action + n);
+        m->h_oid.insert(m->h_oid.end(), in->oid, in->oid + n);
+        m->h_aid.insert(m->h_aid.end(), in->aid, in->aid + n);
+        m->h_sid.insert(m->h_sid.end(), in->sid, in->sid + n);
+        m->h_price.insert(m->h_price.end(), in->price, in->price + n);
+        m->h_size.insert(m->h_size.end(), in->size, in->size + n);
+    } catch (const std::bad_alloc&) {
+        hist_lost(m, "out of host memory");
+    }
 }
 static kme_orders hist_at(const kme_multi* m, uint64_t a) {
     return kme_orders{m->h_action.data() + a, m->h_oid.data() + a, m->h_aid.data() + a, m->h_sid.data() + a,
@@ -807,8 +812,14 @@ static bool hist_load(kme_multi* m, const std::string& base, uint64_t records, u
     FILE* fp = std::fopen(f.c_str(), "rb");
     if (!fp) return false;
     const size_t n = (size_t)records;
-    m->h_action.resize(n); m->h_price.resize(n); m->h_size.resize(n);
-    m->h_oid.resize(n); m->h_aid.resize(n); m->h_sid.resize(n);
+    try {
+        m->h_action.resize(n); m->h_price.resize(n); m->h_size.resize(n);
+        m->h_oid.resize(n); m->h_aid.resize(n); m->h_sid.resize(n);
+    } catch (const std::bad_alloc&) {
+        std::fclose(fp);
+        hist_clear(m);
+        return false;
+    }
     std::vector<HistRec> buf(std::min<size_t>(n, 1u << 16));
     kme::Digest dg;
     bool ok = true;
