@@ -702,6 +702,14 @@ __global__ void k_route(DevState S, EpochIO io, int funded) {
 constexpr int RADIX_DIGITS = 1 << RADIX_BITS;
 constexpr int RADIX_PER_T = RADIX_DIGITS / 256;   // digits per thread of a 256-thread block
 
+// c ? b : a for two fields of a kernel argument, as arithmetic: a select between two of its fields was
+// folded into a load at a computed offset, which keeps a private copy of the whole argument (136 B
+// per lane of scratch, written at every scatter's start and read back on its critical path)
+template <typename P>
+KDEV P pick(bool c, P a, P b) {
+    const uint64_t x = (uint64_t)(uintptr_t)a, y = (uint64_t)(uintptr_t)b;
+    return (P)(uintptr_t)(x ^ ((x ^ y) & (0ull - (uint64_t)c)));
+}
 KDEV uint32_t radix_n(const RadixIO& R) {
     if (!R.n_dev) return R.n;
     const uint32_t d = (uint32_t)*R.n_dev;
@@ -721,8 +729,9 @@ KDEV void radix_load(const RadixIO& R, int pass, int src, uint32_t n, uint32_t f
     }
     // (selects, not an index into the argument's arrays: a dynamic index reads them through a vector
     // load whose wait then lands before every later memory operation)
-    const KG uint32_t* kp = pass == 0 ? reinterpret_cast<const KG uint32_t*>(R.key0) : (src ? R.keys[1] : R.keys[0]);
-    const KG uint32_t* vp = pass == 0 ? R.val0 : (src ? R.vals[1] : R.vals[0]);
+    const KG uint32_t* kp = pick<const KG uint32_t*>(pass == 0, pick<const KG uint32_t*>(src != 0, R.keys0, R.keys1),
+                                                     reinterpret_cast<const KG uint32_t*>(R.key0));
+    const KG uint32_t* vp = pick<const KG uint32_t*>(pass == 0, pick<const KG uint32_t*>(src != 0, R.vals0, R.vals1), R.val0);
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
         const uint32_t k = first + j * stride;
@@ -803,8 +812,18 @@ __global__ void __launch_bounds__(256) k_radix_tcnt(RadixIO R) {
 // waits for a later one).  t0 / t1: this tile's counts of digits 2t, 2t + 1; returns their offsets.
 KDEV uint32_t block_excl_scan_256(uint32_t v, uint32_t* wsum, uint32_t& total);
 constexpr int LB_BATCH = 32;   // (tiles read per round trip)
+// The first LB_BATCH tiles' rows of tcnt (thread t's two digits), loaded by the caller before its
+// ranking so that their latency overlaps it (the rows are the previous kernel's: nothing to wait for).
+KDEV void radix_lb_rows(const RadixIO& R, int pass, uint32_t ntiles, uint2* v) {
+    const KG uint32_t* tc = R.tcnt + (size_t)pass * gridDim.x * RADIX_DIGITS;
+#pragma unroll
+    for (int b = 0; b < LB_BATCH; ++b) {
+        const uint32_t q = (uint32_t)b < ntiles ? (uint32_t)b : 0;
+        v[b] = *reinterpret_cast<const KG uint2*>(&tc[(size_t)q * RADIX_DIGITS + 2 * threadIdx.x]);
+    }
+}
 KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t ntiles, uint32_t t0, uint32_t t1,
-                           uint32_t* wsum, uint32_t& g0, uint32_t& g1) {
+                           uint32_t* wsum, const uint2* first, uint32_t& g0, uint32_t& g1) {
     const int t = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     KG unsigned long long* lb = R.lb;   // per tile 256 words: thread t's two digit counts (12 bits each) | stamp << 32
@@ -812,10 +831,15 @@ KDEV void radix_lb_offsets(const RadixIO& R, int pass, uint32_t stamp, uint32_t 
     if (pass > 0)   // (pass 0's tiles are the unpermuted keys': their counts are tcnt's row 0 already)
         __hip_atomic_store(&lb[(size_t)tile * 256 + t], st | (t1 << 16) | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the digits' totals over the sort's tiles, exclusive over the digits (pass 0: and the earlier
-    // tiles' counts, from the same rows)
+    // tiles' counts, from the same rows; the first LB_BATCH rows are the caller's, `first`)
     const KG uint32_t* tc = R.tcnt + (size_t)pass * gridDim.x * RADIX_DIGITS;
     uint32_t T0 = 0, T1 = 0, P0 = 0, P1 = 0;
-    for (uint32_t q0 = 0; q0 < ntiles; q0 += LB_BATCH) {
+#pragma unroll
+    for (int b = 0; b < LB_BATCH; ++b) {
+        if ((uint32_t)b < ntiles) { T0 += first[b].x; T1 += first[b].y; }
+        if (pass == 0 && (uint32_t)b < tile) { P0 += first[b].x; P1 += first[b].y; }
+    }
+    for (uint32_t q0 = LB_BATCH; q0 < ntiles; q0 += LB_BATCH) {
         uint2 v[LB_BATCH];
 #pragma unroll
         for (int b = 0; b < LB_BATCH; ++b) {
@@ -878,6 +902,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     constexpr int WCH = TILE / 4;                // elements per wavefront
     uint32_t keys[RJ], vals[RJ], wr[RJ];
     radix_load<RJ, true>(R, pass, src, n, base + w * WCH + lane, 64, keys, vals);
+    uint2 rows[LB ? LB_BATCH : 1];
+    if constexpr (LB) radix_lb_rows(R, pass, (n + TILE - 1) / TILE, rows);
 #pragma unroll
     for (int q = 0; q < RADIX_DIGITS / 64; ++q) wh[w][lane + 64 * q] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -914,7 +940,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
         uint32_t r0 = ex, r1 = ex + t0;
         if constexpr (LB) {
             uint32_t g0, g1;
-            radix_lb_offsets(R, pass, stamp, (n + TILE - 1) / TILE, t0, t1, wsum, g0, g1);
+            radix_lb_offsets(R, pass, stamp, (n + TILE - 1) / TILE, t0, t1, wsum, rows, g0, g1);
             gdelta[2 * t] = g0 - r0;
             gdelta[2 * t + 1] = g1 - r1;
         } else {
@@ -936,8 +962,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(RadixIO R, int pass, int 
     __syncthreads();
     if (base >= n) return;
     const uint32_t cnt = n - base < (uint32_t)TILE ? n - base : (uint32_t)TILE;
-    KG uint32_t* okeys = dst ? R.keys[1] : R.keys[0];
-    KG uint32_t* ovals = dst ? R.vals[1] : R.vals[0];
+    KG uint32_t* okeys = pick(dst != 0, R.keys0, R.keys1);
+    KG uint32_t* ovals = pick(dst != 0, R.vals0, R.vals1);
     const bool last = pass == R.passes - 1 && R.rank;
     const bool pay = pass == R.passes - 1 && R.pay_src;
 #pragma unroll
@@ -4393,8 +4419,8 @@ int launch_partition(const DevState& S, const EpochIO& io, hipStream_t st, int l
     RadixIO R{};
     R.key0 = S.route_grp;
     R.val0 = nullptr;
-    R.keys[0] = S.rkeys[0]; R.keys[1] = S.rkeys[1];
-    R.vals[0] = S.rvals[0]; R.vals[1] = S.rvals[1];
+    R.keys0 = S.rkeys[0]; R.keys1 = S.rkeys[1];
+    R.vals0 = S.rvals[0]; R.vals1 = S.rvals[1];
     R.ghist = S.ghist;
     R.rank = S.rank;
     R.none = (uint32_t)S.G;

@@ -28,8 +28,14 @@ constexpr int kOsLanesMaxLight = 512;  // light_max up to which light groups' OU
 struct RadixIO {
     const KG int32_t* key0;
     const KG uint32_t* val0;
-    KG uint32_t* keys[2];
-    KG uint32_t* vals[2];
+    // the ping-pong buffers as four named fields, not arrays: a pass selects them by its parity, and
+    // a select between two elements of an array member was folded into a dynamic index into the
+    // kernel argument -- which put the whole struct in scratch memory (136 B per lane, stored at
+    // every scatter's start and read back on its critical path)
+    KG uint32_t* keys0;
+    KG uint32_t* keys1;
+    KG uint32_t* vals0;
+    KG uint32_t* vals1;
     KG uint32_t* ghist;              // RADIX_DIGITS x tiles + the scan's scratch
     KG int32_t* rank;                // the last pass: rank[value] = position (nullptr: none)
     const KG uint4* pay_src;         // the last pass: pay_dst[position] = pay_src[value] (nullptr: none)

@@ -886,8 +886,8 @@ void launch_ledger_parallel(const DevState& S, const EpochIO& io, uint32_t max_t
     RadixIO R{};
     R.key0 = reinterpret_cast<const KG int32_t*>(S.lk0);
     R.val0 = nullptr;
-    R.keys[0] = S.lkey[0]; R.keys[1] = S.lkey[1];
-    R.vals[0] = S.lval[0]; R.vals[1] = S.lval[1];
+    R.keys0 = S.lkey[0]; R.keys1 = S.lkey[1];
+    R.vals0 = S.lval[0]; R.vals1 = S.lval[1];
     R.ghist = S.lghist;
     R.rank = nullptr;
     R.pay_src = reinterpret_cast<const KG uint4*>(S.lrec);   // the ops themselves, into sorted order
